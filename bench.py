@@ -1,0 +1,224 @@
+#!/usr/bin/env python3
+"""Benchmark: OFDM LS + MRC receiver throughput on MI355X.
+
+Workload (BASELINE.json metric "OFDM symbols/s (LS+MRC) at 1024 subcarriers x
+64 ant"; configs[3] "8xMI355X: 1024 subcarriers, 64 antennas, 1M symbols
+sharded by symbol index (no RCCL), per-GPU hipStreams"): each GPU holds
+`--frames` frames (default 1250) of S = 101 symbols (1 pilot + 100 data,
+lenOfBuffer of ShMemSymBuff_gpu.hpp:74) x R = 64 antennas x C = 1024
+time-domain IQ samples, synthetic, resident in HBM (66 GB per GPU).  One step =
+ofdm_frame_estimate (pilot FFT + LS) + ofdm_frame_combine (FFT + MRC +
+normalise + rotate) over the whole batch: 125,000 data symbols per GPU, 1M at
+8 GPUs (weak scaling, frame-sharded, no collective on the data path).
+
+value = data symbols demodulated per second, whole job (all ranks).
+roofline: dominant kernel (MRC), algorithmic bytes per data symbol
+  B_sym = R*C*8 (IQ read once) + K*8 (output written once)  
+  divided by its HIP-event-measured average launch time, vs 8 TB/s HBM3E.
+cpu_baseline: the oracle's C restatement of cpuLS.hpp (oracle/, FFT in
+  float64) timed on this host, rank 0 at N=1, on a bounded sample of frames of
+  the same shape, OpenMP over frames.
+
+python bench.py [--gpus N] [--steps K] [--warmup W]
+torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "gpu-accel-ofdm-ls-mrc_amd"))
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--frames", type=int, default=1250, help="frames per GPU")
+    ap.add_argument("--S", type=int, default=101)
+    ap.add_argument("--R", type=int, default=64)
+    ap.add_argument("--C", type=int, default=1024)
+    ap.add_argument("--prefix", type=int, default=0)
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--noise", type=float, default=0.01)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="target wall time of the CPU-baseline sample")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
+                    help="PMC traffic summary (profiles/) for roofline.traffic")
+    return ap.parse_args()
+
+
+def cpu_baseline(args, X, ofdm, torch, dev):
+    """Oracle (C restatement of cpuLS.hpp) on the host cores of this box."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_bindings import Oracle
+    o = Oracle()
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    threads = max(1, min(16, cores))  # the box's CPU share is 16
+    Xh = X.cpu().numpy()
+
+    def sample(nf):
+        iq = ofdm.synth_frames(nf, args.S, args.R, args.C, X, prefix=args.prefix,
+                               seed=args.seed + 7, noise_std=args.noise)
+        torch.cuda.synchronize()
+        return iq.cpu().numpy()
+
+    iq1 = sample(threads)
+    t0 = time.perf_counter()
+    o.frames_demod(iq1, Xh, args.prefix, nthreads=threads)
+    t1 = time.perf_counter() - t0
+    nf = max(threads, int(args.cpu_seconds / max(t1, 1e-3) * threads) // threads * threads)
+    nf = min(nf, 64 * threads)
+    iq = sample(nf) if nf != threads else iq1
+    t0 = time.perf_counter()
+    o.frames_demod(iq, Xh, args.prefix, nthreads=threads)
+    dt = time.perf_counter() - t0
+    syms = nf * (args.S - 1)
+    return {"value": syms / dt, "unit": "symbols/s", "cores": threads, "kind": "port",
+            "sample": f"{nf} frames x {args.S} symbols (R={args.R}, C={args.C}, prefix="
+                      f"{args.prefix}), FFT+LS+MRC+rotate, OpenMP over frames, "
+                      f"{dt:.1f} s wall", "seconds": dt}
+
+
+def pmc_traffic(path, cfg):
+    try:
+        with open(path) as fp:
+            d = json.load(fp)
+    except (OSError, ValueError):
+        return None, None
+    if any(d.get("config", {}).get(k) != cfg[k] for k in ("R", "C", "S", "frames_per_gpu", "prefix")):
+        return None, None
+    return d.get("mrc_hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    import ofdm_lsmrc as ofdm
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    F, S, R, C, prefix = args.frames, args.S, args.R, args.C, args.prefix
+    K = C - 1
+    Q = F * (S - 1)  # data symbols per GPU per step
+    import numpy as np
+    rng = np.random.default_rng(args.seed)
+    a = np.float32(0.70710678)
+    X = torch.from_numpy((rng.choice([-a, a], K) + 1j * rng.choice([-a, a], K))
+                         .astype(np.complex64)).to(dev)
+
+    t = time.perf_counter()
+    iq = ofdm.synth_frames(F, S, R, C, X, prefix=prefix, seed=args.seed, frame0=rank * F,
+                           noise_std=args.noise)
+    ws = ofdm.workspace(F, S, R, C, dev)
+    out = ofdm.c64((F, S - 1, K), dev)
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] synthesised {iq.numel() * 8 / 1e9:.1f} GB in {time.perf_counter() - t:.1f} s")
+
+    stream = torch.cuda.current_stream()
+
+    def step(evs=None):
+        if evs:
+            evs[0].record(stream)
+        ofdm.frame_estimate(iq, X, prefix, ws, stream)
+        if evs:
+            evs[1].record(stream)
+        ofdm.frame_combine(iq, prefix, ws, out, stream)
+        if evs:
+            evs[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    errs = int(ofdm.count_symbol_errors(out, S, seed=args.seed, frame0=rank * F).item())
+
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(events[i])
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    barrier()
+
+    ls_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
+    mrc_ms = sum(e[1].elapsed_time(e[2]) for e in events) / args.steps
+    stats = torch.tensor([elapsed, float(errs)], dtype=torch.float64, device=dev)
+    if world > 1:
+        mx = stats.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        tot = stats.clone()
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        elapsed, errs = float(mx[0]), int(tot[1])
+
+    cfg = {"workload": f"OFDM uplink LS+MRC, time-domain IQ in HBM, {F} frames x {S} symbols "
+                       f"(1 pilot + {S - 1} data) x {R} antennas x {C} subcarriers per GPU",
+           "R": R, "C": C, "S": S, "prefix": prefix, "frames_per_gpu": F,
+           "data_symbols_per_gpu": Q, "global_data_symbols": Q * world,
+           "parallelism": f"frame-sharded x{world}, no collective"}
+    b_sym = R * C * 8 + K * 8
+    achieved = Q * b_sym / (mrc_ms * 1e-3) / 1e9
+    traffic, tsrc = pmc_traffic(args.pmc, cfg)
+    step_bytes = F * S * R * C * 8 + Q * K * 8
+    result = {
+        "metric": "OFDM symbols/s (LS+MRC) at 1024 subcarriers x 64 ant; achieved HBM GB/s vs peak",
+        "value": Q * world / (elapsed / args.steps),
+        "unit": "symbols/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (device-generated Rayleigh channel, QPSK, sigma=%g)" % args.noise,
+        "config": cfg,
+        "roofline": {"kernel": "k_mrc_td1024 (FFT+MRC+normalise+rotate)", "bound": "hbm",
+                     "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+                     "traffic_source": tsrc,
+                     "bytes_per_launch": Q * b_sym, "avg_launch_ms": mrc_ms},
+        "stages_ms": {"estimate_ls_td1024": ls_ms, "combine_mrc_td1024": mrc_ms},
+        "step_algorithmic_GBps": step_bytes / (elapsed / args.steps) / 1e9,
+        "check": {"qpsk_symbol_errors": errs},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        result["cpu_baseline"] = cpu_baseline(args, X, ofdm, torch, dev)
+        result["speedup_vs_cpu_baseline"] = result["value"] / result["cpu_baseline"]["value"]
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,366 @@
+// capi.cpp -- the C ABI (include/ofdm_lsmrc.h): argument validation, error
+// reporting, workspace carving and kernel dispatch.  Compiled by hipcc as HIP.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "../../include/ofdm_lsmrc.h"
+#include "launch.hpp"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+int hip_check(hipError_t e, const char *what) {
+    if (e == hipSuccess) return OFDM_OK;
+    return fail(OFDM_E_HIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+bool pow2_c(int C) { return C >= 4 && C <= 4096 && (C & (C - 1)) == 0; }
+
+inline hipStream_t hs(ofdm_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+inline const float2 *F2(const ofdm_cf32 *p) { return reinterpret_cast<const float2 *>(p); }
+inline float2 *F2(ofdm_cf32 *p) { return reinterpret_cast<float2 *>(p); }
+inline bool aligned(const void *p, size_t a) { return (reinterpret_cast<uintptr_t>(p) % a) == 0; }
+
+size_t up256(size_t x) { return (x + 255) & ~size_t(255); }
+
+// fused one-pass kernels exist for these FFT sizes
+bool fused_c(int C) { return C == 1024; }
+
+long long staging_frames(long long nframes, int S, int R, int C) {
+    const long long per = (long long)S * R * C * (long long)sizeof(float2);
+    long long n = (256ll << 20) / (per > 0 ? per : 1);
+    if (n < 1) n = 1;
+    return n < nframes ? n : nframes;
+}
+
+struct Workspace {
+    float2 *Hc;       // [F][R][C] bin layout
+    float *P;         // [F][C]   bin layout
+    float2 *staging;  // [chunk][S][R][C] (non-fused C only)
+    long long chunk;
+};
+
+size_t ws_bytes(long long F, int S, int R, int C, bool need_staging) {
+    size_t b = up256((size_t)F * R * C * sizeof(float2)) + up256((size_t)F * C * sizeof(float));
+    if (need_staging) b += up256((size_t)staging_frames(F, S, R, C) * S * R * C * sizeof(float2));
+    return b;
+}
+
+int carve(void *d_ws, size_t bytes, long long F, int S, int R, int C, bool need_staging,
+          Workspace &w) {
+    const size_t need = ws_bytes(F, S, R, C, need_staging);
+    if (!d_ws || bytes < need)
+        return fail(OFDM_E_ARG, "workspace too small: %zu bytes given, %zu needed", bytes, need);
+    if (!aligned(d_ws, 256)) return fail(OFDM_E_ARG, "workspace must be 256-byte aligned");
+    char *p = static_cast<char *>(d_ws);
+    w.Hc = reinterpret_cast<float2 *>(p);
+    p += up256((size_t)F * R * C * sizeof(float2));
+    w.P = reinterpret_cast<float *>(p);
+    p += up256((size_t)F * C * sizeof(float));
+    w.staging = need_staging ? reinterpret_cast<float2 *>(p) : nullptr;
+    w.chunk = need_staging ? staging_frames(F, S, R, C) : F;
+    return OFDM_OK;
+}
+
+int check_frame_args(const void *in, long long F, int S, int R, int C, int prefix,
+                     const void *out, const char *fn) {
+    if (!in || !out) return fail(OFDM_E_ARG, "%s: null pointer", fn);
+    if (F < 0) return fail(OFDM_E_ARG, "%s: nframes < 0", fn);
+    if (S < 2) return fail(OFDM_E_ARG, "%s: S=%d, a frame needs a pilot and >= 1 data symbol", fn, S);
+    if (R < 1) return fail(OFDM_E_ARG, "%s: R=%d < 1", fn, R);
+    if (!pow2_c(C)) return fail(OFDM_E_UNSUPPORTED, "%s: C=%d not a power of two in [4, 4096]", fn, C);
+    if (prefix < 0 || prefix > C) return fail(OFDM_E_ARG, "%s: prefix=%d out of [0, C]", fn, prefix);
+    if (!aligned(in, 16)) return fail(OFDM_E_ARG, "%s: input must be 16-byte aligned", fn);
+    return OFDM_OK;
+}
+
+// Generic (non-fused) time-domain frames: FFT rows of each chunk into the
+// staging buffer, then the frequency-domain LS / MRC kernels.
+// mode: 0 = full demod, 1 = MRC numerator only, 2 = LS only,
+//       3 = full demod against an estimate already in the workspace
+int td_staged(const float2 *iq, long long F, int S, int R, int C, int prefix, const float2 *X,
+              const Workspace &w, float2 *out, int mode, hipStream_t s) {
+    const int K = C - 1;
+    const long long frame_in = (long long)S * R * (C + prefix);
+    const long long frame_st = (long long)S * R * C;
+    for (long long f0 = 0; f0 < F; f0 += w.chunk) {
+        const long long n = F - f0 < w.chunk ? F - f0 : w.chunk;
+        const long long rows = mode == 2 ? 0 : n * S * R;
+        hipError_t e;
+        if (mode == 2) {  // only the pilot rows are needed
+            for (long long f = 0; f < n; ++f) {
+                e = ofdm::launch_fft_rows(iq + (f0 + f) * frame_in, C + prefix, prefix,
+                                          w.staging + f * frame_st, C, 0, R, C, false, 1.f, s);
+                if (e != hipSuccess) return hip_check(e, "fft (pilot rows)");
+            }
+        } else {
+            e = ofdm::launch_fft_rows(iq + f0 * frame_in, C + prefix, prefix, w.staging, C, 0, rows,
+                                      C, false, 1.f, s);
+            if (e != hipSuccess) return hip_check(e, "fft (frame rows)");
+        }
+        if (mode == 0 || mode == 2) {
+            e = ofdm::launch_ls_freq(w.staging, frame_st, n, R, C, X, w.Hc + f0 * R * C,
+                                     (long long)R * C, C, 1, w.P + f0 * C, C, 1, s);
+            if (e != hipSuccess) return hip_check(e, "ls_freq");
+        }
+        if (mode != 2) {
+            e = ofdm::launch_mrc_freq(w.staging + (long long)R * C, frame_st, (long long)R * C, n,
+                                      S - 1, R, C, w.Hc + f0 * R * C, (long long)R * C, C, 0,
+                                      w.P + f0 * C, C, 1, out + f0 * (S - 1) * K,
+                                      mode == 1 ? 1 : 0, s);
+            if (e != hipSuccess) return hip_check(e, "mrc_freq");
+        }
+    }
+    return OFDM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ofdm_version(void) { return OFDM_LSMRC_VERSION; }
+
+const char *ofdm_last_error(void) { return g_err.c_str(); }
+
+int ofdm_pilot_rotate(const ofdm_cf32 *raw, int K, ofdm_cf32 *X) {
+    if (!raw || !X || K < 1) return fail(OFDM_E_ARG, "ofdm_pilot_rotate: bad arguments");
+    // X[j] = raw[(j + (K+1)/2) mod K] for odd K; literal memmove semantics of
+    // matrix_readX (cpuLS.hpp:105-112) for any K.
+    const int nt = (K - 1) / 2;
+    ofdm_cf32 *tmp = new ofdm_cf32[nt > 0 ? nt : 1];
+    if (X != raw) std::memmove(X, raw, sizeof(ofdm_cf32) * K);
+    std::memmove(tmp, &X[(K + 1) / 2], sizeof(ofdm_cf32) * nt);
+    std::memmove(&X[(K - 1) / 2], X, sizeof(ofdm_cf32) * ((K + 1) / 2));
+    std::memmove(X, tmp, sizeof(ofdm_cf32) * nt);
+    delete[] tmp;
+    return OFDM_OK;
+}
+
+int ofdm_read_pilots(const char *path, int K, float fill, ofdm_cf32 *X) {
+    if (!X || K < 1) return fail(OFDM_E_ARG, "ofdm_read_pilots: bad arguments");
+    FILE *fp = path ? std::fopen(path, "rb") : nullptr;
+    if (!fp) {
+        for (int j = 0; j < K; ++j) X[j] = ofdm_cf32{fill, fill};
+        fail(1, "ofdm_read_pilots: cannot open %s, filled %g+%gi", path ? path : "(null)", fill, fill);
+        return 1;
+    }
+    // the reference reads K values without checking the count (cpuLS.hpp:93);
+    // a short file leaves the tail as it was -- here it is zero-filled.
+    std::memset(X, 0, sizeof(ofdm_cf32) * K);
+    size_t got = std::fread(X, sizeof(ofdm_cf32), (size_t)K, fp);
+    std::fclose(fp);
+    (void)got;
+    return ofdm_pilot_rotate(X, K, X);
+}
+
+int ofdm_fft_rows(const ofdm_cf32 *d_in, ofdm_cf32 *d_out, long long nrows, int C, int inverse,
+                  ofdm_stream_t stream) {
+    if (!d_in || !d_out || nrows < 0) return fail(OFDM_E_ARG, "ofdm_fft_rows: bad arguments");
+    if (!pow2_c(C)) return fail(OFDM_E_UNSUPPORTED, "ofdm_fft_rows: C=%d not a power of two in [4, 4096]", C);
+    return hip_check(ofdm::launch_fft_rows(F2(d_in), C, 0, F2(d_out), C, 0, nrows, C, inverse != 0,
+                                           1.f, hs(stream)),
+                     "ofdm_fft_rows");
+}
+
+int ofdm_ls_estimate(const ofdm_cf32 *d_Y, const ofdm_cf32 *d_X, int R, int C, ofdm_cf32 *d_Hconj,
+                     float *d_Hsqrd, ofdm_stream_t stream) {
+    if (!d_Y || !d_X || !d_Hconj || !d_Hsqrd || R < 1)
+        return fail(OFDM_E_ARG, "ofdm_ls_estimate: bad arguments");
+    if (!pow2_c(C)) return fail(OFDM_E_UNSUPPORTED, "ofdm_ls_estimate: C=%d unsupported", C);
+    const int K = C - 1;
+    return hip_check(ofdm::launch_ls_freq(F2(d_Y), 0, 1, R, C, F2(d_X), F2(d_Hconj), 0, K, 0, d_Hsqrd,
+                                          0, 0, hs(stream)),
+                     "ofdm_ls_estimate");
+}
+
+static int mrc_common(const ofdm_cf32 *d_Y, long long nsyms, const ofdm_cf32 *d_Hconj,
+                      const float *d_Hsqrd, int R, int C, ofdm_cf32 *d_out, int mode,
+                      ofdm_stream_t stream, const char *fn) {
+    if (!d_Y || !d_Hconj || !d_out || (mode == 0 && !d_Hsqrd) || R < 1 || nsyms < 0)
+        return fail(OFDM_E_ARG, "%s: bad arguments", fn);
+    if (!pow2_c(C)) return fail(OFDM_E_UNSUPPORTED, "%s: C=%d unsupported", fn, C);
+    if (!aligned(d_Y, 16)) return fail(OFDM_E_ARG, "%s: d_Y must be 16-byte aligned", fn);
+    const int K = C - 1;
+    // all symbols share one estimate: one "frame" holding nsyms data symbols
+    return hip_check(ofdm::launch_mrc_freq(F2(d_Y), 0, (long long)R * C, 1, (int)nsyms, R, C,
+                                           F2(d_Hconj), 0, K, 0, d_Hsqrd, 0, 0, F2(d_out), mode,
+                                           hs(stream)),
+                     fn);
+}
+
+int ofdm_mrc_demod(const ofdm_cf32 *d_Y, long long nsyms, const ofdm_cf32 *d_Hconj,
+                   const float *d_Hsqrd, int R, int C, ofdm_cf32 *d_out, ofdm_stream_t stream) {
+    if (nsyms > 0x7fffffffll) return fail(OFDM_E_ARG, "ofdm_mrc_demod: nsyms too large");
+    return mrc_common(d_Y, nsyms, d_Hconj, d_Hsqrd, R, C, d_out, 0, stream, "ofdm_mrc_demod");
+}
+
+int ofdm_mrc_numerator(const ofdm_cf32 *d_Y, long long nsyms, const ofdm_cf32 *d_Hconj, int R,
+                       int C, ofdm_cf32 *d_num, ofdm_stream_t stream) {
+    if (nsyms > 0x7fffffffll) return fail(OFDM_E_ARG, "ofdm_mrc_numerator: nsyms too large");
+    return mrc_common(d_Y, nsyms, d_Hconj, nullptr, R, C, d_num, 1, stream, "ofdm_mrc_numerator");
+}
+
+int ofdm_mrc_finalize(const ofdm_cf32 *d_num, long long e0, long long count, int nsym, int K,
+                      const float *d_Hsqrd, ofdm_cf32 *d_out, ofdm_stream_t stream) {
+    if (!d_num || !d_Hsqrd || !d_out || e0 < 0 || count < 0 || nsym < 1 || K < 1)
+        return fail(OFDM_E_ARG, "ofdm_mrc_finalize: bad arguments");
+    return hip_check(ofdm::launch_mrc_finalize(F2(d_num), e0, count, nsym, K, d_Hsqrd, F2(d_out),
+                                               hs(stream)),
+                     "ofdm_mrc_finalize");
+}
+
+size_t ofdm_frame_workspace_bytes(long long nframes, int S, int R, int C) {
+    if (nframes < 0 || S < 2 || R < 1 || !pow2_c(C)) return 0;
+    return ws_bytes(nframes, S, R, C, !fused_c(C));
+}
+
+int ofdm_frame_estimate(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, int prefix,
+                        const ofdm_cf32 *d_X, void *d_ws, size_t ws_bytes_, ofdm_stream_t stream) {
+    int rc = check_frame_args(d_iq, nframes, S, R, C, prefix, d_ws, "ofdm_frame_estimate");
+    if (rc) return rc;
+    if (!d_X) return fail(OFDM_E_ARG, "ofdm_frame_estimate: null pilots");
+    if (nframes == 0) return OFDM_OK;
+    Workspace w;
+    if ((rc = carve(d_ws, ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
+    hipStream_t s = hs(stream);
+    if (fused_c(C))
+        return hip_check(ofdm::launch_ls_td1024(F2(d_iq), nframes, S, R, prefix, F2(d_X), w.Hc, w.P, 0, s),
+                         "ls_td1024");
+    return td_staged(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w, nullptr, 2, s);
+}
+
+int ofdm_frame_combine(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, int prefix,
+                       void *d_ws, size_t ws_bytes_, ofdm_cf32 *d_out, ofdm_stream_t stream) {
+    int rc = check_frame_args(d_iq, nframes, S, R, C, prefix, d_out, "ofdm_frame_combine");
+    if (rc) return rc;
+    if (nframes == 0) return OFDM_OK;
+    Workspace w;
+    if ((rc = carve(d_ws, ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
+    hipStream_t s = hs(stream);
+    if (fused_c(C))
+        return hip_check(ofdm::launch_mrc_td1024(F2(d_iq), nframes, S, R, prefix, w.Hc, w.P,
+                                                 F2(d_out), 0, s),
+                         "mrc_td1024");
+    // staged path: the FFT of every chunk is redone here (estimate kept only Hc/P)
+    return td_staged(F2(d_iq), nframes, S, R, C, prefix, nullptr, w, F2(d_out), 3, s);
+}
+
+int ofdm_frame_demod(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, int prefix,
+                     const ofdm_cf32 *d_X, void *d_ws, size_t ws_bytes_, ofdm_cf32 *d_out,
+                     ofdm_stream_t stream) {
+    int rc = check_frame_args(d_iq, nframes, S, R, C, prefix, d_out, "ofdm_frame_demod");
+    if (rc) return rc;
+    if (!d_X) return fail(OFDM_E_ARG, "ofdm_frame_demod: null pilots");
+    if (nframes == 0) return OFDM_OK;
+    Workspace w;
+    if ((rc = carve(d_ws, ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
+    hipStream_t s = hs(stream);
+    if (fused_c(C)) {
+        rc = hip_check(ofdm::launch_ls_td1024(F2(d_iq), nframes, S, R, prefix, F2(d_X), w.Hc, w.P, 0, s),
+                       "ls_td1024");
+        if (rc) return rc;
+        return hip_check(ofdm::launch_mrc_td1024(F2(d_iq), nframes, S, R, prefix, w.Hc, w.P,
+                                                 F2(d_out), 0, s),
+                         "mrc_td1024");
+    }
+    return td_staged(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w, F2(d_out), 0, s);
+}
+
+int ofdm_frame_demod_freq(const ofdm_cf32 *d_Y, long long nframes, int S, int R, int C,
+                          const ofdm_cf32 *d_X, void *d_ws, size_t ws_bytes_, ofdm_cf32 *d_out,
+                          ofdm_stream_t stream) {
+    int rc = check_frame_args(d_Y, nframes, S, R, C, 0, d_out, "ofdm_frame_demod_freq");
+    if (rc) return rc;
+    if (!d_X) return fail(OFDM_E_ARG, "ofdm_frame_demod_freq: null pilots");
+    if (nframes == 0) return OFDM_OK;
+    Workspace w;
+    if ((rc = carve(d_ws, ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
+    hipStream_t s = hs(stream);
+    const long long fst = (long long)S * R * C;
+    rc = hip_check(ofdm::launch_ls_freq(F2(d_Y), fst, nframes, R, C, F2(d_X), w.Hc, (long long)R * C, C,
+                                        1, w.P, C, 1, s),
+                   "ls_freq");
+    if (rc) return rc;
+    return hip_check(ofdm::launch_mrc_freq(F2(d_Y) + (long long)R * C, fst, (long long)R * C, nframes,
+                                           S - 1, R, C, w.Hc, (long long)R * C, C, 0, w.P, C, 1,
+                                           F2(d_out), 0, s),
+                     "mrc_freq");
+}
+
+int ofdm_frame_ls_partial(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, int prefix,
+                          const ofdm_cf32 *d_X, void *d_ws, size_t ws_bytes_, float *d_P,
+                          ofdm_stream_t stream) {
+    int rc = check_frame_args(d_iq, nframes, S, R, C, prefix, d_P, "ofdm_frame_ls_partial");
+    if (rc) return rc;
+    if (!d_X) return fail(OFDM_E_ARG, "ofdm_frame_ls_partial: null pilots");
+    if (nframes == 0) return OFDM_OK;
+    Workspace w;
+    if ((rc = carve(d_ws, ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
+    hipStream_t s = hs(stream);
+    if (fused_c(C))
+        rc = hip_check(ofdm::launch_ls_td1024(F2(d_iq), nframes, S, R, prefix, F2(d_X), w.Hc, w.P, 1, s),
+                       "ls_td1024");
+    else
+        rc = td_staged(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w, nullptr, 2, s);
+    if (rc) return rc;
+    // bins 1..C-1 of the bin-layout P -> [F][K]
+    const int K = C - 1;
+    return hip_check(hipMemcpy2DAsync(d_P, K * sizeof(float), w.P + 1, C * sizeof(float),
+                                      K * sizeof(float), (size_t)nframes, hipMemcpyDeviceToDevice, s),
+                     "copy partial P");
+}
+
+int ofdm_frame_mrc_partial(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int C,
+                           int prefix, void *d_ws, size_t ws_bytes_, ofdm_cf32 *d_num,
+                           ofdm_stream_t stream) {
+    int rc = check_frame_args(d_iq, nframes, S, R, C, prefix, d_num, "ofdm_frame_mrc_partial");
+    if (rc) return rc;
+    if (nframes == 0) return OFDM_OK;
+    Workspace w;
+    if ((rc = carve(d_ws, ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
+    hipStream_t s = hs(stream);
+    if (fused_c(C))
+        return hip_check(ofdm::launch_mrc_td1024(F2(d_iq), nframes, S, R, prefix, w.Hc, w.P,
+                                                 F2(d_num), 1, s),
+                         "mrc_td1024");
+    return td_staged(F2(d_iq), nframes, S, R, C, prefix, nullptr, w, F2(d_num), 1, s);
+}
+
+int ofdm_synth_frames(ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, int prefix,
+                      const ofdm_cf32 *d_X, unsigned long long seed, long long frame0,
+                      float noise_std, int freq_domain, int r0, ofdm_stream_t stream) {
+    if (!d_iq || !d_X || nframes < 0 || S < 1 || R < 1 || prefix < 0 || prefix > C || r0 < 0)
+        return fail(OFDM_E_ARG, "ofdm_synth_frames: bad arguments");
+    if (!pow2_c(C)) return fail(OFDM_E_UNSUPPORTED, "ofdm_synth_frames: C=%d unsupported", C);
+    return hip_check(ofdm::launch_synth(F2(d_iq), nframes, S, R, C, freq_domain ? 0 : prefix, F2(d_X),
+                                        seed, frame0, noise_std, freq_domain, r0, hs(stream)),
+                     "ofdm_synth_frames");
+}
+
+int ofdm_count_symbol_errors(const ofdm_cf32 *d_out, long long nframes, int S, int C,
+                             unsigned long long seed, long long frame0,
+                             unsigned long long *d_errors, ofdm_stream_t stream) {
+    if (!d_out || !d_errors || nframes < 0 || S < 2 || !pow2_c(C))
+        return fail(OFDM_E_ARG, "ofdm_count_symbol_errors: bad arguments");
+    return hip_check(ofdm::launch_count_errors(F2(d_out), nframes, S, C, seed, frame0, d_errors,
+                                               hs(stream)),
+                     "ofdm_count_symbol_errors");
+}
+
+}  // extern "C"

@@ -1,0 +1,207 @@
+// fft_synth.hip -- generic batched row FFT (Stockham in LDS) and the synthetic
+// OFDM frame generator / hard-decision checker used by tests and bench.
+//
+// The FFT replaces the reference's cuFFT batch (gpuLS::batchedFFT,
+// gpuLS.cu:343-349; cufftPlan1d + cufftExecC2C, gpuLS.cu:377-381) and FFTW's
+// fftOneRow (cpuLS.hpp:165-174): unnormalised forward C2C, sign -1.
+#include "common.hpp"
+#include "launch.hpp"
+
+namespace ofdm {
+
+template <int LOG2C, bool INV>
+__global__ void __launch_bounds__(256) k_fft_rows(const float2 *__restrict__ in, long long in_stride,
+                                                  int in_off, float2 *out, long long out_stride,
+                                                  int out_off, float scale) {
+    constexpr int C = 1 << LOG2C;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    float2 *a = lds, *b = lds + C;
+    const long long row = blockIdx.x;
+    const float2 *src = in + row * in_stride + in_off;
+    for (int i = threadIdx.x; i < C; i += blockDim.x) a[i] = src[i];
+    __syncthreads();
+    float2 *res = stockham_lds<LOG2C, INV>(a, b);
+    float2 *dst = out + row * out_stride + out_off;
+    for (int i = threadIdx.x; i < C; i += blockDim.x) {
+        float2 v = res[i];
+        dst[i] = float2{v.x * scale, v.y * scale};
+    }
+}
+
+template <int LOG2C>
+static hipError_t fft_rows_t(const float2 *in, long long in_stride, int in_off, float2 *out,
+                             long long out_stride, int out_off, long long nrows, bool inverse,
+                             float scale, hipStream_t s) {
+    constexpr int C = 1 << LOG2C;
+    const int threads = C / 4 < 256 ? (C / 4 < 64 ? 64 : C / 4) : 256;
+    const size_t lds = 2 * C * sizeof(float2);
+    // grid.x limit is 2^31-1; split very large batches
+    const long long maxg = 1ll << 30;
+    for (long long r0 = 0; r0 < nrows; r0 += maxg) {
+        const long long n = nrows - r0 < maxg ? nrows - r0 : maxg;
+        if (inverse)
+            hipLaunchKernelGGL((k_fft_rows<LOG2C, true>), dim3((unsigned)n), dim3(threads), lds, s,
+                               in + r0 * in_stride, in_stride, in_off, out + r0 * out_stride,
+                               out_stride, out_off, scale);
+        else
+            hipLaunchKernelGGL((k_fft_rows<LOG2C, false>), dim3((unsigned)n), dim3(threads), lds, s,
+                               in + r0 * in_stride, in_stride, in_off, out + r0 * out_stride,
+                               out_stride, out_off, scale);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_fft_rows(const float2 *in, long long in_stride, int in_off, float2 *out,
+                           long long out_stride, int out_off, long long nrows, int C,
+                           bool inverse, float scale, hipStream_t s) {
+    if (nrows <= 0) return hipSuccess;
+    switch (C) {
+#define OFDM_FFT_CASE(L) \
+    case 1 << L: return fft_rows_t<L>(in, in_stride, in_off, out, out_stride, out_off, nrows, inverse, scale, s);
+        OFDM_FFT_CASE(2) OFDM_FFT_CASE(3) OFDM_FFT_CASE(4) OFDM_FFT_CASE(5) OFDM_FFT_CASE(6)
+        OFDM_FFT_CASE(7) OFDM_FFT_CASE(8) OFDM_FFT_CASE(9) OFDM_FFT_CASE(10) OFDM_FFT_CASE(11)
+        OFDM_FFT_CASE(12)
+#undef OFDM_FFT_CASE
+    default: return hipErrorInvalidValue;
+    }
+}
+
+// --------------------------------------------------------------------------
+// Synthetic frames (SURVEY.md 8(d) "Synthetic inputs", RX convention of
+// 8(a) item 7): per frame f, antenna r, subcarrier j:
+//   H ~ CN(0,1), x_0 = X (pilot), x_s = QPSK (+-1/sqrt2 +- i/sqrt2), s >= 1
+//   Y[j+1] = H x, Y[0] = 0;  y = IFFT_C(Y)/sqrt(C) + CN(0, noise^2), with a
+//   cyclic prefix of `prefix` samples (time domain), or y = Y + noise (freq).
+// Everything is a pure function of (seed, global frame, symbol, antenna, bin)
+// so any shard of a batch can be regenerated independently.
+// --------------------------------------------------------------------------
+__device__ __forceinline__ float2 synth_channel(uint64_t seed, long long fg, int r, int j) {
+    const float2 g = gauss2(hash4(seed, 1, (uint64_t)fg, ((uint64_t)r << 32) | (uint32_t)j));
+    return {g.x * 0.70710678118654752f, g.y * 0.70710678118654752f};
+}
+__device__ __forceinline__ uint32_t synth_bits(uint64_t seed, long long fg, int s, int j) {
+    return (uint32_t)hash4(seed, 2, (uint64_t)fg, ((uint64_t)s << 32) | (uint32_t)j) & 3u;
+}
+__device__ __forceinline__ float2 qpsk(uint32_t bits) {
+    const float a = 0.70710678118654752f;
+    return {(bits & 1u) ? a : -a, (bits & 2u) ? a : -a};
+}
+
+template <int LOG2C>
+__global__ void __launch_bounds__(256) k_synth(float2 *iq, int S, int R, int prefix,
+                                               const float2 *__restrict__ X, uint64_t seed,
+                                               long long frame0, float noise_std, int freq_domain,
+                                               int r0) {
+    constexpr int C = 1 << LOG2C;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    float2 *a = lds, *b = lds + C;
+    // one block per (frame, symbol, antenna) row
+    const long long row = blockIdx.x;
+    const int r = (int)(row % R);
+    const long long fs = row / R;
+    const int s = (int)(fs % S);
+    const long long f = fs / S;
+    const long long fg = frame0 + f;
+    const int rg = r0 + r;
+    const int Cp = freq_domain ? C : C + prefix;
+    float2 *dst = iq + row * Cp;
+    for (int bin = threadIdx.x; bin < C; bin += blockDim.x) {
+        float2 v{0.f, 0.f};
+        if (bin > 0) {
+            const int j = bin - 1;
+            const float2 h = synth_channel(seed, fg, rg, j);
+            const float2 x = s == 0 ? X[j] : qpsk(synth_bits(seed, fg, s, j));
+            v = cmul(h, x);
+        }
+        a[bin] = v;
+    }
+    __syncthreads();
+    const float ns = noise_std * 0.70710678118654752f;
+    const uint64_t nkey = (((uint64_t)fg * (uint64_t)S + (uint64_t)s) << 20) ^ (uint64_t)rg;
+    if (freq_domain) {
+        for (int n = threadIdx.x; n < C; n += blockDim.x) {
+            const float2 g = gauss2(hash4(seed, 3, nkey, (uint64_t)n));
+            dst[n] = float2{a[n].x + ns * g.x, a[n].y + ns * g.y};
+        }
+        return;
+    }
+    float2 *res = stockham_lds<LOG2C, true>(a, b);
+    const float sc = rsqrtf((float)C);
+    for (int n = threadIdx.x; n < C; n += blockDim.x) {
+        const float2 g = gauss2(hash4(seed, 3, nkey, (uint64_t)n));
+        res[n] = float2{res[n].x * sc + ns * g.x, res[n].y * sc + ns * g.y};
+    }
+    __syncthreads();
+    for (int n = threadIdx.x; n < C + prefix; n += blockDim.x)
+        dst[n] = n < prefix ? res[C - prefix + n] : res[n - prefix];
+}
+
+template <int LOG2C>
+static hipError_t synth_t(float2 *iq, long long nframes, int S, int R, int prefix,
+                          const float2 *X, uint64_t seed, long long frame0, float noise_std,
+                          int freq_domain, int r0, hipStream_t s) {
+    constexpr int C = 1 << LOG2C;
+    const int threads = C / 4 < 256 ? (C / 4 < 64 ? 64 : C / 4) : 256;
+    const size_t lds = 2 * C * sizeof(float2);
+    const long long rows = nframes * S * R;
+    const long long maxg = 1ll << 30;
+    const long long Cp = freq_domain ? C : C + prefix;
+    for (long long q0 = 0; q0 < rows; q0 += maxg) {
+        // chunk boundaries must be whole frames for the index math
+        long long n = rows - q0 < maxg ? rows - q0 : maxg;
+        const long long frame_rows = (long long)S * R;
+        n = (n / frame_rows) * frame_rows;
+        hipLaunchKernelGGL(k_synth<LOG2C>, dim3((unsigned)n), dim3(threads), lds, s, iq + q0 * Cp, S,
+                           R, prefix, X, seed, frame0 + q0 / frame_rows, noise_std, freq_domain, r0);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_synth(float2 *iq, long long nframes, int S, int R, int C, int prefix,
+                        const float2 *X, uint64_t seed, long long frame0, float noise_std,
+                        int freq_domain, int r0, hipStream_t s) {
+    if (nframes <= 0) return hipSuccess;
+    switch (C) {
+#define OFDM_SYN_CASE(L) \
+    case 1 << L: return synth_t<L>(iq, nframes, S, R, prefix, X, seed, frame0, noise_std, freq_domain, r0, s);
+        OFDM_SYN_CASE(2) OFDM_SYN_CASE(3) OFDM_SYN_CASE(4) OFDM_SYN_CASE(5) OFDM_SYN_CASE(6)
+        OFDM_SYN_CASE(7) OFDM_SYN_CASE(8) OFDM_SYN_CASE(9) OFDM_SYN_CASE(10) OFDM_SYN_CASE(11)
+        OFDM_SYN_CASE(12)
+#undef OFDM_SYN_CASE
+    default: return hipErrorInvalidValue;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_count_errors(const float2 *__restrict__ out, long long total,
+                                                      int S, int K, uint64_t seed, long long frame0,
+                                                      unsigned long long *errors) {
+    unsigned long long local = 0;
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += stride) {
+        const int k = (int)(e % K);
+        const long long q = e / K;  // data symbol index
+        const long long f = q / (S - 1);
+        const int s = 1 + (int)(q % (S - 1));
+        const int j = k < (K + 1) / 2 ? k + (K - 1) / 2 : k - (K + 1) / 2;
+        const uint32_t bits = synth_bits(seed, frame0 + f, s, j);
+        const float2 v = out[e];
+        const bool ok = ((v.x > 0.f) == ((bits & 1u) != 0)) && ((v.y > 0.f) == ((bits & 2u) != 0));
+        local += ok ? 0 : 1;
+    }
+    // wave reduce then one atomic per wave
+    for (int o = 32; o > 0; o >>= 1) local += __shfl_xor(local, o);
+    if ((threadIdx.x & 63) == 0 && local) atomicAdd(errors, local);
+}
+
+hipError_t launch_count_errors(const float2 *out, long long nframes, int S, int C, uint64_t seed,
+                               long long frame0, unsigned long long *errors, hipStream_t s) {
+    const long long total = nframes * (S - 1) * (long long)(C - 1);
+    if (total <= 0) return hipSuccess;
+    long long blocks = (total + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(k_count_errors, dim3((unsigned)blocks), dim3(256), 0, s, out, total, S, C - 1,
+                       seed, frame0, errors);
+    return hipGetLastError();
+}
+
+}  // namespace ofdm

@@ -1,0 +1,64 @@
+// launch.hpp -- internal host-side launchers for the LS/MRC kernels.
+// Arguments are validated by the C-ABI layer (capi.cpp) before these run;
+// every launcher returns hipGetLastError() of its launch(es).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace ofdm {
+
+// Generic batched row FFT (Stockham in LDS), in place or out of place.
+// Row i is read from in + i*in_stride + in_off and written to
+// out + i*out_stride + out_off.  C power of two, 4 <= C <= 4096.
+hipError_t launch_fft_rows(const float2 *in, long long in_stride, int in_off, float2 *out,
+                           long long out_stride, int out_off, long long nrows, int C,
+                           bool inverse, float scale, hipStream_t s);
+
+// LS channel estimate on frequency-domain pilot symbols.
+// Pilot of frame f: Y + f*frame_stride, R rows of C bins.
+// Hconj(f, r, j) at Hc + f*hc_fstride + r*hc_ld + j + hc_jofs  (j = 0..K-1)
+// P(f, j)        at P  + f*p_fstride + j + p_jofs
+// (reference layout: hc_ld = K, jofs = 0; bin layout: hc_ld = C, jofs = 1).
+hipError_t launch_ls_freq(const float2 *Y, long long frame_stride, long long nframes, int R,
+                          int C, const float2 *X, float2 *Hc, long long hc_fstride, int hc_ld,
+                          int hc_jofs, float *P, long long p_fstride, int p_jofs, hipStream_t s);
+
+// MRC on frequency-domain data symbols.  Data symbol q (q < nframes*nsym)
+// belongs to frame q / nsym and lives at
+// Y + (q / nsym)*frame_stride + (q % nsym)*sym_stride (R rows of C bins).
+// mode 0: full demod  out[q][out_pos(j)] = (sum_r Y*Hc) / P
+// mode 1: numerator   out[q][j] = sum_r Y*Hc  (antenna-split partial)
+hipError_t launch_mrc_freq(const float2 *Y, long long frame_stride, long long sym_stride,
+                           long long nframes, int nsym, int R, int C, const float2 *Hc,
+                           long long hc_fstride, int hc_ld, int hc_jofs, const float *P,
+                           long long p_fstride, int p_jofs, float2 *out, int mode,
+                           hipStream_t s);
+
+// Finalise antenna-split numerators: elements [e0, e0+count) of the flat
+// [nframes][nsym][K] numerator array (num points at element e0) are divided
+// by P[f][j] and stored rotated into out ([nframes][nsym][K], full array).
+hipError_t launch_mrc_finalize(const float2 *num, long long e0, long long count, int nsym,
+                               int K, const float *P, float2 *out, hipStream_t s);
+
+// Fused time-domain receiver, C = 1024 (32 x 32 wave FFT).
+// Frames: iq + f*S*R*(C+prefix); pilot = symbol 0, data = symbols 1..S-1.
+// Workspace: Hc [F][R][C] (bin layout), P [F][C].
+hipError_t launch_ls_td1024(const float2 *iq, long long nframes, int S, int R, int prefix,
+                            const float2 *X, float2 *Hc, float *P, int partial,
+                            hipStream_t s);
+hipError_t launch_mrc_td1024(const float2 *iq, long long nframes, int S, int R, int prefix,
+                             const float2 *Hc, const float *P, float2 *out, int mode,
+                             hipStream_t s);
+
+// Synthetic frames: time-domain (freq_domain=0, rows of C+prefix with a
+// cyclic prefix) or frequency-domain (freq_domain=1, rows of C) IQ.
+hipError_t launch_synth(float2 *iq, long long nframes, int S, int R, int C, int prefix,
+                        const float2 *X, uint64_t seed, long long frame0, float noise_std,
+                        int freq_domain, int r0, hipStream_t s);
+// Hard-decision QPSK errors of demodulated output against the synthetic data.
+hipError_t launch_count_errors(const float2 *out, long long nframes, int S, int C,
+                               uint64_t seed, long long frame0, unsigned long long *errors,
+                               hipStream_t s);
+
+}  // namespace ofdm

@@ -1,0 +1,165 @@
+// lsmrc_freq.hip -- LS channel estimation and MRC combining on
+// frequency-domain symbols (FFT already applied).
+//
+// These are the north-star kernels of the reference's GPU path re-designed
+// for CDNA4:
+//   findHs (gpuLS.cu:158-182) + findDistSqrd (gpuLS.cu:185-209)
+//     -> k_ls_freq: one lane per subcarrier, antenna loop in registers
+//        (coalesced along subcarriers, no shared-memory tree, no race), the
+//        |H|^2 sum kept in the reference's sequential antenna order
+//        (cpuLS.hpp:211-228).
+//   multiplyWithChannelConj + combineForMRC + shiftOneRow (gpuLS.cu:109-125,
+//   212-259) -> k_mrc_freq: one pass, no materialised R x K product tensor,
+//   16-byte loads of two adjacent bins per lane, the output rotation folded
+//   into the store index.
+#include "common.hpp"
+#include "launch.hpp"
+
+namespace ofdm {
+
+__global__ void __launch_bounds__(256) k_ls_freq(const float2 *__restrict__ Y, long long frame_stride,
+                                                 int R, int C, const float2 *__restrict__ X,
+                                                 float2 *__restrict__ Hc, long long hc_fstride,
+                                                 int hc_ld, int hc_jofs, float *__restrict__ P,
+                                                 long long p_fstride, int p_jofs) {
+    const int K = C - 1;
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    const long long f = blockIdx.y;
+    const float2 *Yf = Y + f * frame_stride;
+    float2 *Hf = Hc + f * hc_fstride;
+    float *Pf = P + f * p_fstride;
+    if (j < K) {
+        const float2 x = X[j];
+        float p = 0.f;
+        for (int r = 0; r < R; ++r) {
+            const float2 h = ls_conj(Yf[(long long)r * C + j + 1], x);
+            Hf[(long long)r * hc_ld + j + hc_jofs] = h;
+            // findDistSqrd: Hsqrd = Hsqrd + re*re + im*im, rows in order
+            p = (r == 0) ? (h.x * h.x) + (h.y * h.y) : p + (h.x * h.x) + (h.y * h.y);
+        }
+        Pf[j + p_jofs] = p;
+    }
+    if (hc_jofs == 1 && j == 0) {  // bin layout: DC slot of H is 0, of P is 1
+        for (int r = 0; r < R; ++r) Hf[(long long)r * hc_ld] = float2{0.f, 0.f};
+        if (p_jofs == 1) Pf[0] = 1.f;
+    }
+}
+
+hipError_t launch_ls_freq(const float2 *Y, long long frame_stride, long long nframes, int R, int C,
+                          const float2 *X, float2 *Hc, long long hc_fstride, int hc_ld, int hc_jofs,
+                          float *P, long long p_fstride, int p_jofs, hipStream_t s) {
+    if (nframes <= 0) return hipSuccess;
+    const int K = C - 1;
+    const long long maxy = 65535;
+    for (long long f0 = 0; f0 < nframes; f0 += maxy) {
+        const long long n = nframes - f0 < maxy ? nframes - f0 : maxy;
+        hipLaunchKernelGGL(k_ls_freq, dim3((K + 255) / 256, (unsigned)n), dim3(256), 0, s,
+                           Y + f0 * frame_stride, frame_stride, R, C, X, Hc + f0 * hc_fstride,
+                           hc_fstride, hc_ld, hc_jofs, P + f0 * p_fstride, p_fstride, p_jofs);
+    }
+    return hipGetLastError();
+}
+
+// One lane = two adjacent bins (b = 2m, 2m+1) of one data symbol.
+template <bool BIN_LAYOUT>
+__global__ void __launch_bounds__(256) k_mrc_freq(const float2 *__restrict__ Y, long long frame_stride,
+                                                  long long sym_stride, long long nq, int nsym, int R,
+                                                  int C, const float2 *__restrict__ Hc,
+                                                  long long hc_fstride, int hc_ld, int hc_jofs,
+                                                  const float *__restrict__ P, long long p_fstride,
+                                                  int p_jofs, float2 *__restrict__ out, int mode) {
+    const int K = C - 1;
+    const int pairs = C / 2;
+    const int bps = (pairs + blockDim.x - 1) / blockDim.x;  // blocks per symbol
+    const long long q = (long long)blockIdx.x / bps;
+    const int m = (int)(blockIdx.x % bps) * blockDim.x + threadIdx.x;
+    if (q >= nq || m >= pairs) return;
+    const long long f = q / nsym;
+    const long long sd = q % nsym;
+    const float2 *Ys = Y + f * frame_stride + sd * sym_stride + 2 * m;
+    const float2 *Hf = Hc + f * hc_fstride;
+    const int j0 = 2 * m - 1, j1 = 2 * m;  // subcarriers of bins 2m, 2m+1
+    float2 a0{0.f, 0.f}, a1{0.f, 0.f};
+    for (int r = 0; r < R; ++r) {
+        const float4 y = *reinterpret_cast<const float4 *>(Ys + (long long)r * C);
+        float2 h0, h1;
+        if (BIN_LAYOUT) {  // Hc(r, b) at r*hc_ld + b, DC slot zero
+            const float4 h = *reinterpret_cast<const float4 *>(Hf + (long long)r * hc_ld + 2 * m);
+            h0 = float2{h.x, h.y};
+            h1 = float2{h.z, h.w};
+        } else {
+            const float2 *hr = Hf + (long long)r * hc_ld + hc_jofs;
+            h0 = m > 0 ? hr[j0] : float2{0.f, 0.f};
+            h1 = hr[j1];
+        }
+        // matrixMultThenSum (cpuLS.hpp:203-204), antennas in order
+        a0.x = a0.x + (y.x * h0.x - y.y * h0.y);
+        a0.y = a0.y + (y.x * h0.y + y.y * h0.x);
+        a1.x = a1.x + (y.z * h1.x - y.w * h1.y);
+        a1.y = a1.y + (y.z * h1.y + y.w * h1.x);
+    }
+    float2 *o = out + q * K;
+    if (mode == 0) {
+        const float *Pf = P + f * p_fstride + p_jofs;
+        if (m > 0) {
+            const float p0 = Pf[j0];
+            o[out_pos(j0, K)] = float2{a0.x / p0, a0.y / p0};
+        }
+        const float p1 = Pf[j1];
+        o[out_pos(j1, K)] = float2{a1.x / p1, a1.y / p1};
+    } else {
+        if (m > 0) o[j0] = a0;
+        o[j1] = a1;
+    }
+}
+
+hipError_t launch_mrc_freq(const float2 *Y, long long frame_stride, long long sym_stride,
+                           long long nframes, int nsym, int R, int C, const float2 *Hc,
+                           long long hc_fstride, int hc_ld, int hc_jofs, const float *P,
+                           long long p_fstride, int p_jofs, float2 *out, int mode, hipStream_t s) {
+    const long long nq = nframes * nsym;
+    if (nq <= 0) return hipSuccess;
+    const int threads = C / 2 < 256 ? 64 * ((C / 2 + 63) / 64) : 256;
+    const int bps = (C / 2 + threads - 1) / threads;
+    const long long blocks = nq * bps;
+    if (blocks > 0x7fffffffll) return hipErrorInvalidValue;
+    const bool bin = (hc_jofs == 0 && hc_ld == C && (hc_fstride % 2) == 0 &&
+                      ((uintptr_t)Hc % 16) == 0);
+    if (bin)
+        hipLaunchKernelGGL(k_mrc_freq<true>, dim3((unsigned)blocks), dim3(threads), 0, s, Y,
+                           frame_stride, sym_stride, nq, nsym, R, C, Hc, hc_fstride, hc_ld, hc_jofs,
+                           P, p_fstride, p_jofs, out, mode);
+    else
+        hipLaunchKernelGGL(k_mrc_freq<false>, dim3((unsigned)blocks), dim3(threads), 0, s, Y,
+                           frame_stride, sym_stride, nq, nsym, R, C, Hc, hc_fstride, hc_ld, hc_jofs,
+                           P, p_fstride, p_jofs, out, mode);
+    return hipGetLastError();
+}
+
+__global__ void __launch_bounds__(256) k_mrc_finalize(const float2 *__restrict__ num, long long e0,
+                                                      long long count, int nsym, int K,
+                                                      const float *__restrict__ P,
+                                                      float2 *__restrict__ out) {
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) {
+        const long long e = e0 + i;
+        const long long q = e / K;
+        const int j = (int)(e % K);
+        const long long f = q / nsym;
+        const float p = P[f * K + j];
+        const float2 v = num[i];
+        out[q * K + out_pos(j, K)] = float2{v.x / p, v.y / p};
+    }
+}
+
+hipError_t launch_mrc_finalize(const float2 *num, long long e0, long long count, int nsym, int K,
+                               const float *P, float2 *out, hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    long long blocks = (count + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(k_mrc_finalize, dim3((unsigned)blocks), dim3(256), 0, s, num, e0, count, nsym, K,
+                       P, out);
+    return hipGetLastError();
+}
+
+}  // namespace ofdm

@@ -1,0 +1,273 @@
+"""Python binding of the C ABI in include/ofdm_lsmrc.h (libofdm_lsmrc.so).
+
+Plumbing for tests and bench.py: device memory and streams come from PyTorch
+(ROCm build), the compute is the HIP library.  There is no CPU fallback:
+every compute call goes through libofdm_lsmrc.so and raises if it fails.
+
+Mirrors the reference's operator surface:
+  gpuLS::batchedFFT / cufft        -> fft_rows
+  findHs + findDistSqrd            -> ls_estimate
+  multiplyWithChannelConj + combineForMRC + shiftOneRow -> mrc_demod
+  demodOneFrameCUDA (batched)      -> frame_demod / frame_demod_freq
+  matrix_readX                     -> read_pilots / pilot_rotate
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libofdm_lsmrc.so")
+HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "ofdm_lsmrc.h")
+
+_c = ctypes
+_P = _c.c_void_p
+_LL = _c.c_longlong
+_I = _c.c_int
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "ofdm_version": (_I, []),
+    "ofdm_last_error": (_c.c_char_p, []),
+    "ofdm_pilot_rotate": (_I, [_P, _I, _P]),
+    "ofdm_read_pilots": (_I, [_c.c_char_p, _I, _c.c_float, _P]),
+    "ofdm_fft_rows": (_I, [_P, _P, _LL, _I, _I, _P]),
+    "ofdm_ls_estimate": (_I, [_P, _P, _I, _I, _P, _P, _P]),
+    "ofdm_mrc_demod": (_I, [_P, _LL, _P, _P, _I, _I, _P, _P]),
+    "ofdm_mrc_numerator": (_I, [_P, _LL, _P, _I, _I, _P, _P]),
+    "ofdm_mrc_finalize": (_I, [_P, _LL, _LL, _I, _I, _P, _P, _P]),
+    "ofdm_frame_workspace_bytes": (_c.c_size_t, [_LL, _I, _I, _I]),
+    "ofdm_frame_demod": (_I, [_P, _LL, _I, _I, _I, _I, _P, _P, _c.c_size_t, _P, _P]),
+    "ofdm_frame_estimate": (_I, [_P, _LL, _I, _I, _I, _I, _P, _P, _c.c_size_t, _P]),
+    "ofdm_frame_combine": (_I, [_P, _LL, _I, _I, _I, _I, _P, _c.c_size_t, _P, _P]),
+    "ofdm_frame_demod_freq": (_I, [_P, _LL, _I, _I, _I, _P, _P, _c.c_size_t, _P, _P]),
+    "ofdm_frame_ls_partial": (_I, [_P, _LL, _I, _I, _I, _I, _P, _P, _c.c_size_t, _P, _P]),
+    "ofdm_frame_mrc_partial": (_I, [_P, _LL, _I, _I, _I, _I, _P, _c.c_size_t, _P, _P]),
+    "ofdm_synth_frames": (_I, [_P, _LL, _I, _I, _I, _I, _P, _c.c_ulonglong, _LL, _c.c_float,
+                               _I, _I, _P]),
+    "ofdm_count_symbol_errors": (_I, [_P, _LL, _I, _I, _c.c_ulonglong, _LL, _P, _P]),
+}
+
+_lib = None
+
+
+class OfdmError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libofdm_lsmrc.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OfdmError(f"{LIB_PATH} not built: run `make -C gpu-accel-ofdm-ls-mrc_amd` "
+                            "(or __graft_entry__.build())")
+        # One HIP runtime per process: torch's wheel bundles libamdhip64
+        # (SONAME libamdhip64.so.7).  Loading torch first lets our NEEDED
+        # libamdhip64.so.7 bind to that copy; loading ours first would pull
+        # in /opt/rocm's and torch would then load a second runtime.
+        import torch  # noqa: F401
+        L = _c.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(rc, fn):
+    if rc < 0:
+        msg = lib().ofdm_last_error().decode(errors="replace")
+        raise OfdmError(f"{fn} failed ({rc}): {msg}")
+    return rc
+
+
+def _dptr(t, name="tensor"):
+    import torch
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise OfdmError(f"{name} must be a device tensor")
+    if not t.is_contiguous():
+        raise OfdmError(f"{name} must be contiguous")
+    return _P(t.data_ptr())
+
+
+def _stream(stream):
+    import torch
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return _P(stream.cuda_stream)
+
+
+def c64(shape, device="cuda"):
+    import torch
+    return torch.empty(shape, dtype=torch.complex64, device=device)
+
+
+# ---------------------------------------------------------------- host side
+
+def pilot_rotate(raw):
+    raw = np.ascontiguousarray(raw, np.complex64)
+    X = np.empty_like(raw)
+    _check(lib().ofdm_pilot_rotate(raw.ctypes.data_as(_P), raw.size, X.ctypes.data_as(_P)),
+           "ofdm_pilot_rotate")
+    return X
+
+
+def read_pilots(path, K, fill=0.707):
+    """matrix_readX: returns (X, used_fill)."""
+    X = np.empty(K, np.complex64)
+    rc = _check(lib().ofdm_read_pilots(None if path is None else path.encode(), K, fill,
+                                       X.ctypes.data_as(_P)), "ofdm_read_pilots")
+    return X, rc == 1
+
+
+# -------------------------------------------------------------- device side
+
+def fft_rows(x, out=None, inverse=False, stream=None):
+    C = x.shape[-1]
+    nrows = x.numel() // C
+    if out is None:
+        out = x
+    _check(lib().ofdm_fft_rows(_dptr(x, "x"), _dptr(out, "out"), nrows, C, int(inverse),
+                               _stream(stream)), "ofdm_fft_rows")
+    return out
+
+
+def ls_estimate(Y, X, stream=None):
+    """Y: (R, C) freq-domain pilot symbol, X: (K,) rotated pilots -> (Hconj (R,K), Hsqrd (K,))."""
+    import torch
+    R, C = Y.shape
+    H = c64((R, C - 1), Y.device)
+    P = torch.empty(C - 1, dtype=torch.float32, device=Y.device)
+    _check(lib().ofdm_ls_estimate(_dptr(Y), _dptr(X), R, C, _dptr(H), _dptr(P), _stream(stream)),
+           "ofdm_ls_estimate")
+    return H, P
+
+
+def mrc_demod(Y, H, P, stream=None):
+    """Y: (nsyms, R, C) freq-domain data symbols -> (nsyms, K)."""
+    n, R, C = Y.shape
+    out = c64((n, C - 1), Y.device)
+    _check(lib().ofdm_mrc_demod(_dptr(Y), n, _dptr(H), _dptr(P), R, C, _dptr(out),
+                                _stream(stream)), "ofdm_mrc_demod")
+    return out
+
+
+def mrc_numerator(Y, H, stream=None):
+    n, R, C = Y.shape
+    out = c64((n, C - 1), Y.device)
+    _check(lib().ofdm_mrc_numerator(_dptr(Y), n, _dptr(H), R, C, _dptr(out), _stream(stream)),
+           "ofdm_mrc_numerator")
+    return out
+
+
+def mrc_finalize(num_chunk, e0, nsym, K, P, out, stream=None):
+    _check(lib().ofdm_mrc_finalize(_dptr(num_chunk), e0, num_chunk.numel(), nsym, K, _dptr(P),
+                                   _dptr(out), _stream(stream)), "ofdm_mrc_finalize")
+    return out
+
+
+def workspace_bytes(nframes, S, R, C):
+    return int(lib().ofdm_frame_workspace_bytes(nframes, S, R, C))
+
+
+def workspace(nframes, S, R, C, device="cuda"):
+    import torch
+    return torch.empty(max(workspace_bytes(nframes, S, R, C), 256), dtype=torch.uint8,
+                       device=device)
+
+
+def frame_demod(iq, X, prefix=0, ws=None, out=None, stream=None):
+    """iq: (F, S, R, C+prefix) time domain -> (F, S-1, K)."""
+    F, S, R, Cp = iq.shape
+    C = Cp - prefix
+    if ws is None:
+        ws = workspace(F, S, R, C, iq.device)
+    if out is None:
+        out = c64((F, S - 1, C - 1), iq.device)
+    _check(lib().ofdm_frame_demod(_dptr(iq), F, S, R, C, prefix, _dptr(X), _dptr(ws), ws.numel(),
+                                  _dptr(out), _stream(stream)), "ofdm_frame_demod")
+    return out
+
+
+def frame_estimate(iq, X, prefix, ws, stream=None):
+    """LS stage of frame_demod: estimates of every frame into the workspace."""
+    F, S, R, Cp = iq.shape
+    _check(lib().ofdm_frame_estimate(_dptr(iq), F, S, R, Cp - prefix, prefix, _dptr(X), _dptr(ws),
+                                     ws.numel(), _stream(stream)), "ofdm_frame_estimate")
+    return ws
+
+
+def frame_combine(iq, prefix, ws, out, stream=None):
+    """MRC stage of frame_demod against the estimates in the workspace."""
+    F, S, R, Cp = iq.shape
+    _check(lib().ofdm_frame_combine(_dptr(iq), F, S, R, Cp - prefix, prefix, _dptr(ws),
+                                    ws.numel(), _dptr(out), _stream(stream)),
+           "ofdm_frame_combine")
+    return out
+
+
+def frame_demod_freq(Y, X, ws=None, out=None, stream=None):
+    """Y: (F, S, R, C) frequency domain -> (F, S-1, K)."""
+    F, S, R, C = Y.shape
+    if ws is None:
+        ws = workspace(F, S, R, C, Y.device)
+    if out is None:
+        out = c64((F, S - 1, C - 1), Y.device)
+    _check(lib().ofdm_frame_demod_freq(_dptr(Y), F, S, R, C, _dptr(X), _dptr(ws), ws.numel(),
+                                       _dptr(out), _stream(stream)), "ofdm_frame_demod_freq")
+    return out
+
+
+def frame_ls_partial(iq, X, prefix=0, ws=None, P=None, stream=None):
+    import torch
+    F, S, R, Cp = iq.shape
+    C = Cp - prefix
+    if ws is None:
+        ws = workspace(F, S, R, C, iq.device)
+    if P is None:
+        P = torch.empty((F, C - 1), dtype=torch.float32, device=iq.device)
+    _check(lib().ofdm_frame_ls_partial(_dptr(iq), F, S, R, C, prefix, _dptr(X), _dptr(ws),
+                                       ws.numel(), _dptr(P), _stream(stream)),
+           "ofdm_frame_ls_partial")
+    return P, ws
+
+
+def frame_mrc_partial(iq, ws, prefix=0, num=None, stream=None):
+    F, S, R, Cp = iq.shape
+    C = Cp - prefix
+    if num is None:
+        num = c64((F, S - 1, C - 1), iq.device)
+    _check(lib().ofdm_frame_mrc_partial(_dptr(iq), F, S, R, C, prefix, _dptr(ws), ws.numel(),
+                                        _dptr(num), _stream(stream)), "ofdm_frame_mrc_partial")
+    return num
+
+
+def synth_frames(F, S, R, C, X, prefix=0, seed=1234, frame0=0, noise_std=0.01,
+                 freq_domain=False, r0=0, out=None, stream=None):
+    Cp = C if freq_domain else C + prefix
+    if out is None:
+        out = c64((F, S, R, Cp), X.device)
+    _check(lib().ofdm_synth_frames(_dptr(out), F, S, R, C, prefix, _dptr(X), seed, frame0,
+                                   noise_std, int(freq_domain), r0, _stream(stream)),
+           "ofdm_synth_frames")
+    return out
+
+
+def count_symbol_errors(out, S, seed=1234, frame0=0, stream=None):
+    import torch
+    F = out.shape[0]
+    K = out.shape[-1]
+    err = torch.zeros(1, dtype=torch.int64, device=out.device)
+    _check(lib().ofdm_count_symbol_errors(_dptr(out), F, S, K + 1, seed, frame0, _dptr(err),
+                                          _stream(stream)), "ofdm_count_symbol_errors")
+    return err
+
+
+def header_symbols(path=HEADER_PATH):
+    """Function names declared in include/ofdm_lsmrc.h."""
+    import re
+    txt = open(path).read()
+    return sorted(set(re.findall(r"^\s*(?:int|size_t|const char \*)\s*(ofdm_\w+)\s*\(", txt,
+                                 re.M)))

@@ -1,0 +1,178 @@
+/*
+ * ofdm_lsmrc.h -- C ABI of the MI355X (gfx950) OFDM uplink receiver hot path:
+ * per-subcarrier Least-Squares channel estimation from a pilot symbol and
+ * Maximal-Ratio-Combining demodulation of data symbols across RX antennas.
+ *
+ * Library: gpu-accel-ofdm-ls-mrc_amd/lib/libofdm_lsmrc.so (hand-written HIP
+ * kernels for CDNA4; no CPU fallback -- every compute entry point runs on the
+ * GPU and returns an error if it cannot).
+ *
+ * Conventions (all cite the reference bhargav0410/gpu-accel-ofdm-ls-mrc):
+ *   R  = RX antennas (numOfRows), C = FFT size / subcarriers (dimension, a
+ *        power of two), K = C - 1 used subcarriers (the DC bin is dropped,
+ *        cpuLS.hpp:290-292), S = symbols per frame (lenOfBuffer), symbol 0 of
+ *        a frame is the pilot, symbols 1..S-1 carry data.
+ *   ofdm_cf32 = {float re, im}, layout-identical to complexF
+ *        (ShMemSymBuff.hpp:86-89), cuFloatComplex and hipFloatComplex.
+ *   A symbol is R rows of C (+prefix) samples, row-major by antenna
+ *        (struct symbol, ShMemSymBuff.hpp:92-94); frames are consecutive
+ *        symbols, batches are consecutive frames.
+ *   Output of a data symbol: K values, shiftOneRow-rotated (cpuLS.hpp:135-149):
+ *        out[k] = Z[(k + (K-1)/2) mod K], Z[j] = sum_r Y[r][j+1] conj(H[r][j])
+ *        / sum_r |H[r][j]|^2.
+ *   Pointers named d_* are device pointers; `stream` is a hipStream_t (NULL =
+ *   the default stream).  Calls are asynchronous on that stream.
+ *   Return value: 0 (OFDM_OK) or a negative OFDM_E_* code; ofdm_last_error()
+ *   describes the last failure on the calling thread.
+ */
+#ifndef OFDM_LSMRC_H_
+#define OFDM_LSMRC_H_
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OFDM_LSMRC_VERSION 1
+
+typedef struct ofdm_cf32 { float re, im; } ofdm_cf32;
+typedef void *ofdm_stream_t; /* hipStream_t */
+
+enum {
+    OFDM_OK = 0,
+    OFDM_E_ARG = -1,         /* invalid argument (shape, null, alignment) */
+    OFDM_E_HIP = -2,         /* HIP runtime / launch failure */
+    OFDM_E_UNSUPPORTED = -3, /* shape not supported by this build */
+    OFDM_E_IO = -4           /* file I/O */
+};
+
+int ofdm_version(void);
+const char *ofdm_last_error(void);
+
+/* ---------------------------------------------------------------- host --- */
+
+/* Pilot rotation of matrix_readX (cpuLS.hpp:105-112, gpuLS.cu:75-82):
+ * X[j] = raw[(j + (K+1)/2) mod K].  raw may equal X. */
+int ofdm_pilot_rotate(const ofdm_cf32 *raw, int K, ofdm_cf32 *X);
+
+/* matrix_readX (cpuLS.hpp:80-117 / gpuLS::matrix_readX, gpuLS.cu:53-86):
+ * read K raw complex floats from `path` and rotate.  If the file cannot be
+ * opened every X[j] = fill + i*fill (the reference uses 0.707 on the CPU path,
+ * cpuLS.hpp:84-90, and 1.0 on the GPU path, gpuLS.cu:57-63) and 1 is
+ * returned. */
+int ofdm_read_pilots(const char *path, int K, float fill, ofdm_cf32 *X);
+
+/* ------------------------------------------------------ device: stages --- */
+
+/* Batched forward (inverse != 0: backward) unnormalised C2C FFT of nrows
+ * contiguous rows of C samples, in place or out of place.
+ * Replaces gpuLS::batchedFFT (gpuLS.cu:343-349) / cufftPlan1d + cufftExecC2C
+ * (gpuLS.cu:377-381, 441-445) and fftOneRow (cpuLS.hpp:165-174).
+ * C in {4, 8, ..., 4096}. */
+int ofdm_fft_rows(const ofdm_cf32 *d_in, ofdm_cf32 *d_out, long long nrows, int C, int inverse,
+                  ofdm_stream_t stream);
+
+/* LS channel estimate from one frequency-domain pilot symbol d_Y (R x C,
+ * bin 0 = DC) and the rotated pilots d_X (K values):
+ *   d_Hconj[r][j] = conj(Y[r][j+1] / X[j])  (R x K)
+ *   d_Hsqrd[j]    = sum_r |Hconj[r][j]|^2   (K floats)
+ * Replaces findHs (gpuLS.cu:158-182) + findDistSqrd (gpuLS.cu:185-209) and
+ * the post-FFT part of firstVector (cpuLS.hpp:290-311). */
+int ofdm_ls_estimate(const ofdm_cf32 *d_Y, const ofdm_cf32 *d_X, int R, int C, ofdm_cf32 *d_Hconj,
+                     float *d_Hsqrd, ofdm_stream_t stream);
+
+/* MRC demodulation of nsyms frequency-domain symbols d_Y (nsyms x R x C)
+ * against one estimate: d_out (nsyms x K) = rotated sum_r Y Hconj / Hsqrd.
+ * Replaces multiplyWithChannelConj + combineForMRC + shiftOneRow
+ * (gpuLS.cu:109-125, 212-259) and the post-FFT part of doOneSymbol
+ * (cpuLS.hpp:354-368). */
+int ofdm_mrc_demod(const ofdm_cf32 *d_Y, long long nsyms, const ofdm_cf32 *d_Hconj,
+                   const float *d_Hsqrd, int R, int C, ofdm_cf32 *d_out, ofdm_stream_t stream);
+
+/* MRC numerator only (matrixMultThenSum, cpuLS.hpp:187-208):
+ * d_num (nsyms x K, subcarrier order, not rotated) = sum_r Y[r][j+1] Hconj[r][j].
+ * With a subset of antennas this is the partial numerator of the antenna-split
+ * multi-GPU path. */
+int ofdm_mrc_numerator(const ofdm_cf32 *d_Y, long long nsyms, const ofdm_cf32 *d_Hconj, int R,
+                       int C, ofdm_cf32 *d_num, ofdm_stream_t stream);
+
+/* Finalise (summed) numerators: elements [e0, e0+count) of a flat
+ * [nframes][nsym][K] numerator array (d_num points at element e0) are divided
+ * by d_Hsqrd[f][j] ([nframes][K]) and stored rotated into d_out, the full
+ * [nframes][nsym][K] output array.  (combineForMRC's divide + shiftOneRow,
+ * gpuLS.cu:254-256, 109-125.) */
+int ofdm_mrc_finalize(const ofdm_cf32 *d_num, long long e0, long long count, int nsym, int K,
+                      const float *d_Hsqrd, ofdm_cf32 *d_out, ofdm_stream_t stream);
+
+/* ------------------------------------------------------ device: frames --- */
+
+/* Workspace for ofdm_frame_demod / ofdm_frame_demod_freq (bytes, 256-aligned
+ * pieces): per-frame channel estimates [F][R][C], |H|^2 [F][C] and, for FFT
+ * sizes without a fused kernel, a frequency-domain staging buffer. */
+size_t ofdm_frame_workspace_bytes(long long nframes, int S, int R, int C);
+
+/* Frame-batched receiver on time-domain IQ (what ShMemSymBuff delivers):
+ * d_iq = nframes x S x R x (C + prefix) samples; the cyclic prefix of every
+ * row is skipped (ShMemSymBuff.hpp:309-322), each row is FFT'd, symbol 0 of
+ * each frame gives the LS estimate, symbols 1..S-1 are MRC-demodulated into
+ * d_out = nframes x (S-1) x K.  Replaces demodOneFrameCUDA / demodOptimized
+ * (gpuLS.cu:575-769) and the cpuLS_main loop (cpuLS_main.cpp:80-92), for a
+ * whole batch of frames in one call.  C = 1024 runs the fused one-pass
+ * kernels; other C run FFT + LS + MRC stages through the workspace. */
+int ofdm_frame_demod(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, int prefix,
+                     const ofdm_cf32 *d_X, void *d_ws, size_t ws_bytes, ofdm_cf32 *d_out,
+                     ofdm_stream_t stream);
+
+/* The two stages of ofdm_frame_demod, for callers that pipeline or time them
+ * separately: ofdm_frame_estimate FFTs the pilot symbol of every frame and
+ * stores the LS estimate (Hconj, |H|^2) in d_ws (gpuLS::firstVector,
+ * gpuLS.cu:351-408, per frame); ofdm_frame_combine MRC-demodulates the data
+ * symbols against it (gpuLS::demodOneSymbol, gpuLS.cu:410-473, per symbol).
+ * ofdm_frame_demod == estimate then combine on the same stream. */
+int ofdm_frame_estimate(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, int prefix,
+                        const ofdm_cf32 *d_X, void *d_ws, size_t ws_bytes, ofdm_stream_t stream);
+int ofdm_frame_combine(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, int prefix,
+                       void *d_ws, size_t ws_bytes, ofdm_cf32 *d_out, ofdm_stream_t stream);
+
+/* ofdm_frame_demod on frequency-domain symbols (FFT done upstream, no prefix):
+ * d_Y = nframes x S x R x C. */
+int ofdm_frame_demod_freq(const ofdm_cf32 *d_Y, long long nframes, int S, int R, int C,
+                          const ofdm_cf32 *d_X, void *d_ws, size_t ws_bytes, ofdm_cf32 *d_out,
+                          ofdm_stream_t stream);
+
+/* Antenna-split pieces (time-domain frames holding this GPU's R antennas):
+ * partial |H|^2 per frame into d_P ([nframes][K], sum over the local
+ * antennas; sum the partials across GPUs), and partial MRC numerators
+ * d_num ([nframes][S-1][K], subcarrier order; sum across GPUs, then
+ * ofdm_mrc_finalize).  d_ws as for ofdm_frame_demod. */
+int ofdm_frame_ls_partial(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, int prefix,
+                          const ofdm_cf32 *d_X, void *d_ws, size_t ws_bytes, float *d_P,
+                          ofdm_stream_t stream);
+int ofdm_frame_mrc_partial(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int C,
+                           int prefix, void *d_ws, size_t ws_bytes, ofdm_cf32 *d_num,
+                           ofdm_stream_t stream);
+
+/* --------------------------------------------------- synthetic frames --- */
+
+/* Deterministic synthetic frames for tests and benchmarks:
+ * H ~ CN(0,1) per (frame, antenna, subcarrier), pilot = d_X, data = QPSK,
+ * bins j+1 carry H x (bin 0 empty), y = IFFT(Y)/sqrt(C) + CN(0, noise_std^2)
+ * with a cyclic prefix (freq_domain = 0), or y = Y + noise (freq_domain = 1,
+ * prefix ignored).  Frame f of the buffer is global frame frame0 + f; antenna
+ * r is global antenna r0 + r (antenna-split shards). */
+int ofdm_synth_frames(ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, int prefix,
+                      const ofdm_cf32 *d_X, unsigned long long seed, long long frame0,
+                      float noise_std, int freq_domain, int r0, ofdm_stream_t stream);
+
+/* Adds to *d_errors the number of demodulated symbols in d_out
+ * (nframes x (S-1) x K) whose QPSK hard decision differs from the synthetic
+ * data of ofdm_synth_frames(seed, frame0). */
+int ofdm_count_symbol_errors(const ofdm_cf32 *d_out, long long nframes, int S, int C,
+                             unsigned long long seed, long long frame0,
+                             unsigned long long *d_errors, ofdm_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OFDM_LSMRC_H_ */

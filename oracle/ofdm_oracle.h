@@ -1,0 +1,90 @@
+/*
+ * ofdm_oracle.h -- CPU restatement of the reference's LS + MRC receiver path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (the HIP library under
+ * gpu-accel-ofdm-ls-mrc_amd/) links, calls or executes this code.  Only tests/,
+ * __graft_entry__.smoke() and bench.py's `cpu_baseline` leg may load it, and
+ * only as the checker / the timed CPU baseline.
+ *
+ * Every function cites the reference file:line it restates (paths are into the
+ * read-only reference checkout, bhargav0410/gpu-accel-ofdm-ls-mrc).
+ *
+ * Parity pinning (see DESIGN.md "Oracle"):
+ *   - the post-FFT arithmetic (pilot rotation, LS divide, conj, |H|^2, MRC sum,
+ *     normalise, output rotation) is checked bit-for-bit against the reference's
+ *     own functions compiled from /root/reference/cpuLS.hpp by
+ *     oracle/build_ref.sh (oracle/_ref/), and through them against the golden
+ *     fixtures in tests/golden/;
+ *   - the FFT stage belongs to FFTW3 (single precision, version unpinned by the
+ *     reference, absent from this image): it is restated as the exact DFT
+ *     (double-precision radix-2, rounded to float) and pinned against numpy's
+ *     pocketfft in float64.
+ *
+ * Complex layout: interleaved {float re, float im} -- identical to the
+ * reference's complexF (ShMemSymBuff.hpp:86-89), cuFloatComplex and
+ * hipFloatComplex.
+ */
+#ifndef OFDM_ORACLE_H_
+#define OFDM_ORACLE_H_
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct { float re, im; } oracle_cf32;
+
+/* matrix_readX rotation (cpuLS.hpp:105-112): X[j] = raw[(j + (K+1)/2) mod K]
+ * for odd K (literal memmove semantics for any K). */
+void oracle_pilot_rotate(const oracle_cf32 *raw, int K, oracle_cf32 *X);
+
+/* shiftOneRow (cpuLS.hpp:135-149) on one row of K values, in place. */
+void oracle_shift_one_row(oracle_cf32 *row, int K);
+
+/* fftOneRow (cpuLS.hpp:165-174): unnormalised forward DFT (sign -1), in place,
+ * on one row of C values.  inverse!=0 gives the unnormalised backward DFT
+ * (ifftOneRow, cpuLS.hpp:152-162).  C must be a power of two. */
+void oracle_fft_row(oracle_cf32 *row, int C, int inverse);
+
+/* firstVector post-FFT part (cpuLS.hpp:290-311): drop DC, divideOneRow,
+ * conjugate, findDistSqrd.  Yfft: R x C (already FFT'd), X: K rotated pilots.
+ * Outputs Hconj: R x K, Hsqrd: K floats (the reference keeps it in X[j].real). */
+void oracle_ls(const oracle_cf32 *Yfft, const oracle_cf32 *X, int R, int C,
+               oracle_cf32 *Hconj, float *Hsqrd);
+
+/* doOneSymbol post-FFT part (cpuLS.hpp:354-368): drop DC, matrixMultThenSum,
+ * divide by Hsqrd, shiftOneRow.  out: K values. */
+void oracle_mrc(const oracle_cf32 *Yfft, const oracle_cf32 *Hconj,
+                const float *Hsqrd, int R, int C, oracle_cf32 *out);
+
+/* MRC numerator only (matrixMultThenSum, cpuLS.hpp:187-208), bins j=0..K-1,
+ * for antennas [0, R): used to check the antenna-split partial path. */
+void oracle_mrc_numerator(const oracle_cf32 *Yfft, const oracle_cf32 *Hconj,
+                          int R, int C, oracle_cf32 *num);
+
+/* One frame, time-domain input (firstVector + doOneSymbol loop,
+ * cpuLS_main.cpp:80-92, with symbol 0 read as the pilot as gpuLS::firstVector
+ * does, gpuLS.cu:359): iq is S symbols x R rows x (C+prefix) samples; the
+ * cyclic prefix is dropped as ShMemSymBuff::readNextSymbol does
+ * (ShMemSymBuff.hpp:281-322).  out: (S-1) x K.  Hconj/Hsqrd may be NULL. */
+void oracle_frame_demod(const oracle_cf32 *iq, int S, int R, int C, int prefix,
+                        const oracle_cf32 *X, oracle_cf32 *out,
+                        oracle_cf32 *Hconj, float *Hsqrd);
+
+/* nframes consecutive frames, OpenMP over frames with nthreads threads
+ * (nthreads<=0: OpenMP default).  Used as the timed CPU baseline. */
+void oracle_frames_demod(const oracle_cf32 *iq, long long nframes, int S, int R,
+                         int C, int prefix, const oracle_cf32 *X,
+                         oracle_cf32 *out, int nthreads);
+
+/* Frequency-domain frames (FFT already applied, no prefix): pilot + (S-1)
+ * data symbols of R x C each.  OpenMP over frames. */
+void oracle_frames_demod_freq(const oracle_cf32 *yf, long long nframes, int S,
+                              int R, int C, const oracle_cf32 *X,
+                              oracle_cf32 *out, int nthreads);
+
+int oracle_max_threads(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

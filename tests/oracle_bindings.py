@@ -1,0 +1,166 @@
+"""ctypes bindings for the CPU oracle (oracle/) and the reference build
+(oracle/_ref/).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg -- never by the product package.
+"""
+import ctypes
+import os
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(ROOT, "oracle", "_build", "libofdm_oracle.so")
+REF_SO = os.path.join(ROOT, "oracle", "_ref", "libref_cpuls.so")
+
+_c = ctypes
+_P = _c.c_void_p
+
+
+def _ptr(a):
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(_P)
+
+
+def c64(a):
+    return np.ascontiguousarray(a, dtype=np.complex64)
+
+
+class Oracle:
+    """CPU restatement of cpuLS.hpp (see oracle/ofdm_oracle.h)."""
+
+    def __init__(self, path=ORACLE_SO):
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"{path} missing: run `make -C oracle`")
+        L = self.lib = _c.CDLL(path)
+        L.oracle_pilot_rotate.argtypes = [_P, _c.c_int, _P]
+        L.oracle_shift_one_row.argtypes = [_P, _c.c_int]
+        L.oracle_fft_row.argtypes = [_P, _c.c_int, _c.c_int]
+        L.oracle_ls.argtypes = [_P, _P, _c.c_int, _c.c_int, _P, _P]
+        L.oracle_mrc.argtypes = [_P, _P, _P, _c.c_int, _c.c_int, _P]
+        L.oracle_mrc_numerator.argtypes = [_P, _P, _c.c_int, _c.c_int, _P]
+        L.oracle_frame_demod.argtypes = [_P, _c.c_int, _c.c_int, _c.c_int, _c.c_int,
+                                         _P, _P, _P, _P]
+        L.oracle_frames_demod.argtypes = [_P, _c.c_longlong, _c.c_int, _c.c_int,
+                                          _c.c_int, _c.c_int, _P, _P, _c.c_int]
+        L.oracle_frames_demod_freq.argtypes = [_P, _c.c_longlong, _c.c_int, _c.c_int,
+                                               _c.c_int, _P, _P, _c.c_int]
+        L.oracle_max_threads.restype = _c.c_int
+
+    def pilot_rotate(self, raw):
+        raw = c64(raw)
+        X = np.empty_like(raw)
+        self.lib.oracle_pilot_rotate(_ptr(raw), raw.size, _ptr(X))
+        return X
+
+    def shift_one_row(self, row):
+        row = c64(row).copy()
+        self.lib.oracle_shift_one_row(_ptr(row), row.size)
+        return row
+
+    def fft_rows(self, rows, inverse=False):
+        rows = c64(rows).copy()
+        C = rows.shape[-1]
+        flat = rows.reshape(-1, C)
+        for i in range(flat.shape[0]):
+            self.lib.oracle_fft_row(flat[i:].ctypes.data_as(_P), C, int(inverse))
+        return rows
+
+    def ls(self, Yfft, X):
+        Yfft, X = c64(Yfft), c64(X)
+        R, C = Yfft.shape
+        H = np.empty((R, C - 1), np.complex64)
+        P = np.empty(C - 1, np.float32)
+        self.lib.oracle_ls(_ptr(Yfft), _ptr(X), R, C, _ptr(H), _ptr(P))
+        return H, P
+
+    def mrc(self, Yfft, H, P):
+        Yfft, H = c64(Yfft), c64(H)
+        P = np.ascontiguousarray(P, np.float32)
+        R, C = Yfft.shape
+        out = np.empty(C - 1, np.complex64)
+        self.lib.oracle_mrc(_ptr(Yfft), _ptr(H), _ptr(P), R, C, _ptr(out))
+        return out
+
+    def mrc_numerator(self, Yfft, H):
+        Yfft, H = c64(Yfft), c64(H)
+        R, C = Yfft.shape
+        out = np.empty(C - 1, np.complex64)
+        self.lib.oracle_mrc_numerator(_ptr(Yfft), _ptr(H), R, C, _ptr(out))
+        return out
+
+    def frame_demod(self, iq, X, prefix=0):
+        """iq: (S, R, C+prefix) time domain -> (out (S-1,K), H (R,K), P (K,))."""
+        iq, X = c64(iq), c64(X)
+        S, R, Cp = iq.shape
+        C = Cp - prefix
+        out = np.empty((S - 1, C - 1), np.complex64)
+        H = np.empty((R, C - 1), np.complex64)
+        P = np.empty(C - 1, np.float32)
+        self.lib.oracle_frame_demod(_ptr(iq), S, R, C, prefix, _ptr(X), _ptr(out),
+                                    _ptr(H), _ptr(P))
+        return out, H, P
+
+    def frames_demod(self, iq, X, prefix=0, nthreads=0):
+        """iq: (F, S, R, C+prefix) -> (F, S-1, K)."""
+        iq, X = c64(iq), c64(X)
+        F, S, R, Cp = iq.shape
+        C = Cp - prefix
+        out = np.empty((F, S - 1, C - 1), np.complex64)
+        self.lib.oracle_frames_demod(_ptr(iq), F, S, R, C, prefix, _ptr(X), _ptr(out),
+                                     nthreads)
+        return out
+
+    def frames_demod_freq(self, yf, X, nthreads=0):
+        yf, X = c64(yf), c64(X)
+        F, S, R, C = yf.shape
+        out = np.empty((F, S - 1, C - 1), np.complex64)
+        self.lib.oracle_frames_demod_freq(_ptr(yf), F, S, R, C, _ptr(X), _ptr(out),
+                                          nthreads)
+        return out
+
+    def max_threads(self):
+        return self.lib.oracle_max_threads()
+
+
+class Reference:
+    """The reference's own RX arithmetic compiled from /root/reference
+    (oracle/build_ref.sh).  Absent on the GPU box."""
+
+    def __init__(self, path=REF_SO):
+        if not os.path.exists(path):
+            raise FileNotFoundError(path)
+        L = self.lib = _c.CDLL(path)
+        L.ref_matrix_readX.argtypes = [_P, _c.c_int, _c.c_char_p]
+        L.ref_shift_one_row.argtypes = [_P, _c.c_int]
+        L.ref_ls_post_fft.argtypes = [_P, _P, _c.c_int, _c.c_int, _P, _P]
+        L.ref_mrc_post_fft.argtypes = [_P, _P, _P, _c.c_int, _c.c_int, _P]
+
+    def matrix_readX(self, path, K):
+        X = np.zeros(K, np.complex64)
+        self.lib.ref_matrix_readX(_ptr(X), K, path.encode())
+        return X
+
+    def shift_one_row(self, row):
+        row = c64(row).copy()
+        self.lib.ref_shift_one_row(_ptr(row), row.size)
+        return row
+
+    def ls(self, Yfft, X):
+        Yfft, X = c64(Yfft), c64(X).copy()
+        R, C = Yfft.shape
+        H = np.empty((R, C - 1), np.complex64)
+        P = np.empty(C - 1, np.float32)
+        self.lib.ref_ls_post_fft(_ptr(Yfft), _ptr(X), R, C, _ptr(H), _ptr(P))
+        return H, P
+
+    def mrc(self, Yfft, H, P):
+        Yfft, H = c64(Yfft), c64(H).copy()
+        P = np.ascontiguousarray(P, np.float32)
+        R, C = Yfft.shape
+        out = np.empty(C - 1, np.complex64)
+        self.lib.ref_mrc_post_fft(_ptr(Yfft), _ptr(H), _ptr(P), R, C, _ptr(out))
+        return out
+
+
+def reference_available():
+    return os.path.exists(REF_SO)

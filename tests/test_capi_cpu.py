@@ -1,0 +1,75 @@
+"""CPU-side checks of the C ABI library: it loads, exports every symbol that
+include/ofdm_lsmrc.h declares, its host functions match the oracle, and its
+argument validation fails loudly before touching any device."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+from helpers import GOLDEN
+
+
+def test_library_exports_header(ofdm):
+    names = ofdm.header_symbols()
+    assert len(names) >= 16, names
+    L = ofdm.lib()
+    for n in names:
+        assert hasattr(L, n), f"{n} declared in include/ofdm_lsmrc.h but not exported"
+    # and the binding's signature table covers the header exactly
+    assert set(names) == set(ofdm._SIGS), set(names) ^ set(ofdm._SIGS)
+    assert L.ofdm_version() == 1
+
+
+def test_pilot_rotate_matches_oracle(ofdm, oracle):
+    for K in (3, 255, 1023, 4095):
+        raw = (np.arange(K) - 1j * np.arange(K)).astype(np.complex64)
+        assert np.array_equal(ofdm.pilot_rotate(raw), oracle.pilot_rotate(raw))
+
+
+def test_read_pilots_file_and_missing(ofdm, tmp_path):
+    X, fill = ofdm.read_pilots(os.path.join(GOLDEN, "Pilots.dat"), 1023)
+    assert not fill
+    assert np.array_equal(X, np.load(os.path.join(GOLDEN, "pilots_rotated_k1023.npy")))
+    # missing file: reference fills 0.707+0.707i on the CPU path (cpuLS.hpp:84-90)
+    # and 1+1i on the GPU path (gpuLS.cu:57-63)
+    X, fill = ofdm.read_pilots(str(tmp_path / "nope.dat"), 7, 0.707)
+    assert fill and np.all(X == np.complex64(0.707 + 0.707j))
+    X, fill = ofdm.read_pilots(str(tmp_path / "nope.dat"), 7, 1.0)
+    assert fill and np.all(X == np.complex64(1 + 1j))
+
+
+def test_argument_validation_without_device(ofdm):
+    L = ofdm.lib()
+    P = ctypes.c_void_p
+    fake = P(4096)  # never dereferenced: validation rejects first
+    # unsupported FFT size
+    assert L.ofdm_fft_rows(fake, fake, 1, 1000, 0, None) == -3
+    assert b"power of two" in L.ofdm_last_error()
+    # null pointers
+    assert L.ofdm_ls_estimate(None, fake, 4, 1024, fake, fake, None) == -1
+    # frame shape errors
+    assert L.ofdm_frame_demod(fake, 1, 1, 4, 1024, 0, fake, fake, 1 << 30, fake, None) == -1
+    assert L.ofdm_frame_demod(fake, 1, 2, 0, 1024, 0, fake, fake, 1 << 30, fake, None) == -1
+    assert L.ofdm_frame_demod(fake, 1, 2, 4, 1024, 2000, fake, fake, 1 << 30, fake, None) == -1
+    # misaligned input
+    assert L.ofdm_frame_demod(P(4104), 1, 2, 4, 1024, 0, fake, fake, 1 << 30, fake, None) == -1
+    assert b"aligned" in L.ofdm_last_error()
+    # workspace too small
+    need = L.ofdm_frame_workspace_bytes(10, 11, 64, 1024)
+    assert need >= 10 * 64 * 1024 * 8
+    assert L.ofdm_frame_demod(fake, 10, 11, 64, 1024, 0, fake, fake, need - 1, fake, None) == -1
+    assert b"workspace" in L.ofdm_last_error()
+    # zero frames is a no-op success (nothing launched)
+    assert L.ofdm_frame_demod(fake, 0, 11, 64, 1024, 0, fake, fake, need, fake, None) == 0
+
+
+def test_workspace_sizes(ofdm):
+    # fused C=1024: Hc [F][R][C] + P [F][C], no staging
+    F, S, R, C = 100, 101, 16, 1024
+    b = ofdm.workspace_bytes(F, S, R, C)
+    assert b == F * R * C * 8 + F * C * 4
+    # non-fused C carries a bounded staging buffer (<= 256 MiB or one frame)
+    b2 = ofdm.workspace_bytes(F, S, 64, 2048)
+    assert b2 - (F * 64 * 2048 * 8 + F * 2048 * 4) <= max(256 << 20, S * 64 * 2048 * 8) + 512
+    assert ofdm.workspace_bytes(F, S, R, 1000) == 0
