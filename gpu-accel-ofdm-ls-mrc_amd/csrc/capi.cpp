@@ -80,8 +80,8 @@ int carve(void *d_ws, size_t bytes, long long F, int S, int R, int C, bool need_
 
 int check_frame_args(const void *in, long long F, int S, int R, int C, int prefix,
                      const void *out, const char *fn) {
-    if (!in || !out) return fail(OFDM_E_ARG, "%s: null pointer", fn);
     if (F < 0) return fail(OFDM_E_ARG, "%s: nframes < 0", fn);
+    if (F > 0 && (!in || !out)) return fail(OFDM_E_ARG, "%s: null pointer", fn);
     if (S < 2) return fail(OFDM_E_ARG, "%s: S=%d, a frame needs a pilot and >= 1 data symbol", fn, S);
     if (R < 1) return fail(OFDM_E_ARG, "%s: R=%d < 1", fn, R);
     if (!pow2_c(C)) return fail(OFDM_E_UNSUPPORTED, "%s: C=%d not a power of two in [4, 4096]", fn, C);

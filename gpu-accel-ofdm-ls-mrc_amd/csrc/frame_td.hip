@@ -8,26 +8,38 @@
 //
 //   k_ls_td1024  one workgroup per frame: FFT the pilot rows (symbol 0),
 //                Hc = conj(Y/X) stored bin-indexed [F][R][C], P = sum_r |Hc|^2.
-//   k_mrc_td1024 one half-wave (32 lanes) per data symbol: for every antenna
-//                row, a 1024-point FFT as 32 x 32 (in-register radix-2 32-point
-//                FFTs, one LDS transpose), then acc += Y * Hc in registers;
+//   k_mrc_td1024 one wave (64 lanes) per data symbol: for every antenna row a
+//                1024-point FFT in registers + one LDS transpose, then
+//                acc += Y * Hc in registers (next row and its Hc prefetched);
 //                finally acc / P stored at the rotated output position.
 //
-// 1024-point FFT on 32 lanes (four-step): lane l holds x[l + 32 m], m < 32.
-//   A[l][k2] = FFT32_m(x[l + 32 m]) * W1024^(l k2)
-//   X[k2 + 32 k1] = FFT32_l(A[l][k2])      (after an LDS transpose lane = k2)
-// so lane l finally owns bins b = l + 32 k1, k1 < 32.
+// 1024-point FFT on one wave (four-step, N = 64 x 16): lane t holds
+// x[t + 64 m], m < 16.
+//   A[t][k2]  = FFT16_m(x[t + 64 m]) * W1024^(t k2)                 k2 < 16
+//   X[k2 + 16 k1] = DFT64_t(A[t][k2])                                k1 < 64
+// The 64-point DFTs run on lane quads after an LDS transpose: lane
+// t = 4 q + a (q = k2, a < 4) holds A[a + 4 l'][q], l' < 16, and
+//   B_a[k'] = FFT16_l'(A[a + 4 l'][q]) * W64^(a k')                   k' < 16
+//   X[q + 16 (k' + 16 c)] = sum_a B_a[k'] W4^(a c)                    c < 4
+// the last sum being a radix-2 x 2 exchange inside the quad (DPP).  Lane
+// (q, a) finally owns bins b = q + 256 c(a) + 16 k', c(a) = (a >> 1) + 2 (a & 1).
 #include "common.hpp"
 #include "launch.hpp"
+
+#include <stdlib.h>
 
 namespace ofdm {
 namespace td1024 {
 
 constexpr int C = 1024;
 constexpr int K = C - 1;
-constexpr int TP = 33;            // padded pitch of 32x32 transposes (bank-conflict free)
-constexpr int TBUF = 32 * TP;     // float2 per half-wave transpose region
-constexpr int TWBUF = 32 * TP;    // block twiddle table W1024^(l*k2), [l][k2]
+constexpr int TP = 68;              // pitch of the [16][64] transpose image (conflict free)
+constexpr int TBUF = 16 * TP;       // float2 per wave
+constexpr int TW1P = 17;            // pitch of TW1[t][k2] = W1024^(t k2)
+constexpr int TW1BUF = 64 * TW1P;
+constexpr int TW2P = 17;            // pitch of TW2[a][k'] = g(a) W64^(a k'): 4 rows on 4 banks
+constexpr int TW2BUF = 4 * TW2P;
+constexpr int TWBUF = TW1BUF + TW2BUF;
 
 __device__ __forceinline__ void wave_lds_sync() {
     // LDS operations of one wave execute in order; this only stops the
@@ -37,155 +49,321 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Quad-DFT signs (found by exhaustive search, verified in tests): lane a of a
+// quad pre-scales its B_a by g(a) (folded into TW2) so that both radix-2
+// stages are one fma(dpp(x), S, x) per float with exact results:
+//   g = (1,-1,-1,1), S1 = (-1,-1,1,1) [partner a^2], S2 = (-1,1,-1,1) [a^1],
+//   lane 3 multiplies by -i between the stages.
+__device__ __forceinline__ float quad_g(int a) { return (a == 0 || a == 3) ? 1.f : -1.f; }
+
 __device__ __forceinline__ void fill_twiddles(float2 *tw) {
-    for (int i = threadIdx.x; i < TWBUF; i += blockDim.x) {
-        const int l = i / TP, k2 = i % TP;
-        tw[i] = k2 < 32 ? g_tw[((l * k2) & (C - 1)) * (OFDM_TW_N / C)] : float2{0.f, 0.f};
+    for (int i = threadIdx.x; i < TW1BUF; i += blockDim.x) {
+        const int t = i / TW1P, k2 = i % TW1P;
+        tw[i] = k2 < 16 ? g_tw[((t * k2) & (C - 1)) * (OFDM_TW_N / C)] : float2{0.f, 0.f};
+    }
+    for (int i = threadIdx.x; i < TW2BUF; i += blockDim.x) {
+        const int a = i / TW2P, k = i % TW2P;
+        const float2 w = g_tw[((16 * a * k) & (C - 1)) * (OFDM_TW_N / C)];
+        const float g = quad_g(a);
+        tw[TW1BUF + i] = k < 16 ? float2{g * w.x, g * w.y} : float2{0.f, 0.f};
     }
 }
 
-// Forward 1024-point FFT of one row by the 32 lanes of a half-wave.
-// src: first sample of the row (cyclic prefix already skipped).
-// On return x[k1] = X[l + 32 k1].
-__device__ __forceinline__ void row_fft(const float2 *__restrict__ src, int l, float2 *T,
-                                        const float2 *tw, float2 (&x)[32]) {
-    float2 a[32];
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL,
+                                                              0xF, 0xF, true));
+}
+constexpr int DPP_XOR1 = 0xB1;  // quad_perm [1,0,3,2]
+constexpr int DPP_XOR2 = 0x4E;  // quad_perm [2,3,0,1]
+
+// a[m] = src[t + 64 m]: 16 coalesced 512-byte wave loads.  NT: non-temporal
+// (streamed once; keeps L2 for the per-frame channel estimates).
+template <bool NT = false>
+__device__ __forceinline__ void row_load(const float2 *__restrict__ src, int t, float2 (&a)[16]) {
+    if (NT) {
+        const unsigned long long *p = reinterpret_cast<const unsigned long long *>(src) + t;
 #pragma unroll
-    for (int m = 0; m < 32; ++m) a[m] = src[l + 32 * m];
-    fft_reg<32, false>(a);
+        for (int m = 0; m < 16; ++m)
+            a[m] = __builtin_bit_cast(float2, __builtin_nontemporal_load(p + 64 * m));
+    } else {
 #pragma unroll
-    for (int k2 = 1; k2 < 32; ++k2) a[k2] = cmul(a[k2], tw[l * TP + k2]);
+        for (int m = 0; m < 16; ++m) a[m] = src[t + 64 * m];
+    }
+}
+
+// v[k] = dpp(v[k]) * S + v[k] for 16 floats, one v_fmac_f32_dpp each (the
+// compiler would emit v_mov_dpp + fma + an s_nop per value).  The leading
+// s_nop 1 covers the "VALU writes VGPR -> DPP reads it" hazard (2 wait states)
+// for whatever the compiler computed last; inside the block no instruction
+// reads another's output (cdna_hip_programming.md 5.7).
+#define OFDM_DPP_Q(CTRL) "quad_perm:" CTRL " row_mask:0xf bank_mask:0xf"
+template <int CTRL>
+__device__ __forceinline__ void quad_fmac_dpp(float (&v)[16], float S) {
+#define OFDM_F(i) "v_fmac_f32_dpp %" #i ", %" #i ", %16 " OFDM_DPP_Q(QP) "\n\t"
+    if constexpr (CTRL == 0x4E) {
+#define QP "[2,3,0,1]"
+        asm("s_nop 1\n\t" OFDM_F(0) OFDM_F(1) OFDM_F(2) OFDM_F(3) OFDM_F(4) OFDM_F(5) OFDM_F(6)
+                OFDM_F(7) OFDM_F(8) OFDM_F(9) OFDM_F(10) OFDM_F(11) OFDM_F(12) OFDM_F(13) OFDM_F(14)
+                    OFDM_F(15)
+            : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),
+              "+v"(v[7]), "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]),
+              "+v"(v[13]), "+v"(v[14]), "+v"(v[15])
+            : "v"(S));
+#undef QP
+    } else {
+        static_assert(CTRL == 0xB1, "quad xor 1 or xor 2");
+#define QP "[1,0,3,2]"
+        asm("s_nop 1\n\t" OFDM_F(0) OFDM_F(1) OFDM_F(2) OFDM_F(3) OFDM_F(4) OFDM_F(5) OFDM_F(6)
+                OFDM_F(7) OFDM_F(8) OFDM_F(9) OFDM_F(10) OFDM_F(11) OFDM_F(12) OFDM_F(13) OFDM_F(14)
+                    OFDM_F(15)
+            : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),
+              "+v"(v[7]), "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]),
+              "+v"(v[13]), "+v"(v[14]), "+v"(v[15])
+            : "v"(S));
+#undef QP
+    }
+#undef OFDM_F
+}
+#undef OFDM_DPP_Q
+
+// Forward 1024-point FFT of the row held in a[] (see header); T is this
+// wave's transpose region.  On return x[k'] = X[b0 + 16 k'],
+// b0 = (t >> 2) + 256 c(t & 3).
+__device__ __forceinline__ void row_fft(float2 (&a)[16], int t, float2 *T, const float2 *tw,
+                                        float2 (&x)[16]) {
+    fft_reg<16, false>(a);
 #pragma unroll
-    for (int k2 = 0; k2 < 32; ++k2) T[k2 * TP + l] = a[k2];
+    for (int k2 = 1; k2 < 16; ++k2) a[k2] = cmul(a[k2], tw[t * TW1P + k2]);
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2) T[k2 * TP + t] = a[k2];
     wave_lds_sync();
+    const int q = t >> 2, qa = t & 3;
 #pragma unroll
-    for (int i = 0; i < 32; ++i) x[i] = T[l * TP + i];
+    for (int l = 0; l < 16; ++l) x[l] = T[q * TP + qa + 4 * l];
     wave_lds_sync();
-    fft_reg<32, false>(x);
+    fft_reg<16, false>(x);
+    const float2 *tw2 = tw + TW1BUF + qa * TW2P;
+    const float g = quad_g(qa);
+    x[0] = float2{g * x[0].x, g * x[0].y};
+#pragma unroll
+    for (int k = 1; k < 16; ++k) x[k] = cmul(x[k], tw2[k]);
+    // 4-point DFT over the quad: two radix-2 stages, one fma per float each
+    const float S1 = (qa & 2) ? 1.f : -1.f;
+    const float S2 = (qa & 1) ? 1.f : -1.f;
+    // lanes with qa == 3 multiply by -i between the stages: (x, y) -> (y, -x)
+    const unsigned long long rot = __builtin_amdgcn_ballot_w64(qa == 3);
+    float xr[16], xi[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) { xr[k] = x[k].x; xi[k] = x[k].y; }
+    quad_fmac_dpp<DPP_XOR2>(xr, S1);
+    quad_fmac_dpp<DPP_XOR2>(xi, S1);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        float nx;
+        asm("v_cndmask_b32_e64 %0, %2, %3, %4\n\tv_cndmask_b32_e64 %1, %3, -%2, %4"
+            : "=&v"(nx), "=v"(xi[k])
+            : "v"(xr[k]), "v"(xi[k]), "s"(rot));
+        xr[k] = nx;
+    }
+    quad_fmac_dpp<DPP_XOR1>(xr, S2);
+    quad_fmac_dpp<DPP_XOR1>(xi, S2);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) x[k] = float2{xr[k], xi[k]};
+}
+
+__device__ __forceinline__ int lane_bin0(int t) {
+    const int qa = t & 3;
+    return (t >> 2) + 256 * ((qa >> 1) + 2 * (qa & 1));
+}
+
+// Channel estimates of one (frame, antenna row) in "lane order": the 16 bins
+// lane t owns (b0(t) + 16 k) as 8 float4 pairs, pair i of lane t at float4
+// index i*64 + t -- one contiguous 1 KiB wave load per pair.  Same 8 KiB per
+// row as the bin layout; written by k_ls_td1024, read by k_mrc_td1024.
+__device__ __forceinline__ void hc_store(float4 *__restrict__ dst, int t, const float2 (&h)[16]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        dst[i * 64 + t] = float4{h[2 * i].x, h[2 * i].y, h[2 * i + 1].x, h[2 * i + 1].y};
+}
+__device__ __forceinline__ void hc_load(const float4 *__restrict__ src, int t, float2 (&h)[16]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const float4 v = src[i * 64 + t];
+        h[2 * i] = float2{v.x, v.y};
+        h[2 * i + 1] = float2{v.z, v.w};
+    }
 }
 
 // ---------------------------------------------------------------------------
-// LS: one workgroup (4 waves = 8 half-waves) per frame; half-wave h takes
-// antenna rows h, h+8, ...; partial |H|^2 sums are combined in half-wave
-// order through LDS (deterministic).
-// partial != 0: antenna-split mode (P is a partial sum, DC slot 0).
+// LS: one workgroup (4 waves) per frame; wave w takes antenna rows w, w+4, ...
+// and keeps a partial |H|^2 per bin; partials are added in wave order through
+// LDS (deterministic).  partial != 0: antenna-split mode (DC slot of P = 0).
+// P is written bin-indexed [F][C]; Hc lane-ordered [F][R][8][64] float4.
 // ---------------------------------------------------------------------------
+constexpr int LS_WAVES = 4;
+
 __global__ void __launch_bounds__(256) k_ls_td1024(const float2 *__restrict__ iq, int S, int R,
                                                    int prefix, const float2 *__restrict__ X,
                                                    float2 *__restrict__ Hc, float *__restrict__ P,
                                                    int partial) {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     float2 *tw = lds;
-    const int half = threadIdx.x >> 5;  // 0..7
-    const int l = threadIdx.x & 31;
-    float2 *T = lds + TWBUF + half * TBUF;
+    const int w = threadIdx.x >> 6;
+    const int t = threadIdx.x & 63;
+    float2 *T = lds + TWBUF + w * TBUF;
     fill_twiddles(tw);
     __syncthreads();
 
     const long long f = blockIdx.x;
     const int Cp = C + prefix;
-    const float2 *pilot = iq + f * (long long)S * R * Cp;
-    float2 *Hf = Hc + f * (long long)R * C;
-    float p[32];
+    const float2 *pilot = iq + f * (long long)S * R * Cp + prefix;
+    float4 *Hf = reinterpret_cast<float4 *>(Hc + f * (long long)R * C);
+    const int b0 = lane_bin0(t);
+    float2 xp[16];  // rotated pilots of this lane's subcarriers
 #pragma unroll
-    for (int k1 = 0; k1 < 32; ++k1) p[k1] = 0.f;
-    // pilots of this lane's subcarriers: bin b = l + 32 k1 -> j = b - 1
-    for (int r = half; r < R; r += 8) {
-        float2 x[32];
-        row_fft(pilot + (long long)r * Cp + prefix, l, T, tw, x);
-        float2 *hr = Hf + (long long)r * C;
+    for (int k = 0; k < 16; ++k) {
+        const int b = b0 + 16 * k;
+        xp[k] = b > 0 ? X[b - 1] : float2{1.f, 0.f};
+    }
+    float p[16];
 #pragma unroll
-        for (int k1 = 0; k1 < 32; ++k1) {
-            const int b = l + 32 * k1;
-            float2 h{0.f, 0.f};
-            if (b > 0) h = ls_conj(x[k1], X[b - 1]);
-            hr[b] = h;
-            p[k1] = p[k1] + (h.x * h.x) + (h.y * h.y);
+    for (int k = 0; k < 16; ++k) p[k] = 0.f;
+    for (int r = w; r < R; r += LS_WAVES) {
+        float2 a[16], x[16];
+        row_load(pilot + (long long)r * Cp, t, a);
+        row_fft(a, t, T, tw, x);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            float2 h = ls_conj(x[k], xp[k]);
+            if (b0 + 16 * k == 0) h = float2{0.f, 0.f};
+            x[k] = h;
+            p[k] = p[k] + (h.x * h.x) + (h.y * h.y);
         }
+        hc_store(Hf + (long long)r * (C / 2), t, x);
     }
     __syncthreads();
-    // partial sums -> LDS [half][bin] (reuses the transpose regions)
-    float *pp = reinterpret_cast<float *>(lds + TWBUF);
+    float *pp = reinterpret_cast<float *>(lds + TWBUF);  // [LS_WAVES][C], reuses T
 #pragma unroll
-    for (int k1 = 0; k1 < 32; ++k1) pp[half * C + l + 32 * k1] = p[k1];
+    for (int k = 0; k < 16; ++k) pp[w * C + b0 + 16 * k] = p[k];
     __syncthreads();
     float *Pf = P + f * C;
     for (int b = threadIdx.x; b < C; b += blockDim.x) {
-        float s = pp[b];
-        for (int h = 1; h < 8; ++h) s = s + pp[h * C + b];
-        Pf[b] = b == 0 ? (partial ? 0.f : 1.f) : s;
+        float sum = pp[b];
+        for (int i = 1; i < LS_WAVES; ++i) sum = sum + pp[i * C + b];
+        Pf[b] = b == 0 ? (partial ? 0.f : 1.f) : sum;
     }
 }
 
 // ---------------------------------------------------------------------------
-// MRC: workgroup = 4 waves = 8 half-waves = 8 consecutive data symbols.
+// MRC: workgroup = WAVES waves = WAVES consecutive data symbols, one per wave.
 // Workgroups are remapped so that consecutive symbols (which share a frame's
 // Hc) land on the same XCD (blocks b and b+8 share an XCD under round-robin
 // dispatch; speed only, never correctness).
 // mode 0: out[q][out_pos(j)] = acc / P;  mode 1: out[q][j] = acc (numerator)
+// Row-loop schedules (A/B-selectable at run time, OFDM_MRC_SCHED):
+//   0 PREFETCH_COPY  next row loaded into a second buffer, copied at the top
+//   1 NOPREFETCH     load, then compute (latency hidden by other waves)
 // ---------------------------------------------------------------------------
-constexpr int MRC_WAVES = 4;
-constexpr int MRC_SYMS = MRC_WAVES * 2;
+enum { PREFETCH_COPY = 0, NOPREFETCH = 1 };
 
-__global__ void __launch_bounds__(256) k_mrc_td1024(const float2 *__restrict__ iq, int S, int R,
-                                                    int prefix, const float2 *__restrict__ Hc,
-                                                    const float *__restrict__ P,
-                                                    float2 *__restrict__ out, long long nq,
-                                                    long long nblocks, long long per_xcd, int mode) {
+template <bool NT>
+__device__ __forceinline__ void mrc_row(float2 (&a)[16], int t, float2 *T, const float2 *tw,
+                                        const float4 *__restrict__ hr, float2 (&acc)[16]) {
+    float2 h[16], x[16];
+    row_fft(a, t, T, tw, x);
+    // keep the Hc loads (L2 hits) out of the FFT's register peak
+    __builtin_amdgcn_sched_barrier(0);
+    hc_load(hr, t, h);
+    // matrixMultThenSum (cpuLS.hpp:203-204), antennas in order
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        acc[k].x = acc[k].x + (x[k].x * h[k].x - x[k].y * h[k].y);
+        acc[k].y = acc[k].y + (x[k].x * h[k].y + x[k].y * h[k].x);
+    }
+}
+
+template <bool NT, int SCHED, int WAVES>
+__device__ __forceinline__ void mrc_body(const float2 *__restrict__ iq, int S, int R, int prefix,
+                                         const float2 *__restrict__ Hc, const float *__restrict__ P,
+                                         float2 *__restrict__ out, long long nq, long long nblocks,
+                                         long long per_xcd, int mode) {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     float2 *tw = lds;
-    const int half = threadIdx.x >> 5;
-    const int l = threadIdx.x & 31;
-    float2 *T = lds + TWBUF + half * TBUF;
+    const int w = threadIdx.x >> 6;
+    const int t = threadIdx.x & 63;
+    float2 *T = lds + TWBUF + w * TBUF;
     const long long pb = blockIdx.x;
     const long long lb = (pb & 7) * per_xcd + (pb >> 3);  // XCD-grouped logical block
     if (lb >= nblocks) return;
     fill_twiddles(tw);
     __syncthreads();
 
-    long long q = lb * MRC_SYMS + half;
-    const bool active = q < nq;
-    if (!active) q = nq - 1;  // duplicate work, never stored
+    long long q = lb * WAVES + w;
+    if (q >= nq) return;  // whole wave idle; no block-level sync follows
     const int nsym = S - 1;
     const long long f = q / nsym;
     const int s = 1 + (int)(q % nsym);
     const int Cp = C + prefix;
     const float2 *sym = iq + (f * S + s) * (long long)R * Cp + prefix;
-    const float2 *Hf = Hc + f * (long long)R * C;
+    const float4 *Hf = reinterpret_cast<const float4 *>(Hc + f * (long long)R * C);
 
-    float2 acc[32];
+    float2 acc[16];
 #pragma unroll
-    for (int k1 = 0; k1 < 32; ++k1) acc[k1] = float2{0.f, 0.f};
-    for (int r = 0; r < R; ++r) {
-        float2 x[32];
-        row_fft(sym + (long long)r * Cp, l, T, tw, x);
-        const float2 *hr = Hf + (long long)r * C + l;
+    for (int k = 0; k < 16; ++k) acc[k] = float2{0.f, 0.f};
+    if (SCHED == PREFETCH_COPY) {
+        float2 nxt[16];
+        row_load<NT>(sym, t, nxt);
+        for (int r = 0; r < R; ++r) {
+            float2 a[16];
 #pragma unroll
-        for (int k1 = 0; k1 < 32; ++k1) {
-            const float2 h = hr[32 * k1];
-            acc[k1].x = acc[k1].x + (x[k1].x * h.x - x[k1].y * h.y);
-            acc[k1].y = acc[k1].y + (x[k1].x * h.y + x[k1].y * h.x);
+            for (int m = 0; m < 16; ++m) a[m] = nxt[m];
+            if (r + 1 < R) row_load<NT>(sym + (long long)(r + 1) * Cp, t, nxt);
+            mrc_row<NT>(a, t, T, tw, Hf + (long long)r * (C / 2), acc);
+        }
+    } else {
+        for (int r = 0; r < R; ++r) {
+            float2 a[16];
+            row_load<NT>(sym + (long long)r * Cp, t, a);
+            mrc_row<NT>(a, t, T, tw, Hf + (long long)r * (C / 2), acc);
         }
     }
-    if (!active) return;
+    const int b0 = lane_bin0(t);
     float2 *o = out + q * K;
     if (mode == 0) {
-        const float *Pf = P + f * C;
+        const float *Pf = P + f * C + b0;
 #pragma unroll
-        for (int k1 = 0; k1 < 32; ++k1) {
-            const int b = l + 32 * k1;
+        for (int k = 0; k < 16; ++k) {
+            const int b = b0 + 16 * k;
             if (b == 0) continue;
-            const float pv = Pf[b];
-            o[out_pos(b - 1, K)] = float2{acc[k1].x / pv, acc[k1].y / pv};
+            const float pv = Pf[16 * k];
+            o[out_pos(b - 1, K)] = float2{acc[k].x / pv, acc[k].y / pv};
         }
     } else {
 #pragma unroll
-        for (int k1 = 0; k1 < 32; ++k1) {
-            const int b = l + 32 * k1;
-            if (b > 0) o[b - 1] = acc[k1];
+        for (int k = 0; k < 16; ++k) {
+            const int b = b0 + 16 * k;
+            if (b > 0) o[b - 1] = acc[k];
         }
     }
 }
+
+#define OFDM_MRC_ARGS                                                                            \
+    const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,     \
+        const float *__restrict__ P, float2 *__restrict__ out, long long nq, long long nblocks, \
+        long long per_xcd, int mode
+// 4 waves per workgroup: occupancy left to the compiler (LDS: 3 groups/CU)
+template <bool NT, int SCHED>
+__global__ void __launch_bounds__(256) k_mrc_td1024(OFDM_MRC_ARGS) {
+    mrc_body<NT, SCHED, 4>(iq, S, R, prefix, Hc, P, out, nq, nblocks, per_xcd, mode);
+}
+// 8 waves per workgroup, register budget for 4 waves/SIMD (2 groups/CU)
+template <bool NT, int SCHED>
+__global__ void __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 4)))
+k_mrc_td1024_w8(OFDM_MRC_ARGS) {
+    mrc_body<NT, SCHED, 8>(iq, S, R, prefix, Hc, P, out, nq, nblocks, per_xcd, mode);
+}
+#undef OFDM_MRC_ARGS
 
 }  // namespace td1024
 
@@ -193,8 +371,8 @@ hipError_t launch_ls_td1024(const float2 *iq, long long nframes, int S, int R, i
                             const float2 *X, float2 *Hc, float *P, int partial, hipStream_t s) {
     using namespace td1024;
     if (nframes <= 0) return hipSuccess;
-    const size_t lds = (TWBUF + 8 * TBUF) * sizeof(float2);
-    hipLaunchKernelGGL(k_ls_td1024, dim3((unsigned)nframes), dim3(256), lds, s, iq, S, R, prefix, X, Hc,
+    const size_t lds = (TWBUF + LS_WAVES * TBUF) * sizeof(float2);
+    hipLaunchKernelGGL(k_ls_td1024, dim3((unsigned)nframes), dim3(64 * LS_WAVES), lds, s, iq, S, R, prefix, X, Hc,
                        P, partial);
     return hipGetLastError();
 }
@@ -205,13 +383,29 @@ hipError_t launch_mrc_td1024(const float2 *iq, long long nframes, int S, int R, 
     using namespace td1024;
     const long long nq = nframes * (S - 1);
     if (nq <= 0) return hipSuccess;
-    const long long nblocks = (nq + MRC_SYMS - 1) / MRC_SYMS;
+    // A/B switches (defaults = the measured best): OFDM_MRC_NT=0/1 plain /
+    // non-temporal IQ loads, OFDM_MRC_SCHED=0/1 row-loop schedule,
+    // OFDM_MRC_WAVES=4/8 waves per workgroup.
+    static const int nt = [] { const char *e = getenv("OFDM_MRC_NT"); return e ? atoi(e) : 1; }();
+    static const int sched = [] { const char *e = getenv("OFDM_MRC_SCHED"); return e ? atoi(e) : 1; }();
+    static const int waves = [] { const char *e = getenv("OFDM_MRC_WAVES"); return e ? atoi(e) : 8; }();
+    const int W = waves == 4 ? 4 : 8;
+    const long long nblocks = (nq + W - 1) / W;
     const long long per_xcd = (nblocks + 7) / 8;
     const long long grid = per_xcd * 8;
     if (grid > 0x7fffffffll) return hipErrorInvalidValue;
-    const size_t lds = (TWBUF + MRC_SYMS * TBUF) * sizeof(float2);
-    hipLaunchKernelGGL(k_mrc_td1024, dim3((unsigned)grid), dim3(64 * MRC_WAVES), lds, s, iq, S, R,
-                       prefix, Hc, P, out, nq, nblocks, per_xcd, mode);
+    const size_t lds = (TWBUF + W * TBUF) * sizeof(float2);
+#define OFDM_MRC_LAUNCH(KER, NTV, SV)                                                              \
+    hipLaunchKernelGGL((KER<NTV, SV>), dim3((unsigned)grid), dim3(64 * W), lds, s, iq, S, R, prefix, \
+                       Hc, P, out, nq, nblocks, per_xcd, mode)
+    if (W == 8) {
+        if (nt) { if (sched) OFDM_MRC_LAUNCH(k_mrc_td1024_w8, true, NOPREFETCH); else OFDM_MRC_LAUNCH(k_mrc_td1024_w8, true, PREFETCH_COPY); }
+        else    { if (sched) OFDM_MRC_LAUNCH(k_mrc_td1024_w8, false, NOPREFETCH); else OFDM_MRC_LAUNCH(k_mrc_td1024_w8, false, PREFETCH_COPY); }
+    } else {
+        if (nt) { if (sched) OFDM_MRC_LAUNCH(k_mrc_td1024, true, NOPREFETCH); else OFDM_MRC_LAUNCH(k_mrc_td1024, true, PREFETCH_COPY); }
+        else    { if (sched) OFDM_MRC_LAUNCH(k_mrc_td1024, false, NOPREFETCH); else OFDM_MRC_LAUNCH(k_mrc_td1024, false, PREFETCH_COPY); }
+    }
+#undef OFDM_MRC_LAUNCH
     return hipGetLastError();
 }
 
