@@ -225,6 +225,38 @@ int ofdm_mrc_finalize(const ofdm_cf32 *d_num, long long e0, long long count, int
                      "ofdm_mrc_finalize");
 }
 
+int ofdm_channel_conj_product(const ofdm_cf32 *d_Y, long long nsyms, const ofdm_cf32 *d_Hconj,
+                              int R, int C, ofdm_cf32 *d_prod, ofdm_stream_t stream) {
+    if (!d_Y || !d_Hconj || !d_prod || nsyms < 0 || R < 1)
+        return fail(OFDM_E_ARG, "ofdm_channel_conj_product: bad arguments");
+    if (!pow2_c(C)) return fail(OFDM_E_UNSUPPORTED, "ofdm_channel_conj_product: C=%d unsupported", C);
+    if (nsyms == 0) return OFDM_OK;
+    return hip_check(ofdm::launch_conj_product(F2(d_Y), nsyms, R, C, F2(d_Hconj), F2(d_prod), hs(stream)),
+                     "ofdm_channel_conj_product");
+}
+
+int ofdm_combine_products(const ofdm_cf32 *d_prod, long long nsyms, const float *d_Hsqrd, int R,
+                          int K, int rotate, ofdm_cf32 *d_out, ofdm_stream_t stream) {
+    if (!d_prod || !d_Hsqrd || !d_out || nsyms < 0 || R < 1 || K < 1)
+        return fail(OFDM_E_ARG, "ofdm_combine_products: bad arguments");
+    if (nsyms == 0) return OFDM_OK;
+    return hip_check(ofdm::launch_combine(F2(d_prod), nsyms, R, K, d_Hsqrd, rotate, F2(d_out), hs(stream)),
+                     "ofdm_combine_products");
+}
+
+int ofdm_shift_rows(const ofdm_cf32 *d_in, long long nrows, int K, ofdm_cf32 *d_out,
+                    ofdm_stream_t stream) {
+    if (!d_in || !d_out || nrows < 0 || K < 1 || d_in == d_out)
+        return fail(OFDM_E_ARG, "ofdm_shift_rows: bad arguments (out of place only)");
+    if (nrows == 0) return OFDM_OK;
+    return hip_check(ofdm::launch_shift_rows(F2(d_in), nrows, K, F2(d_out), hs(stream)), "ofdm_shift_rows");
+}
+
+int ofdm_dist_sqrd(const ofdm_cf32 *d_H, int R, int K, float *d_Hsqrd, ofdm_stream_t stream) {
+    if (!d_H || !d_Hsqrd || R < 1 || K < 1) return fail(OFDM_E_ARG, "ofdm_dist_sqrd: bad arguments");
+    return hip_check(ofdm::launch_dist_sqrd(F2(d_H), R, K, d_Hsqrd, hs(stream)), "ofdm_dist_sqrd");
+}
+
 size_t ofdm_frame_workspace_bytes(long long nframes, int S, int R, int C) {
     if (nframes < 0 || S < 2 || R < 1 || !pow2_c(C)) return 0;
     return ws_bytes(nframes, S, R, C, !fused_c(C));

@@ -267,14 +267,24 @@ __global__ void __launch_bounds__(256) k_ls_td1024(const float2 *__restrict__ iq
 // ---------------------------------------------------------------------------
 enum { PREFETCH_COPY = 0, NOPREFETCH = 1 };
 
-template <bool NT>
+template <bool NT, int DBG = 0>
 __device__ __forceinline__ void mrc_row(float2 (&a)[16], int t, float2 *T, const float2 *tw,
                                         const float4 *__restrict__ hr, float2 (&acc)[16]) {
     float2 h[16], x[16];
-    row_fft(a, t, T, tw, x);
+    if (DBG & 1) {  // diagnostic only: same memory traffic, no FFT
+#pragma unroll
+        for (int k = 0; k < 16; ++k) x[k] = a[k];
+    } else {
+        row_fft(a, t, T, tw, x);
+    }
     // keep the Hc loads (L2 hits) out of the FFT's register peak
     __builtin_amdgcn_sched_barrier(0);
-    hc_load(hr, t, h);
+    if (DBG & 2) {  // diagnostic only: no Hc traffic
+#pragma unroll
+        for (int k = 0; k < 16; ++k) h[k] = float2{1.f, (float)k};
+    } else {
+        hc_load(hr, t, h);
+    }
     // matrixMultThenSum (cpuLS.hpp:203-204), antennas in order
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
@@ -283,7 +293,7 @@ __device__ __forceinline__ void mrc_row(float2 (&a)[16], int t, float2 *T, const
     }
 }
 
-template <bool NT, int SCHED, int WAVES>
+template <bool NT, int SCHED, int WAVES, int DBG = 0>
 __device__ __forceinline__ void mrc_body(const float2 *__restrict__ iq, int S, int R, int prefix,
                                          const float2 *__restrict__ Hc, const float *__restrict__ P,
                                          float2 *__restrict__ out, long long nq, long long nblocks,
@@ -325,7 +335,7 @@ __device__ __forceinline__ void mrc_body(const float2 *__restrict__ iq, int S, i
         for (int r = 0; r < R; ++r) {
             float2 a[16];
             row_load<NT>(sym + (long long)r * Cp, t, a);
-            mrc_row<NT>(a, t, T, tw, Hf + (long long)r * (C / 2), acc);
+            mrc_row<NT, DBG>(a, t, T, tw, Hf + (long long)r * (C / 2), acc);
         }
     }
     const int b0 = lane_bin0(t);
@@ -358,10 +368,10 @@ __global__ void __launch_bounds__(256) k_mrc_td1024(OFDM_MRC_ARGS) {
     mrc_body<NT, SCHED, 4>(iq, S, R, prefix, Hc, P, out, nq, nblocks, per_xcd, mode);
 }
 // 8 waves per workgroup, register budget for 4 waves/SIMD (2 groups/CU)
-template <bool NT, int SCHED>
+template <bool NT, int SCHED, int DBG = 0>
 __global__ void __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 4)))
 k_mrc_td1024_w8(OFDM_MRC_ARGS) {
-    mrc_body<NT, SCHED, 8>(iq, S, R, prefix, Hc, P, out, nq, nblocks, per_xcd, mode);
+    mrc_body<NT, SCHED, 8, DBG>(iq, S, R, prefix, Hc, P, out, nq, nblocks, per_xcd, mode);
 }
 #undef OFDM_MRC_ARGS
 
@@ -398,6 +408,18 @@ hipError_t launch_mrc_td1024(const float2 *iq, long long nframes, int S, int R, 
 #define OFDM_MRC_LAUNCH(KER, NTV, SV)                                                              \
     hipLaunchKernelGGL((KER<NTV, SV>), dim3((unsigned)grid), dim3(64 * W), lds, s, iq, S, R, prefix, \
                        Hc, P, out, nq, nblocks, per_xcd, mode)
+    // OFDM_MRC_DEBUG=1|2|3: diagnostic variants (wrong results) pricing the
+    // memory side: 1 = no FFT, 2 = no Hc loads, 3 = neither
+    static const int dbg = [] { const char *e = getenv("OFDM_MRC_DEBUG"); return e ? atoi(e) : 0; }();
+    if (dbg) {
+        const long long nb8 = (nq + 7) / 8, px8 = (nb8 + 7) / 8;
+        const size_t l8 = (TWBUF + 8 * TBUF) * sizeof(float2);
+#define OFDM_DBG(D) hipLaunchKernelGGL((k_mrc_td1024_w8<true, NOPREFETCH, D>), dim3((unsigned)(px8 * 8)), \
+                                       dim3(512), l8, s, iq, S, R, prefix, Hc, P, out, nq, nb8, px8, mode)
+        if (dbg == 1) OFDM_DBG(1); else if (dbg == 2) OFDM_DBG(2); else OFDM_DBG(3);
+#undef OFDM_DBG
+        return hipGetLastError();
+    }
     if (W == 8) {
         if (nt) { if (sched) OFDM_MRC_LAUNCH(k_mrc_td1024_w8, true, NOPREFETCH); else OFDM_MRC_LAUNCH(k_mrc_td1024_w8, true, PREFETCH_COPY); }
         else    { if (sched) OFDM_MRC_LAUNCH(k_mrc_td1024_w8, false, NOPREFETCH); else OFDM_MRC_LAUNCH(k_mrc_td1024_w8, false, PREFETCH_COPY); }

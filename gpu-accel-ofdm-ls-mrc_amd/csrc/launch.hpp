@@ -51,6 +51,14 @@ hipError_t launch_mrc_td1024(const float2 *iq, long long nframes, int S, int R, 
                              const float2 *Hc, const float *P, float2 *out, int mode,
                              hipStream_t s);
 
+// Stage-wise operations of the reference's per-stage gpuLS methods (stages.hip).
+hipError_t launch_conj_product(const float2 *Y, long long nsyms, int R, int C, const float2 *Hc,
+                               float2 *prod, hipStream_t s);
+hipError_t launch_combine(const float2 *prod, long long nsyms, int R, int K, const float *P,
+                          int rotate, float2 *out, hipStream_t s);
+hipError_t launch_shift_rows(const float2 *in, long long nrows, int K, float2 *out, hipStream_t s);
+hipError_t launch_dist_sqrd(const float2 *H, int R, int K, float *P, hipStream_t s);
+
 // Synthetic frames: time-domain (freq_domain=0, rows of C+prefix with a
 // cyclic prefix) or frequency-domain (freq_domain=1, rows of C) IQ.
 hipError_t launch_synth(float2 *iq, long long nframes, int S, int R, int C, int prefix,

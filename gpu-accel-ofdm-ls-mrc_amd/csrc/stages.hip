@@ -1,0 +1,102 @@
+// stages.hip -- the reference's stage-wise GPU operations, for callers of the
+// gpuLS per-stage API (gpuLS.cu:261-293).  The fused kernels (frame_td.hip,
+// lsmrc_freq.hip) never materialise these intermediates; these exist so the
+// individual methods keep their meaning:
+//   k_conj_product   multiplyWithChannelConj (gpuLS.cu:212-233):
+//                    prod[s][r][j] = Y[s][r][j+1] * Hconj[r][j]
+//   k_combine        combineForMRC (gpuLS.cu:236-259) [+ shiftOneRow]:
+//                    out[s][k] = sum_r prod[s][r][j] / Hsqrd[j], antennas in
+//                    order (the reference's shared-memory tree also lacked a
+//                    barrier, gpuLS.cu:245-247)
+//   k_shift_rows     shiftOneRow (gpuLS.cu:109-125), out of place
+//   k_dist_sqrd      findDistSqrd (gpuLS.cu:185-209, cpuLS.hpp:211-228) on an
+//                    arbitrary R x K matrix, rows summed in order
+#include "common.hpp"
+#include "launch.hpp"
+
+namespace ofdm {
+
+__global__ void __launch_bounds__(256) k_conj_product(const float2 *__restrict__ Y, long long rows,
+                                                      int R, int C, const float2 *__restrict__ Hc,
+                                                      float2 *__restrict__ prod) {
+    const int K = C - 1;
+    const long long row = blockIdx.y;  // s * R + r
+    const int r = (int)(row % R);
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < K; j += gridDim.x * blockDim.x)
+        prod[row * K + j] = cmul(Y[row * C + j + 1], Hc[(long long)r * K + j]);
+}
+
+__global__ void __launch_bounds__(256) k_combine(const float2 *__restrict__ prod, int R, int K,
+                                                 const float *__restrict__ P, int rotate,
+                                                 float2 *__restrict__ out) {
+    const long long s = blockIdx.y;
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < K; j += gridDim.x * blockDim.x) {
+        float2 acc = prod[s * R * K + j];
+        for (int r = 1; r < R; ++r) acc = cadd(acc, prod[(s * R + r) * K + j]);
+        const float p = P[j];
+        out[s * K + (rotate ? out_pos(j, K) : j)] = float2{acc.x / p, acc.y / p};
+    }
+}
+
+__global__ void __launch_bounds__(256) k_shift_rows(const float2 *__restrict__ in, int K,
+                                                    float2 *__restrict__ out) {
+    const long long row = blockIdx.y;
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < K; j += gridDim.x * blockDim.x)
+        out[row * K + out_pos(j, K)] = in[row * K + j];
+}
+
+__global__ void __launch_bounds__(256) k_dist_sqrd(const float2 *__restrict__ H, int R, int K,
+                                                   float *__restrict__ P) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= K) return;
+    float p = 0.f;
+    for (int r = 0; r < R; ++r) {
+        const float2 h = H[(long long)r * K + j];
+        p = (r == 0) ? (h.x * h.x) + (h.y * h.y) : p + (h.x * h.x) + (h.y * h.y);
+    }
+    P[j] = p;
+}
+
+static dim3 grid_rows(int K, long long rows) {
+    return dim3((unsigned)((K + 255) / 256), (unsigned)rows);
+}
+
+hipError_t launch_conj_product(const float2 *Y, long long nsyms, int R, int C, const float2 *Hc,
+                               float2 *prod, hipStream_t s) {
+    const long long rows = nsyms * R;
+    // chunks start on symbol boundaries so that r = row % R holds per chunk
+    const long long chunk = (65535 / R) * R;
+    if (chunk == 0) return hipErrorInvalidValue;
+    for (long long r0 = 0; r0 < rows; r0 += chunk) {
+        const long long n = rows - r0 < chunk ? rows - r0 : chunk;
+        hipLaunchKernelGGL(k_conj_product, grid_rows(C - 1, n), dim3(256), 0, s, Y + r0 * C, n, R, C,
+                           Hc, prod + r0 * (C - 1));
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_combine(const float2 *prod, long long nsyms, int R, int K, const float *P,
+                          int rotate, float2 *out, hipStream_t s) {
+    for (long long s0 = 0; s0 < nsyms; s0 += 65535) {
+        const long long n = nsyms - s0 < 65535 ? nsyms - s0 : 65535;
+        hipLaunchKernelGGL(k_combine, grid_rows(K, n), dim3(256), 0, s, prod + s0 * R * K, R, K, P,
+                           rotate, out + s0 * K);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_shift_rows(const float2 *in, long long nrows, int K, float2 *out, hipStream_t s) {
+    for (long long r0 = 0; r0 < nrows; r0 += 65535) {
+        const long long n = nrows - r0 < 65535 ? nrows - r0 : 65535;
+        hipLaunchKernelGGL(k_shift_rows, grid_rows(K, n), dim3(256), 0, s, in + r0 * K, K,
+                           out + r0 * K);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_dist_sqrd(const float2 *H, int R, int K, float *P, hipStream_t s) {
+    hipLaunchKernelGGL(k_dist_sqrd, dim3((K + 255) / 256), dim3(256), 0, s, H, R, K, P);
+    return hipGetLastError();
+}
+
+}  // namespace ofdm

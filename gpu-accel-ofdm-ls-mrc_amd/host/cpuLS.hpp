@@ -1,0 +1,203 @@
+// cpuLS.hpp -- the reference's host-pointer receiver API, run on MI355X.
+//
+// Drop-in for the RX part of the reference's cpuLS.hpp (cpuLS.hpp:55-389):
+// same global names (buffPtr, file, outfile, numTimes, the per-phase timing
+// arrays, buffIter), same free functions and signatures, same buffer
+// ownership (the caller allocates Y [rows x cols], Hconj [rows x (cols-1)],
+// X [cols-1], which firstVector turns into |H|^2 in X[j].real), same output
+// file (Output_cpu.dat: K rotated complex floats appended per data symbol,
+// truncated on the first one).  Behind each call the data is staged to the
+// GPU and computed by the HIP library -- there is no host implementation of
+// the FFT, LS or MRC arithmetic here.
+//
+// Intended semantics are implemented where the reference's code defeats
+// them:
+//   * firstVector reads the pilot (symbol 0) from the ring, as
+//     gpuLS::firstVector does; the reference zeroes Y instead and every output
+//     becomes NaN (cpuLS.hpp:251-272);
+//   * a missing Pilots.dat fills 0.707 + 0.707i, as cpuLS.hpp:84-90 does;
+//   * the FFT plan is not rebuilt per row and doOneSymbol does not leak.
+// The TX-side helpers (ifftShiftOneRow, addPrefix, rotCube, the zero-forcing
+// precoder, modRefSymbol, modOneSymbol; cpuLS.hpp:119-132, 391-529) are not
+// part of the receiver path and are not provided.
+#ifndef _CPULS_HPP_
+#define _CPULS_HPP_
+
+#include <csignal>
+#include <cmath>
+#include <cstdlib>
+#include <ctime>
+#include <fstream>
+#include <string>
+
+#include <vector>
+
+#include "ofdm_engine.hpp"  // before the ring: its config macros are plain identifiers
+#include "CSharedMemSimple.hpp"
+#include "ShMemSymBuff.hpp"
+
+#define fileNameForX "Pilots.dat"
+#ifndef mode
+#define mode 1
+#endif
+
+using namespace std;
+
+// ---- globals of the reference (cpuLS.hpp:61-66, ShMemSymBuff.hpp:62-83) --
+inline ShMemSymBuff *buffPtr = nullptr;
+inline string file = "Output_cpu.dat";
+inline string in_file = "Input_cpu.dat";
+inline int num_syms = 0;
+inline std::ofstream outfile;
+inline int numTimes = 1;
+inline float readT[numberOfSymbolsToTest];
+inline float decode[numberOfSymbolsToTest];
+inline float drop[numberOfSymbolsToTest];
+inline float fft[numberOfSymbolsToTest];
+inline int buffIter = 0;
+
+inline void printOutArr(complexF *a, int rows, int cols) {
+    for (int i = 0; i < rows; i++) {
+        for (int j = 0; j < cols; j++)
+            std::cout << "(" << a[i * cols + j].real << ", " << a[i * cols + j].imag << "), ";
+        std::printf("\n");
+    }
+}
+inline void printInfo() {
+    std::printf("\tSymbol Dimension(w/o prefix) = %d x %d \n", numOfRows, dimension);
+    std::printf("\tPrefix = %d\n", prefix);
+    std::printf("\t# Of Symbols To Test = %d\n", numberOfSymbolsToTest);
+}
+inline complexF findAvgAndVar(float *times, int amt) {
+    float mean = 0.f, var = 0.f;
+    for (int i = 0; i < amt; i++) mean += times[i];
+    mean /= amt;
+    for (int i = 0; i < amt; i++) var += (times[i] - mean) * (times[i] - mean);
+    return complexF{mean, var / amt};
+}
+// (ShMemSymBuff.hpp:149-189; readT comes from the ring object when present)
+inline void printTimes(bool cpu) {
+    float *rt = buffPtr ? buffPtr->readT : readT;
+    complexF rd = findAvgAndVar(rt, numberOfSymbolsToTest);
+    complexF dec = findAvgAndVar(&decode[1], numberOfSymbolsToTest - 1);
+    complexF ff = findAvgAndVar(fft, numberOfSymbolsToTest);
+    std::printf("\t \t Avg Time(s) \t Variance (s^2) \n");
+    std::printf("Read: \t \t %e \t %e \n", rd.real / numTimes, rd.imag / numTimes);
+    std::printf("ChanEst: \t %e \n", decode[0] / numTimes);
+    std::printf("Decode: \t %e \t %e \n", dec.real / numTimes, dec.imag / numTimes);
+    std::printf("FFT: \t \t %e \t %e \n", ff.real / numTimes, ff.imag / numTimes);
+    if (cpu) {
+        complexF dr = findAvgAndVar(buffPtr ? buffPtr->drop : drop, numberOfSymbolsToTest);
+        std::printf("Drop: \t \t %e \t %e \n", dr.real / numTimes, dr.imag / numTimes);
+    }
+}
+inline void storeTimes(bool cpu) {
+    float *rt = buffPtr ? buffPtr->readT : readT;
+    complexF rd = findAvgAndVar(rt, numberOfSymbolsToTest);
+    complexF dec = findAvgAndVar(&decode[1], numberOfSymbolsToTest - 1);
+    complexF ff = findAvgAndVar(fft, numberOfSymbolsToTest);
+    complexF dr = findAvgAndVar(buffPtr ? buffPtr->drop : drop, numberOfSymbolsToTest);
+    const float v[5] = {rd.real / numTimes, decode[0] / numTimes, dec.real / numTimes,
+                        ff.real / numTimes, dr.real / numTimes};
+    std::ofstream out(cpu ? "time_cpu.dat" : "time_gpu.dat", std::ofstream::binary);
+    out.write(reinterpret_cast<const char *>(v), sizeof v);
+}
+
+namespace ofdm_cpuls {
+inline clock_t tic() { return timerEn ? clock() : 0; }
+inline void toc(float *arr, int it, clock_t t0) {
+    if (timerEn && it >= 0 && it < numberOfSymbolsToTest)
+        arr[it] += (float)(clock() - t0) / (float)CLOCKS_PER_SEC;
+}
+}  // namespace ofdm_cpuls
+
+// matrix_readX (cpuLS.hpp:80-117): K pilots from Pilots.dat, rotated
+inline void matrix_readX(complexF *X, int cols) {
+    if (ofdm_read_pilots(fileNameForX, cols, 0.707f, reinterpret_cast<ofdm_cf32 *>(X)) == 1)
+        std::cerr << "Unable to open file data file, filling in 1+i for x\n";
+}
+
+// shiftOneRow (cpuLS.hpp:135-149): output rotation of row `row`
+inline void shiftOneRow(complexF *Y, int cols, int row) {
+    ofdm::HostEngine::get().shift(&Y[(size_t)row * cols], cols);
+}
+
+// fftOneRow / ifftOneRow (cpuLS.hpp:152-174): unnormalised C2C of row `row`
+inline void fftOneRow(complexF *Y, int cols, int row) {
+    ofdm::HostEngine::get().fft_rows(&Y[(size_t)row * cols], 1, cols, 0);
+}
+inline void ifftOneRow(complexF *Y, int cols, int row) {
+    ofdm::HostEngine::get().fft_rows(&Y[(size_t)row * cols], 1, cols, 1);
+}
+
+// numSyms (cpuLS.hpp:176-184): symbols of cols-1 samples in a file
+inline void numSyms(std::string in_file1, int cols) {
+    std::ifstream f(in_file1.c_str(), std::ifstream::binary | std::ifstream::ate);
+    const size_t n = f ? (size_t)f.tellg() / sizeof(complexF) : 0;
+    num_syms = (int)std::ceil((float)n / (float)(cols - 1));
+}
+
+// matrixMultThenSum (cpuLS.hpp:187-208): Yf[j] = sum_r Y[r][j] * Hconj[r][j],
+// Y and Hconj rows x (cols-1)
+inline void matrixMultThenSum(complexF *Y, complexF *Hconj, complexF *Yf, int rows, int cols) {
+    ofdm::HostEngine::get().numerator(Y, Hconj, rows, cols - 1, Yf);
+}
+
+// findDistSqrd (cpuLS.hpp:211-228): Hsqrd[j] = {sum_r |H[r][j]|^2, 0}
+inline void findDistSqrd(complexF *H, complexF *Hsqrd, int rows, int cols) {
+    std::vector<float> p((size_t)cols);
+    ofdm::HostEngine::get().dist_sqrd(H, rows, cols, p.data());
+    for (int j = 0; j < cols; j++) Hsqrd[j] = complexF{p[j], 0.f};
+}
+
+// divideOneRow (cpuLS.hpp:233-244): A[row][j] /= B[j]
+inline void divideOneRow(complexF *A, complexF *B, int cols, int row) {
+    ofdm::HostEngine::get().divide(&A[(size_t)row * cols], B, cols);
+}
+
+// firstVector (cpuLS.hpp:247-317): pilots, then the pilot symbol from the
+// ring -> Hconj (rows x (cols-1)) and |H|^2 in X[j].real (X[j].imag = 0).
+inline void firstVector(complexF *Y, complexF *Hconj, complexF *X, int rows, int cols,
+                        int iter = 0) {
+    const int K = cols - 1;
+    matrix_readX(X, K);
+    if (iter < numberOfSymbolsToTest - 1)
+        buffPtr->readNextSymbol(Y, iter);
+    else
+        buffPtr->readLastSymbol(Y);
+    auto &e = ofdm::HostEngine::get();
+    clock_t t0 = ofdm_cpuls::tic();
+    e.fft_rows(Y, rows, cols, 0);
+    ofdm_cpuls::toc(fft, iter, t0);
+    t0 = ofdm_cpuls::tic();
+    std::vector<float> p((size_t)K);
+    e.ls(Y, X, rows, cols, Hconj, p.data());
+    for (int j = 0; j < K; j++) X[j] = complexF{p[j], 0.f};
+    ofdm_cpuls::toc(decode, iter, t0);
+}
+
+// doOneSymbol (cpuLS.hpp:319-389): data symbol `it` from the ring -> K
+// rotated MRC outputs appended to Output_cpu.dat (truncated when it <= 1).
+inline void doOneSymbol(complexF *Y, complexF *Hconj, complexF *Hsqrd, int rows, int cols, int it) {
+    const int K = cols - 1;
+    if (it == numberOfSymbolsToTest - 1)
+        buffPtr->readLastSymbol(Y);
+    else
+        buffPtr->readNextSymbol(Y, it);
+    auto &e = ofdm::HostEngine::get();
+    clock_t t0 = ofdm_cpuls::tic();
+    e.fft_rows(Y, rows, cols, 0);
+    ofdm_cpuls::toc(fft, it, t0);
+    t0 = ofdm_cpuls::tic();
+    std::vector<float> p((size_t)K);
+    for (int j = 0; j < K; j++) p[j] = Hsqrd[j].real;
+    std::vector<complexF> Yf((size_t)K);
+    e.mrc(Y, Hconj, p.data(), rows, cols, Yf.data());
+    ofdm_cpuls::toc(decode, it, t0);
+    outfile.open(file.c_str(), it <= 1 ? (std::ofstream::binary | std::ofstream::trunc)
+                                       : (std::ofstream::binary | std::ofstream::app));
+    outfile.write(reinterpret_cast<const char *>(Yf.data()), (std::streamsize)K * sizeof(complexF));
+    outfile.close();
+}
+
+#endif  // _CPULS_HPP_

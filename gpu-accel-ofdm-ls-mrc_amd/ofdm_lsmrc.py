@@ -36,6 +36,10 @@ _SIGS = {
     "ofdm_mrc_demod": (_I, [_P, _LL, _P, _P, _I, _I, _P, _P]),
     "ofdm_mrc_numerator": (_I, [_P, _LL, _P, _I, _I, _P, _P]),
     "ofdm_mrc_finalize": (_I, [_P, _LL, _LL, _I, _I, _P, _P, _P]),
+    "ofdm_channel_conj_product": (_I, [_P, _LL, _P, _I, _I, _P, _P]),
+    "ofdm_combine_products": (_I, [_P, _LL, _P, _I, _I, _I, _P, _P]),
+    "ofdm_shift_rows": (_I, [_P, _LL, _I, _P, _P]),
+    "ofdm_dist_sqrd": (_I, [_P, _I, _I, _P, _P]),
     "ofdm_frame_workspace_bytes": (_c.c_size_t, [_LL, _I, _I, _I]),
     "ofdm_frame_demod": (_I, [_P, _LL, _I, _I, _I, _I, _P, _P, _c.c_size_t, _P, _P]),
     "ofdm_frame_estimate": (_I, [_P, _LL, _I, _I, _I, _I, _P, _P, _c.c_size_t, _P]),
@@ -166,6 +170,40 @@ def mrc_finalize(num_chunk, e0, nsym, K, P, out, stream=None):
     _check(lib().ofdm_mrc_finalize(_dptr(num_chunk), e0, num_chunk.numel(), nsym, K, _dptr(P),
                                    _dptr(out), _stream(stream)), "ofdm_mrc_finalize")
     return out
+
+
+def channel_conj_product(Y, H, stream=None):
+    """multiplyWithChannelConj: Y (nsyms, R, C), H (R, K) -> (nsyms, R, K)."""
+    n, R, C = Y.shape
+    out = c64((n, R, C - 1), Y.device)
+    _check(lib().ofdm_channel_conj_product(_dptr(Y), n, _dptr(H), R, C, _dptr(out),
+                                           _stream(stream)), "ofdm_channel_conj_product")
+    return out
+
+
+def combine_products(prod, P, rotate=True, stream=None):
+    """combineForMRC [+ shiftOneRow]: prod (nsyms, R, K) -> (nsyms, K)."""
+    n, R, K = prod.shape
+    out = c64((n, K), prod.device)
+    _check(lib().ofdm_combine_products(_dptr(prod), n, _dptr(P), R, K, int(rotate), _dptr(out),
+                                       _stream(stream)), "ofdm_combine_products")
+    return out
+
+
+def shift_rows(x, stream=None):
+    K = x.shape[-1]
+    out = c64(x.shape, x.device)
+    _check(lib().ofdm_shift_rows(_dptr(x), x.numel() // K, K, _dptr(out), _stream(stream)),
+           "ofdm_shift_rows")
+    return out
+
+
+def dist_sqrd(H, stream=None):
+    import torch
+    R, K = H.shape
+    P = torch.empty(K, dtype=torch.float32, device=H.device)
+    _check(lib().ofdm_dist_sqrd(_dptr(H), R, K, _dptr(P), _stream(stream)), "ofdm_dist_sqrd")
+    return P
 
 
 def workspace_bytes(nframes, S, R, C):

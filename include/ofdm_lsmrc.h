@@ -105,6 +105,25 @@ int ofdm_mrc_numerator(const ofdm_cf32 *d_Y, long long nsyms, const ofdm_cf32 *d
 int ofdm_mrc_finalize(const ofdm_cf32 *d_num, long long e0, long long count, int nsym, int K,
                       const float *d_Hsqrd, ofdm_cf32 *d_out, ofdm_stream_t stream);
 
+/* Stage-wise operations behind the reference's per-stage GPU methods, which
+ * materialise their intermediates (the fused entry points above do not):
+ *   ofdm_channel_conj_product: d_prod[s][r][j] = Y[s][r][j+1] * Hconj[r][j]
+ *       (nsyms x R x K; multiplyWithChannelConj, gpuLS.cu:212-233)
+ *   ofdm_combine_products: d_out[s][k] = sum_r prod[s][r][j] / Hsqrd[j], at
+ *       k = rotated position of j if rotate != 0, else k = j
+ *       (combineForMRC [+ shiftOneRow], gpuLS.cu:236-259, 109-125)
+ *   ofdm_shift_rows: shiftOneRow on nrows device rows of K, out of place
+ *       (gpuLS.cu:109-125, cpuLS.hpp:135-149)
+ *   ofdm_dist_sqrd: d_Hsqrd[j] = sum_r |H[r][j]|^2 of an R x K matrix
+ *       (findDistSqrd, gpuLS.cu:185-209, cpuLS.hpp:211-228) */
+int ofdm_channel_conj_product(const ofdm_cf32 *d_Y, long long nsyms, const ofdm_cf32 *d_Hconj,
+                              int R, int C, ofdm_cf32 *d_prod, ofdm_stream_t stream);
+int ofdm_combine_products(const ofdm_cf32 *d_prod, long long nsyms, const float *d_Hsqrd, int R,
+                          int K, int rotate, ofdm_cf32 *d_out, ofdm_stream_t stream);
+int ofdm_shift_rows(const ofdm_cf32 *d_in, long long nrows, int K, ofdm_cf32 *d_out,
+                    ofdm_stream_t stream);
+int ofdm_dist_sqrd(const ofdm_cf32 *d_H, int R, int K, float *d_Hsqrd, ofdm_stream_t stream);
+
 /* ------------------------------------------------------ device: frames --- */
 
 /* Workspace for ofdm_frame_demod / ofdm_frame_demod_freq (bytes, 256-aligned
@@ -113,14 +132,14 @@ int ofdm_mrc_finalize(const ofdm_cf32 *d_num, long long e0, long long count, int
 size_t ofdm_frame_workspace_bytes(long long nframes, int S, int R, int C);
 
 /* Frame-batched receiver on time-domain IQ (what ShMemSymBuff delivers):
- * d_iq = nframes x S x R x (C + prefix) samples; the cyclic prefix of every
+ * d_iq = nframes x S x R x (C + cp_len) samples; the cyclic prefix of every
  * row is skipped (ShMemSymBuff.hpp:309-322), each row is FFT'd, symbol 0 of
  * each frame gives the LS estimate, symbols 1..S-1 are MRC-demodulated into
  * d_out = nframes x (S-1) x K.  Replaces demodOneFrameCUDA / demodOptimized
  * (gpuLS.cu:575-769) and the cpuLS_main loop (cpuLS_main.cpp:80-92), for a
  * whole batch of frames in one call.  C = 1024 runs the fused one-pass
  * kernels; other C run FFT + LS + MRC stages through the workspace. */
-int ofdm_frame_demod(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, int prefix,
+int ofdm_frame_demod(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, int cp_len,
                      const ofdm_cf32 *d_X, void *d_ws, size_t ws_bytes, ofdm_cf32 *d_out,
                      ofdm_stream_t stream);
 
@@ -130,9 +149,9 @@ int ofdm_frame_demod(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int
  * gpuLS.cu:351-408, per frame); ofdm_frame_combine MRC-demodulates the data
  * symbols against it (gpuLS::demodOneSymbol, gpuLS.cu:410-473, per symbol).
  * ofdm_frame_demod == estimate then combine on the same stream. */
-int ofdm_frame_estimate(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, int prefix,
+int ofdm_frame_estimate(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, int cp_len,
                         const ofdm_cf32 *d_X, void *d_ws, size_t ws_bytes, ofdm_stream_t stream);
-int ofdm_frame_combine(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, int prefix,
+int ofdm_frame_combine(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, int cp_len,
                        void *d_ws, size_t ws_bytes, ofdm_cf32 *d_out, ofdm_stream_t stream);
 
 /* ofdm_frame_demod on frequency-domain symbols (FFT done upstream, no prefix):
@@ -146,11 +165,11 @@ int ofdm_frame_demod_freq(const ofdm_cf32 *d_Y, long long nframes, int S, int R,
  * antennas; sum the partials across GPUs), and partial MRC numerators
  * d_num ([nframes][S-1][K], subcarrier order; sum across GPUs, then
  * ofdm_mrc_finalize).  d_ws as for ofdm_frame_demod. */
-int ofdm_frame_ls_partial(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, int prefix,
+int ofdm_frame_ls_partial(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, int cp_len,
                           const ofdm_cf32 *d_X, void *d_ws, size_t ws_bytes, float *d_P,
                           ofdm_stream_t stream);
 int ofdm_frame_mrc_partial(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int C,
-                           int prefix, void *d_ws, size_t ws_bytes, ofdm_cf32 *d_num,
+                           int cp_len, void *d_ws, size_t ws_bytes, ofdm_cf32 *d_num,
                            ofdm_stream_t stream);
 
 /* --------------------------------------------------- synthetic frames --- */
@@ -159,9 +178,9 @@ int ofdm_frame_mrc_partial(const ofdm_cf32 *d_iq, long long nframes, int S, int 
  * H ~ CN(0,1) per (frame, antenna, subcarrier), pilot = d_X, data = QPSK,
  * bins j+1 carry H x (bin 0 empty), y = IFFT(Y)/sqrt(C) + CN(0, noise_std^2)
  * with a cyclic prefix (freq_domain = 0), or y = Y + noise (freq_domain = 1,
- * prefix ignored).  Frame f of the buffer is global frame frame0 + f; antenna
+ * cp_len ignored).  Frame f of the buffer is global frame frame0 + f; antenna
  * r is global antenna r0 + r (antenna-split shards). */
-int ofdm_synth_frames(ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, int prefix,
+int ofdm_synth_frames(ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, int cp_len,
                       const ofdm_cf32 *d_X, unsigned long long seed, long long frame0,
                       float noise_std, int freq_domain, int r0, ofdm_stream_t stream);
 

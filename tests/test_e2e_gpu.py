@@ -1,0 +1,69 @@
+"""End-to-end through the drop-in boundary on the GPU: a writer process
+(master, like rx_and_corr.cpp) pushes IQ symbols through the ShMemSymBuff
+shared-memory ring; a reader process runs one of the reference's receiver
+flows written against this package's headers (cpuLS.hpp free functions,
+gpuLS per-symbol, gpuLS frame); its Output_*.dat must match the golden
+output computed by the reference's own arithmetic (tests/golden/)."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from helpers import GOLDEN, parity
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "gpu-accel-ofdm-ls-mrc_amd")
+CPP = os.path.join(ROOT, "tests", "cpp")
+
+
+def raw_pilots(X):
+    """Inverse of matrix_readX's rotation: the file content that reads as X."""
+    K = X.size
+    return X[(np.arange(K) - (K + 1) // 2) % K]
+
+
+def build(tmp, name, R, C, prefix, S, shm):
+    exe = os.path.join(tmp, name)
+    cmd = ["g++", "-O2", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
+           f"-I{PKG}/host", f"-I{ROOT}/include", f"-DnumOfRows={R}", f"-Ddimension={C}",
+           f"-Dprefix={prefix}", f"-DlenOfBuffer={S}", f"-DshmemID=\"{shm}\"",
+           os.path.join(CPP, name + ".cpp"), "-o", exe, f"-L{PKG}/lib", "-lofdm_lsmrc",
+           f"-Wl,-rpath,{PKG}/lib", "-L/opt/rocm/lib", "-lamdhip64", "-lrt"]
+    subprocess.run(cmd, check=True)
+    return exe
+
+
+@pytest.mark.parametrize("fixture,flow", [("cfg1_r4_c1024_s10", "cpuls"),
+                                          ("cfg1_r4_c1024_s10", "symbol"),
+                                          ("cfg1_r4_c1024_s10", "frame"),
+                                          ("r8_c2048_s3_cp16", "symbol"),
+                                          ("r8_c2048_s3_cp16", "cpuls"),
+                                          ("r4_c256_s5_cp32", "frame")])
+def test_ring_to_output_file(tmp_path, fixture, flow):
+    z = np.load(os.path.join(GOLDEN, fixture + ".npz"), allow_pickle=False)
+    iq = z["iq"][0]  # first frame: S x R x (C + prefix)
+    S, R, Cp = iq.shape
+    prefix = int(z["prefix"])
+    C = Cp - prefix
+    tmp = str(tmp_path)
+    raw_pilots(z["X"]).astype(np.complex64).tofile(os.path.join(tmp, "Pilots.dat"))
+    iq.astype(np.complex64).tofile(os.path.join(tmp, "iq.bin"))
+    shm = f"/ofdm_e2e_{os.getpid()}_{flow}_{C}"
+    writer = build(tmp, "e2e_writer", R, C, prefix, S, shm)
+    reader = build(tmp, "e2e_reader", R, C, prefix, S, shm)
+    w = subprocess.Popen([writer, "iq.bin"], cwd=tmp, stdout=subprocess.PIPE,
+                         stderr=subprocess.PIPE, text=True)
+    try:
+        r = subprocess.run([reader, flow], cwd=tmp, capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stdout + r.stderr
+        out, err = w.communicate(timeout=60)
+        assert w.returncode == 0, out + err
+    finally:
+        if w.poll() is None:
+            w.kill()
+    name = "Output_cpu.dat" if flow == "cpuls" else "Output_gpu.dat"
+    got = np.fromfile(os.path.join(tmp, name), np.complex64).reshape(S - 1, C - 1)
+    parity(got, z["out"][0])

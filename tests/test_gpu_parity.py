@@ -199,3 +199,28 @@ def test_full_size_properties(ofdm, dev, F, S, R, C):
     for f in (0, F - 1):
         ref, _, _ = o.frame_demod(host(iq[f]), host(X))
         parity(host(out[f]), ref)
+
+
+# ------------------------------------------- stage-wise reference GPU API
+
+@pytest.mark.parametrize("R,C", [(1, 64), (16, 1024), (5, 256)])
+def test_stagewise_ops_vs_oracle(ofdm, oracle, dev, R, C):
+    """multiplyWithChannelConj -> combineForMRC (+shiftOneRow) and findDistSqrd
+    (gpuLS.cu:185-259) reproduce the fused MRC result."""
+    rng = np.random.default_rng(R * 7 + C)
+    K = C - 1
+    nsym = 3
+    H = ((rng.standard_normal((R, K)) + 1j * rng.standard_normal((R, K)))).astype(np.complex64)
+    Y = (rng.standard_normal((nsym, R, C)) + 1j * rng.standard_normal((nsym, R, C))).astype(np.complex64)
+    P_ref = (np.abs(H.astype(np.complex128)) ** 2).sum(0)
+    P = ofdm.dist_sqrd(to_dev(H, dev))
+    parity(host(P), P_ref)
+    prod = ofdm.channel_conj_product(to_dev(Y, dev), to_dev(H, dev))
+    parity(host(prod), Y[:, :, 1:] * H[None])
+    out = host(ofdm.combine_products(prod, P, rotate=True))
+    ref = np.stack([oracle.mrc(Y[s], H, host(P)) for s in range(nsym)])
+    parity(out, ref)
+    unrot = host(ofdm.combine_products(prod, P, rotate=False))
+    parity(np.stack([oracle.shift_one_row(u) for u in unrot]), ref)
+    sh = host(ofdm.shift_rows(to_dev(unrot, dev)))
+    parity(sh, ref)
