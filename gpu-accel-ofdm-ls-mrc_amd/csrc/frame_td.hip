@@ -127,28 +127,9 @@ __device__ __forceinline__ void quad_fmac_dpp(float (&v)[16], float S) {
 }
 #undef OFDM_DPP_Q
 
-// Forward 1024-point FFT of the row held in a[] (see header); T is this
-// wave's transpose region.  On return x[k'] = X[b0 + 16 k'],
-// b0 = (t >> 2) + 256 c(t & 3).
-__device__ __forceinline__ void row_fft(float2 (&a)[16], int t, float2 *T, const float2 *tw,
-                                        float2 (&x)[16]) {
-    fft_reg<16, false>(a);
-#pragma unroll
-    for (int k2 = 1; k2 < 16; ++k2) a[k2] = cmul(a[k2], tw[t * TW1P + k2]);
-#pragma unroll
-    for (int k2 = 0; k2 < 16; ++k2) T[k2 * TP + t] = a[k2];
-    wave_lds_sync();
-    const int q = t >> 2, qa = t & 3;
-#pragma unroll
-    for (int l = 0; l < 16; ++l) x[l] = T[q * TP + qa + 4 * l];
-    wave_lds_sync();
-    fft_reg<16, false>(x);
-    const float2 *tw2 = tw + TW1BUF + qa * TW2P;
-    const float g = quad_g(qa);
-    x[0] = float2{g * x[0].x, g * x[0].y};
-#pragma unroll
-    for (int k = 1; k < 16; ++k) x[k] = cmul(x[k], tw2[k]);
-    // 4-point DFT over the quad: two radix-2 stages, one fma per float each
+// 4-point DFT over the lanes of each quad (see header), in place.
+__device__ __forceinline__ void quad_dft(float2 (&x)[16], int qa) {
+    // two radix-2 stages, one fma per float each
     const float S1 = (qa & 2) ? 1.f : -1.f;
     const float S2 = (qa & 1) ? 1.f : -1.f;
     // lanes with qa == 3 multiply by -i between the stages: (x, y) -> (y, -x)
@@ -170,6 +151,30 @@ __device__ __forceinline__ void row_fft(float2 (&a)[16], int t, float2 *T, const
     quad_fmac_dpp<DPP_XOR1>(xi, S2);
 #pragma unroll
     for (int k = 0; k < 16; ++k) x[k] = float2{xr[k], xi[k]};
+}
+
+// Forward 1024-point FFT of the row held in a[] (see header); T is this
+// wave's transpose region.  On return x[k'] = X[b0 + 16 k'],
+// b0 = (t >> 2) + 256 c(t & 3).
+__device__ __forceinline__ void row_fft(float2 (&a)[16], int t, float2 *T, const float2 *tw,
+                                        float2 (&x)[16]) {
+    fft_reg<16, false>(a);
+#pragma unroll
+    for (int k2 = 1; k2 < 16; ++k2) a[k2] = cmul(a[k2], tw[t * TW1P + k2]);
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2) T[k2 * TP + t] = a[k2];
+    wave_lds_sync();
+    const int q = t >> 2, qa = t & 3;
+#pragma unroll
+    for (int l = 0; l < 16; ++l) x[l] = T[q * TP + qa + 4 * l];
+    wave_lds_sync();
+    fft_reg<16, false>(x);
+    const float2 *tw2 = tw + TW1BUF + qa * TW2P;
+    const float g = quad_g(qa);
+    x[0] = float2{g * x[0].x, g * x[0].y};
+#pragma unroll
+    for (int k = 1; k < 16; ++k) x[k] = cmul(x[k], tw2[k]);
+    quad_dft(x, qa);
 }
 
 __device__ __forceinline__ int lane_bin0(int t) {
@@ -293,24 +298,15 @@ __device__ __forceinline__ void mrc_row(float2 (&a)[16], int t, float2 *T, const
     }
 }
 
-template <bool NT, int SCHED, int WAVES, int DBG = 0>
-__device__ __forceinline__ void mrc_body(const float2 *__restrict__ iq, int S, int R, int prefix,
-                                         const float2 *__restrict__ Hc, const float *__restrict__ P,
-                                         float2 *__restrict__ out, long long nq, long long nblocks,
-                                         long long per_xcd, int mode) {
-    extern __shared__ __attribute__((aligned(16))) float2 lds[];
-    float2 *tw = lds;
-    const int w = threadIdx.x >> 6;
-    const int t = threadIdx.x & 63;
-    float2 *T = lds + TWBUF + w * TBUF;
-    const long long pb = blockIdx.x;
-    const long long lb = (pb & 7) * per_xcd + (pb >> 3);  // XCD-grouped logical block
-    if (lb >= nblocks) return;
-    fill_twiddles(tw);
-    __syncthreads();
-
-    long long q = lb * WAVES + w;
-    if (q >= nq) return;  // whole wave idle; no block-level sync follows
+// One symbol per wave.  PERSIST: a grid of ~2 workgroups per CU walks the
+// symbol groups; each XCD (blocks b with equal b % 8 under round-robin
+// dispatch; speed only) takes a contiguous range of groups so the frames in
+// flight on an XCD share their Hc in its L2.
+template <bool NT, int SCHED, int DBG, bool SYNC = false>
+__device__ __forceinline__ void mrc_symbol(const float2 *__restrict__ iq, int S, int R, int prefix,
+                                           const float2 *__restrict__ Hc, const float *__restrict__ P,
+                                           float2 *__restrict__ out, long long q, int mode, int t,
+                                           float2 *T, const float2 *tw, bool store = true) {
     const int nsym = S - 1;
     const long long f = q / nsym;
     const int s = 1 + (int)(q % nsym);
@@ -329,25 +325,259 @@ __device__ __forceinline__ void mrc_body(const float2 *__restrict__ iq, int S, i
 #pragma unroll
             for (int m = 0; m < 16; ++m) a[m] = nxt[m];
             if (r + 1 < R) row_load<NT>(sym + (long long)(r + 1) * Cp, t, nxt);
-            mrc_row<NT>(a, t, T, tw, Hf + (long long)r * (C / 2), acc);
+            mrc_row<NT, DBG>(a, t, T, tw, Hf + (long long)r * (C / 2), acc);
         }
     } else {
         for (int r = 0; r < R; ++r) {
             float2 a[16];
             row_load<NT>(sym + (long long)r * Cp, t, a);
+            // SYNC: the workgroup's waves (consecutive symbols, mostly one
+            // frame) stay on the same antenna row, so its Hc row is fetched
+            // from L2 once and re-read from L1
+            if (SYNC) __syncthreads();
             mrc_row<NT, DBG>(a, t, T, tw, Hf + (long long)r * (C / 2), acc);
         }
     }
+    if (!store) return;
+    if (DBG & 4) {  // diagnostic only: no output stores
+        float sacc = 0.f;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) sacc += acc[k].x;
+        if (sacc == 1234.5f) out[q] = float2{sacc, 0.f};
+        return;
+    }
     const int b0 = lane_bin0(t);
     float2 *o = out + q * K;
-    if (mode == 0) {
+    if ((mode & 1) == 0) {
         const float *Pf = P + f * C + b0;
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             const int b = b0 + 16 * k;
             if (b == 0) continue;
             const float pv = Pf[16 * k];
-            o[out_pos(b - 1, K)] = float2{acc[k].x / pv, acc[k].y / pv};
+            const float2 v = float2{acc[k].x / pv, acc[k].y / pv};
+            if (mode & 2)
+                __builtin_nontemporal_store(__builtin_bit_cast(unsigned long long, v),
+                                            reinterpret_cast<unsigned long long *>(o + out_pos(b - 1, K)));
+            else o[out_pos(b - 1, K)] = v;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int b = b0 + 16 * k;
+            if (b > 0) o[b - 1] = acc[k];
+        }
+    }
+}
+
+template <bool NT, int SCHED, int WAVES, int DBG = 0, bool PERSIST = false, bool SYNC = false>
+__device__ __forceinline__ void mrc_body(const float2 *__restrict__ iq, int S, int R, int prefix,
+                                         const float2 *__restrict__ Hc, const float *__restrict__ P,
+                                         float2 *__restrict__ out, long long nq, long long nblocks,
+                                         long long per_xcd, int mode) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    float2 *tw = lds;
+    const int w = threadIdx.x >> 6;
+    const int t = threadIdx.x & 63;
+    float2 *T = lds + TWBUF + w * TBUF;
+    if (!PERSIST) {
+        const long long pb = blockIdx.x;
+        const long long lb = (pb & 7) * per_xcd + (pb >> 3);  // XCD-grouped logical block
+        if (lb >= nblocks) return;
+        fill_twiddles(tw);
+        __syncthreads();
+        const long long q = lb * WAVES + w;
+        if (SYNC) {  // every wave takes part in the per-row barriers
+            mrc_symbol<NT, SCHED, DBG, true>(iq, S, R, prefix, Hc, P, out, q < nq ? q : nq - 1,
+                                             mode, t, T, tw, q < nq);
+            return;
+        }
+        if (q >= nq) return;  // whole wave idle; no block-level sync follows
+        mrc_symbol<NT, SCHED, DBG>(iq, S, R, prefix, Hc, P, out, q, mode, t, T, tw);
+    } else {
+        fill_twiddles(tw);
+        __syncthreads();
+        // XCD x (blocks b = x + 8 i) owns groups [x*per_xcd, (x+1)*per_xcd)
+        const int x = blockIdx.x & 7;
+        const long long i = blockIdx.x >> 3, nb_x = (gridDim.x + 7 - x) / 8;
+        const long long g0 = x * per_xcd, g1 = min(nblocks, g0 + per_xcd);
+        for (long long g = g0 + i; g < g1; g += nb_x) {
+            const long long q = g * WAVES + w;
+            if (q < nq) mrc_symbol<NT, SCHED, DBG>(iq, S, R, prefix, Hc, P, out, q, mode, t, T, tw);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// MRC with the channel estimates staged in LDS (HLDS): the 8 waves of a
+// workgroup walk the antenna rows in lockstep; each thread prefetches 16 B of
+// the next Hc row into a register before the FFT, the workgroup stores the
+// row to LDS once and every wave reads its 16 values from there -- one
+// dwordx4 per thread per row instead of eight per lane, and only LDS latency
+// in front of the MAC.  LDS per workgroup is exactly 80 KiB (2 per CU):
+//   TW1s [15][64] W1024^(c k2), k2 = 1..15     7680 B (k2-major: conflict free)
+//   TW2s [16][4]  g(a) W64^(a k')                512 B
+//   T    8 x [16][68] transpose images        69632 B (pitch 68: conflict free)
+//   Hfree  Hc float4s 0..255                    4096 B
+// and Hc float4s 256..511 live in the 16 unused 4-float2 row tails of the
+// 8 transpose images (never touched by the transposes).  Both halves are
+// read with per-lane affine addresses and no bank conflicts.
+// ---------------------------------------------------------------------------
+namespace hlds {
+constexpr int TW1S = 15 * 64;
+constexpr int TW2S = 16 * 4;
+constexpr int TP = 68;
+constexpr int TS = 16 * TP;
+constexpr int WAVES = 8;
+constexpr size_t LDS_BYTES = (TW1S + TW2S + WAVES * TS) * sizeof(float2) + 256 * sizeof(float4);
+static_assert(LDS_BYTES == 81920, "two workgroups per CU");
+
+// slot of Hc float4 j (0..511) of the staged row; T0 = first transpose image
+__device__ __forceinline__ float4 *hslot(float2 *T0, float4 *hfree, int j) {
+    if (j < 256) return hfree + j;
+    const int jj = j - 256;  // wave image jj>>5, row (jj>>1)&15, tail half jj&1
+    return reinterpret_cast<float4 *>(T0 + (jj >> 5) * TS + ((jj >> 1) & 15) * TP + 64 + 2 * (jj & 1));
+}
+
+__device__ __forceinline__ void fill(float2 *tw1, float2 *tw2) {
+    for (int i = threadIdx.x; i < TW1S; i += blockDim.x) {
+        const int k2 = 1 + i / 64, t = i % 64;
+        tw1[i] = g_tw[((t * k2) & (C - 1)) * (OFDM_TW_N / C)];
+    }
+    for (int i = threadIdx.x; i < TW2S; i += blockDim.x) {
+        const int k = i / 4, a = i % 4;
+        const float2 w = g_tw[((16 * a * k) & (C - 1)) * (OFDM_TW_N / C)];
+        const float g = quad_g(a);
+        tw2[i] = float2{g * w.x, g * w.y};
+    }
+}
+// index of (row, col) in a transpose image
+__device__ __forceinline__ int swz(int row, int col) { return row * TP + col; }
+
+// first half: radix-16 over m, twiddles, transpose write
+__device__ __forceinline__ void row_fft_a(float2 (&a)[16], int t, float2 *T, const float2 *tw1) {
+    fft_reg<16, false>(a);
+#pragma unroll
+    for (int k2 = 1; k2 < 16; ++k2) a[k2] = cmul(a[k2], tw1[(k2 - 1) * 64 + t]);
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2) T[swz(k2, t)] = a[k2];
+}
+// second half: transpose read, radix-16, twiddles, quad DFT
+__device__ __forceinline__ void row_fft_b(int t, float2 *T, const float2 *tw2, float2 (&x)[16]) {
+    wave_lds_sync();
+    const int q = t >> 2, qa = t & 3;
+#pragma unroll
+    for (int l = 0; l < 16; ++l) x[l] = T[swz(q, qa + 4 * l)];
+    wave_lds_sync();
+    fft_reg<16, false>(x);
+    const float g = quad_g(qa);
+    x[0] = float2{g * x[0].x, g * x[0].y};
+#pragma unroll
+    for (int k = 1; k < 16; ++k) x[k] = cmul(x[k], tw2[k * 4 + qa]);
+    quad_dft(x, qa);
+}
+}  // namespace hlds
+
+// Antenna-row loop of the HLDS kernel.  SHARED: the workgroup's 8 symbols
+// share one frame and the Hc row goes through LDS; otherwise (a workgroup
+// straddling a frame boundary) each wave loads its own Hc row from L2.
+template <bool NT, bool SHARED>
+__device__ __forceinline__ void hlds_rows(const float2 *sym, int Cp, int R, const float4 *Hf, int t,
+                                          float2 *T, const float2 *tw1, const float2 *tw2,
+                                          float2 *T0, float4 *hfree, float2 (&acc)[16]) {
+    using namespace hlds;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) acc[k] = float2{0.f, 0.f};
+    for (int r = 0; r < R; ++r) {
+        float2 a[16], x[16], h[16];
+        row_load<NT>(sym + (long long)r * Cp, t, a);
+        row_fft_a(a, t, T, tw1);
+        if constexpr (SHARED) {
+            // prefetch 16 B of the Hc row once a[] is dead: its latency
+            // hides behind the second half of the FFT
+            const float4 hreg = Hf[(long long)r * (C / 2) + threadIdx.x];
+            row_fft_b(t, T, tw2, x);
+            __syncthreads();  // every wave is done with the previous Hc row
+            *hslot(T0, hfree, threadIdx.x) = hreg;
+            __syncthreads();
+            const float4 *lo = hfree + t;
+            const float4 *hi = hslot(T0, hfree, 256 + t);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const float4 v = i < 4 ? lo[i * 64] : hi[(i - 4) * TS];  // 2 images = TS float4s
+                h[2 * i] = float2{v.x, v.y};
+                h[2 * i + 1] = float2{v.z, v.w};
+            }
+        } else {
+            row_fft_b(t, T, tw2, x);
+            __builtin_amdgcn_sched_barrier(0);
+            hc_load(Hf + (long long)r * (C / 2), t, h);
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            acc[k].x = acc[k].x + (x[k].x * h[k].x - x[k].y * h[k].y);
+            acc[k].y = acc[k].y + (x[k].x * h[k].y + x[k].y * h[k].x);
+        }
+    }
+}
+
+template <bool NT>
+__global__ void __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 4)))
+k_mrc_td1024_hlds(const float2 *__restrict__ iq, int S, int R, int prefix,
+                  const float2 *__restrict__ Hc, const float *__restrict__ P,
+                  float2 *__restrict__ out, long long nq, long long nblocks, long long per_xcd,
+                  int mode) {
+    using namespace hlds;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    float2 *tw1 = lds, *tw2 = lds + TW1S;
+    const int w = threadIdx.x >> 6, t = threadIdx.x & 63;
+    float2 *T = lds + TW1S + TW2S + w * TS;
+    float2 *T0 = lds + TW1S + TW2S;
+    float4 *hfree = reinterpret_cast<float4 *>(T0 + WAVES * TS);
+    const long long pb = blockIdx.x;
+    const long long lb = (pb & 7) * per_xcd + (pb >> 3);  // XCD-grouped logical block
+    if (lb >= nblocks) return;
+    fill(tw1, tw2);
+    __syncthreads();
+
+    // every wave takes part in the per-row barriers: tail waves duplicate the
+    // last symbol and do not store
+    const long long qw = lb * WAVES + w;
+    const bool store = qw < nq;
+    const long long q = store ? qw : nq - 1;
+    // the workgroup's Hc rows come from the frame of its first symbol; a
+    // workgroup straddling two frames falls back to per-wave L2 loads
+    const int nsym = S - 1;
+    const long long f = q / nsym;
+    const long long f0 = (lb * WAVES) / nsym;
+    const long long fl = ((lb * WAVES + WAVES - 1 < nq ? lb * WAVES + WAVES - 1 : nq - 1)) / nsym;
+    const bool shared = (f0 == fl);
+    const int s = 1 + (int)(q % nsym);
+    const int Cp = C + prefix;
+    const float2 *sym = iq + (f * S + s) * (long long)R * Cp + prefix;
+    const float4 *Hf = reinterpret_cast<const float4 *>(Hc + f * (long long)R * C);
+    const float4 *Hf0 = reinterpret_cast<const float4 *>(Hc + f0 * (long long)R * C);
+
+    float2 acc[16];
+    if (shared)
+        hlds_rows<NT, true>(sym, Cp, R, Hf0, t, T, tw1, tw2, T0, hfree, acc);
+    else
+        hlds_rows<NT, false>(sym, Cp, R, Hf, t, T, tw1, tw2, T0, hfree, acc);
+    if (!store) return;
+    const int b0 = lane_bin0(t);
+    float2 *o = out + q * K;
+    if ((mode & 1) == 0) {
+        const float *Pf = P + f * C + b0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int b = b0 + 16 * k;
+            if (b == 0) continue;
+            const float pv = Pf[16 * k];
+            const float2 v = float2{acc[k].x / pv, acc[k].y / pv};
+            if (mode & 2)
+                __builtin_nontemporal_store(__builtin_bit_cast(unsigned long long, v),
+                                            reinterpret_cast<unsigned long long *>(o + out_pos(b - 1, K)));
+            else o[out_pos(b - 1, K)] = v;
         }
     } else {
 #pragma unroll
@@ -368,10 +598,11 @@ __global__ void __launch_bounds__(256) k_mrc_td1024(OFDM_MRC_ARGS) {
     mrc_body<NT, SCHED, 4>(iq, S, R, prefix, Hc, P, out, nq, nblocks, per_xcd, mode);
 }
 // 8 waves per workgroup, register budget for 4 waves/SIMD (2 groups/CU)
-template <bool NT, int SCHED, int DBG = 0>
+template <bool NT, int SCHED, int DBG = 0, bool PERSIST = false, bool SYNC = false>
 __global__ void __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 4)))
 k_mrc_td1024_w8(OFDM_MRC_ARGS) {
-    mrc_body<NT, SCHED, 8, DBG>(iq, S, R, prefix, Hc, P, out, nq, nblocks, per_xcd, mode);
+    mrc_body<NT, SCHED, 8, DBG, PERSIST, SYNC>(iq, S, R, prefix, Hc, P, out, nq, nblocks, per_xcd,
+                                               mode);
 }
 #undef OFDM_MRC_ARGS
 
@@ -393,35 +624,59 @@ hipError_t launch_mrc_td1024(const float2 *iq, long long nframes, int S, int R, 
     using namespace td1024;
     const long long nq = nframes * (S - 1);
     if (nq <= 0) return hipSuccess;
-    // A/B switches (defaults = the measured best): OFDM_MRC_NT=0/1 plain /
-    // non-temporal IQ loads, OFDM_MRC_SCHED=0/1 row-loop schedule,
-    // OFDM_MRC_WAVES=4/8 waves per workgroup.
-    static const int nt = [] { const char *e = getenv("OFDM_MRC_NT"); return e ? atoi(e) : 1; }();
-    static const int sched = [] { const char *e = getenv("OFDM_MRC_SCHED"); return e ? atoi(e) : 1; }();
-    static const int waves = [] { const char *e = getenv("OFDM_MRC_WAVES"); return e ? atoi(e) : 8; }();
-    const int W = waves == 4 ? 4 : 8;
+    // A/B switches, re-read on every launch so one process can compare them
+    // (defaults = the measured best): OFDM_MRC_NT=0/1 plain / non-temporal IQ
+    // loads, OFDM_MRC_SCHED=0/1 row-loop schedule, OFDM_MRC_WAVES=4/8 waves
+    // per workgroup, OFDM_MRC_PERSIST=0/1 one workgroup per symbol group /
+    // persistent grid (8-wave only), OFDM_MRC_SYNC=1 barrier per antenna row,
+    // OFDM_MRC_HLDS=0/1 Hc rows staged in LDS per workgroup (8-wave), OFDM_MRC_DEBUG=1|2|3|4|7 diagnostic variants
+    // (bit 0 no FFT, bit 1 no Hc, bit 2 no output stores)
+    // (wrong results) pricing the memory side: 1 no FFT, 2 no Hc, 3 neither.
+    auto knob = [](const char *n, int d) { const char *e = getenv(n); return e ? atoi(e) : d; };
+    const int nt = knob("OFDM_MRC_NT", 1), sched = knob("OFDM_MRC_SCHED", 1);
+    const int W = knob("OFDM_MRC_WAVES", 8) == 4 ? 4 : 8;
+    const int persist = knob("OFDM_MRC_PERSIST", 0), dbg = knob("OFDM_MRC_DEBUG", 0);
+    const int sync = knob("OFDM_MRC_SYNC", 0), hlds_on = knob("OFDM_MRC_HLDS", 1);
+    if (knob("OFDM_MRC_NTSTORE", 0)) mode |= 2;  // bit 1: nontemporal output stores
     const long long nblocks = (nq + W - 1) / W;
     const long long per_xcd = (nblocks + 7) / 8;
-    const long long grid = per_xcd * 8;
+    long long grid = per_xcd * 8;
+    if (W == 8 && persist) {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess)
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        const long long pg = (long long)cus * 2;  // 2 resident 8-wave groups per CU
+        grid = pg < grid ? pg : grid;
+    }
     if (grid > 0x7fffffffll) return hipErrorInvalidValue;
-    const size_t lds = (TWBUF + W * TBUF) * sizeof(float2);
-#define OFDM_MRC_LAUNCH(KER, NTV, SV)                                                              \
-    hipLaunchKernelGGL((KER<NTV, SV>), dim3((unsigned)grid), dim3(64 * W), lds, s, iq, S, R, prefix, \
-                       Hc, P, out, nq, nblocks, per_xcd, mode)
-    // OFDM_MRC_DEBUG=1|2|3: diagnostic variants (wrong results) pricing the
-    // memory side: 1 = no FFT, 2 = no Hc loads, 3 = neither
-    static const int dbg = [] { const char *e = getenv("OFDM_MRC_DEBUG"); return e ? atoi(e) : 0; }();
-    if (dbg) {
-        const long long nb8 = (nq + 7) / 8, px8 = (nb8 + 7) / 8;
-        const size_t l8 = (TWBUF + 8 * TBUF) * sizeof(float2);
-#define OFDM_DBG(D) hipLaunchKernelGGL((k_mrc_td1024_w8<true, NOPREFETCH, D>), dim3((unsigned)(px8 * 8)), \
-                                       dim3(512), l8, s, iq, S, R, prefix, Hc, P, out, nq, nb8, px8, mode)
-        if (dbg == 1) OFDM_DBG(1); else if (dbg == 2) OFDM_DBG(2); else OFDM_DBG(3);
-#undef OFDM_DBG
+    if (W == 8 && hlds_on && !persist && !sync && !dbg) {
+        if (nt)
+            hipLaunchKernelGGL((k_mrc_td1024_hlds<true>), dim3((unsigned)grid), dim3(512), hlds::LDS_BYTES, s,
+                               iq, S, R, prefix, Hc, P, out, nq, nblocks, per_xcd, mode);
+        else
+            hipLaunchKernelGGL((k_mrc_td1024_hlds<false>), dim3((unsigned)grid), dim3(512), hlds::LDS_BYTES, s,
+                               iq, S, R, prefix, Hc, P, out, nq, nblocks, per_xcd, mode);
         return hipGetLastError();
     }
-    if (W == 8) {
-        if (nt) { if (sched) OFDM_MRC_LAUNCH(k_mrc_td1024_w8, true, NOPREFETCH); else OFDM_MRC_LAUNCH(k_mrc_td1024_w8, true, PREFETCH_COPY); }
+    const size_t lds = (TWBUF + W * TBUF) * sizeof(float2);
+#define OFDM_MRC_LAUNCH(KER, ...)                                                                  \
+    hipLaunchKernelGGL((KER<__VA_ARGS__>), dim3((unsigned)grid), dim3(64 * W), lds, s, iq, S, R,   \
+                       prefix, Hc, P, out, nq, nblocks, per_xcd, mode)
+    if (W == 8 && persist) {
+        if (dbg == 1) OFDM_MRC_LAUNCH(k_mrc_td1024_w8, true, NOPREFETCH, 1, true);
+        else if (dbg == 2) OFDM_MRC_LAUNCH(k_mrc_td1024_w8, true, NOPREFETCH, 2, true);
+        else if (dbg == 3) OFDM_MRC_LAUNCH(k_mrc_td1024_w8, true, NOPREFETCH, 3, true);
+        else if (nt) OFDM_MRC_LAUNCH(k_mrc_td1024_w8, true, NOPREFETCH, 0, true);
+        else OFDM_MRC_LAUNCH(k_mrc_td1024_w8, false, NOPREFETCH, 0, true);
+    } else if (W == 8 && sync) {
+        OFDM_MRC_LAUNCH(k_mrc_td1024_w8, true, NOPREFETCH, 0, false, true);
+    } else if (W == 8) {
+        if (dbg == 1) OFDM_MRC_LAUNCH(k_mrc_td1024_w8, true, NOPREFETCH, 1);
+        else if (dbg == 2) OFDM_MRC_LAUNCH(k_mrc_td1024_w8, true, NOPREFETCH, 2);
+        else if (dbg == 3) OFDM_MRC_LAUNCH(k_mrc_td1024_w8, true, NOPREFETCH, 3);
+        else if (dbg == 4) OFDM_MRC_LAUNCH(k_mrc_td1024_w8, true, NOPREFETCH, 4);
+        else if (dbg == 7) OFDM_MRC_LAUNCH(k_mrc_td1024_w8, true, NOPREFETCH, 7);
+        else if (nt) { if (sched) OFDM_MRC_LAUNCH(k_mrc_td1024_w8, true, NOPREFETCH); else OFDM_MRC_LAUNCH(k_mrc_td1024_w8, true, PREFETCH_COPY); }
         else    { if (sched) OFDM_MRC_LAUNCH(k_mrc_td1024_w8, false, NOPREFETCH); else OFDM_MRC_LAUNCH(k_mrc_td1024_w8, false, PREFETCH_COPY); }
     } else {
         if (nt) { if (sched) OFDM_MRC_LAUNCH(k_mrc_td1024, true, NOPREFETCH); else OFDM_MRC_LAUNCH(k_mrc_td1024, true, PREFETCH_COPY); }

@@ -1,0 +1,55 @@
+"""Same-process A/B of the MRC kernel variants (env knobs re-read per launch),
+so box-to-box clock/HBM variation does not enter the comparison.
+usage: python scripts/ab_mrc.py [frames] [reps] VAR=VAL[,VAR=VAL...] ..."""
+import os
+import sys
+import numpy as np
+import torch
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "gpu-accel-ofdm-ls-mrc_amd"))
+import ofdm_lsmrc as ofdm
+
+F = int(sys.argv[1]) if len(sys.argv) > 1 else 1250
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+variants = sys.argv[3:] or ["default"]
+S, R, C = 101, 64, 1024
+K = C - 1
+Q = F * (S - 1)
+dev = torch.device("cuda")
+rng = np.random.default_rng(1)
+a = np.float32(0.70710678)
+X = torch.from_numpy((rng.choice([-a, a], K) + 1j * rng.choice([-a, a], K)).astype(np.complex64)).to(dev)
+iq = ofdm.synth_frames(F, S, R, C, X, seed=1, noise_std=0.01)
+ws = ofdm.workspace(F, S, R, C, dev)
+out = ofdm.c64((F, S - 1, K), dev)
+ofdm.frame_estimate(iq, X, 0, ws)
+keys = set()
+for v in variants:
+    if v != "default":
+        keys |= {kv.split("=")[0] for kv in v.split(",")}
+res = {v: [] for v in variants}
+for rep in range(reps):           # interleave variants across reps
+    for v in variants:
+        for k in keys:
+            os.environ.pop(k, None)
+        if v != "default":
+            for kv in v.split(","):
+                k, val = kv.split("=")
+                os.environ[k] = val
+        ofdm.frame_combine(iq, 0, ws, out)  # warm
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        n = 5
+        for _ in range(n):
+            ofdm.frame_combine(iq, 0, ws, out)
+        e1.record()
+        torch.cuda.synchronize()
+        res[v].append(e0.elapsed_time(e1) / n)
+        if rep == 0 and "DEBUG" not in v:
+            err = int(ofdm.count_symbol_errors(out, S, seed=1).item())
+            if err:
+                print(f"{v}: {err} symbol errors!")
+b = Q * (R * C * 8 + K * 8)
+for v in variants:
+    ms = min(res[v])
+    print(f"{v:45s} {ms:7.3f} ms  {b / ms / 1e6:6.0f} GB/s  frac {b / ms / 1e6 / 8000:.3f}  (all: {' '.join(f'{x:.2f}' for x in res[v])})")

@@ -5,6 +5,11 @@
 //  mode 1: the 8 waves of a block share one symbol, wave w reads rows
 //          w, w+8, ... (a block streams 64 KB contiguous per step)
 //  mode 2: grid-stride contiguous 8-B loads (reference)
+//  mode 3: one symbol per wave, one-shot grid (nsym/8 blocks), XCD-grouped
+//          block remap, 78.9 KB dynamic LDS (the k_mrc_td1024_w8 skeleton)
+//  mode 4: as 3 without the remap; mode 5: as 3 without the LDS
+//  mode 6: as 3 plus 8 KB of stores per wave at the end (pitch 1023 float2)
+//  mode 7: pitch 1024 (line aligned); 8: pitch 1024 with dwordx4; 9: mode 6 with nt stores
 #include <hip/hip_runtime.h>
 #include <cstdio>
 typedef unsigned long long u64;
@@ -34,6 +39,40 @@ __global__ void __launch_bounds__(512) rd(const u64 *__restrict__ p, long long n
                 }
             }
         }
+    } else if (MODE >= 3) {
+        extern __shared__ float lds[];
+        const long long pb = blockIdx.x, per_xcd = gridDim.x / 8;
+        const long long lb = MODE == 4 ? pb : (pb & 7) * per_xcd + (pb >> 3);
+        const long long q = lb * 8 + w;
+        if (q < nsym) {
+            const u64 *s = p + q * 65536;
+            for (int r = 0; r < 64; ++r) {
+#pragma unroll
+                for (int m = 0; m < 16; ++m) {
+                    u64 v = __builtin_nontemporal_load(s + r * 1024 + t + 64 * m);
+                    acc += __builtin_bit_cast(float, (unsigned)v);
+                }
+            }
+        }
+        if (MODE != 5 && acc == 1234.5f) lds[threadIdx.x] = acc;
+        if (MODE >= 6 && q < nsym) {  // 8 KB of output per wave, like the MRC epilogue
+            const int pitch = (MODE == 7 || MODE == 8) ? 1024 : 1023;
+            float2 *o = reinterpret_cast<float2 *>(out) + 16 + q * pitch;
+            if (MODE == 8) {
+                float4 *o4 = reinterpret_cast<float4 *>(o);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) o4[t + 64 * k] = float4{acc, (float)k, acc, 1.f};
+            } else {
+#pragma unroll
+                for (int k = 0; k < 16; ++k) {
+                    const int j = t + 64 * k;
+                    if (j < 1023) {
+                        if (MODE == 9) __builtin_nontemporal_store(__builtin_bit_cast(u64, float2{acc, (float)k}), reinterpret_cast<u64 *>(o + j));
+                        else o[j] = float2{acc, (float)k};
+                    }
+                }
+            }
+        }
     } else {
         const long long n = nsym * 65536;
         for (long long i = (long long)blockIdx.x * 512 + threadIdx.x; i < n; i += (long long)gridDim.x * 512) {
@@ -47,20 +86,40 @@ template <int MODE>
 double run(const u64 *p, long long nsym, float *out, int blocks) {
     hipEvent_t a, b;
     hipEventCreate(&a); hipEventCreate(&b);
-    rd<MODE><<<blocks, 512>>>(p, nsym, out);
+    size_t lds = 0;
+    if (MODE >= 3) { blocks = (int)(nsym / 8); lds = MODE == 5 ? 0 : 80768; }
+    rd<MODE><<<blocks, 512, lds>>>(p, nsym, out);
     hipEventRecord(a);
-    for (int i = 0; i < 3; ++i) rd<MODE><<<blocks, 512>>>(p, nsym, out);
+    for (int i = 0; i < 3; ++i) rd<MODE><<<blocks, 512, lds>>>(p, nsym, out);
     hipEventRecord(b); hipEventSynchronize(b);
     float ms; hipEventElapsedTime(&ms, a, b);
     return nsym * 524288.0 * 3 / (ms * 1e-3) / 1e9;
+}
+__global__ void fill_random(u64 *p, long long n) {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        u64 z = (u64)i * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        p[i] = z ^ (z >> 31);
+    }
 }
 int main() {
     const long long nsym = 65536;  // 32 GiB
     u64 *p; float *out;
     if (hipMalloc(&p, nsym * 524288) != hipSuccess) return 1;
-    hipMalloc(&out, 4);
-    hipMemset(p, 0, nsym * 524288);
-    for (int blocks : {512, 1024, 4096})
-        printf("blocks %5d: per-wave symbol %5.0f  block-shared symbol %5.0f  grid-stride %5.0f GB/s\n",
-               blocks, run<0>(p, nsym, out, blocks), run<1>(p, nsym, out, blocks), run<2>(p, nsym, out, blocks));
+    hipMalloc(&out, (size_t)nsym * 8192 + 8192);
+    for (int fill = 0; fill < 2; ++fill) {
+        if (fill == 0) hipMemset(p, 0, nsym * 524288);
+        else fill_random<<<4096, 256>>>(p, nsym * 65536);
+        hipDeviceSynchronize();
+        for (int blocks : {512, 1024, 4096})
+            printf("%s blocks %5d: per-wave symbol %5.0f  block-shared symbol %5.0f  grid-stride %5.0f GB/s\n",
+                   fill ? "random" : "zeros ", blocks, run<0>(p, nsym, out, blocks), run<1>(p, nsym, out, blocks),
+                   run<2>(p, nsym, out, blocks));
+        printf("%s one-shot grid: remap+lds %5.0f  lds only %5.0f  remap only %5.0f GB/s\n",
+               fill ? "random" : "zeros ", run<3>(p, nsym, out, 0), run<4>(p, nsym, out, 0), run<5>(p, nsym, out, 0));
+        printf("%s +stores: pitch1023 %5.0f  pitch1024 %5.0f  pitch1024 x4 %5.0f  pitch1023 nt %5.0f GB/s\n",
+               fill ? "random" : "zeros ", run<6>(p, nsym, out, 0), run<7>(p, nsym, out, 0), run<8>(p, nsym, out, 0),
+               run<9>(p, nsym, out, 0));
+    }
 }
