@@ -201,7 +201,7 @@ def main():
         "dtype": "f32",
         "data": "synthetic (device-generated Rayleigh channel, QPSK, sigma=%g)" % args.noise,
         "config": cfg,
-        "roofline": {"kernel": "k_mrc_td1024 (FFT+MRC+normalise+rotate)", "bound": "hbm",
+        "roofline": {"kernel": "k_mrc_td1024_hlds (FFT+MRC+normalise+rotate)", "bound": "hbm",
                      "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                      "traffic_source": tsrc,

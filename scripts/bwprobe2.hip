@@ -10,6 +10,7 @@
 //  mode 4: as 3 without the remap; mode 5: as 3 without the LDS
 //  mode 6: as 3 plus 8 KB of stores per wave at the end (pitch 1023 float2)
 //  mode 7: pitch 1024 (line aligned); 8: pitch 1024 with dwordx4; 9: mode 6 with nt stores
+//  mode 10: mode 0 (persistent) with the stores; 11: mode 6 into a 512 KB (L2-resident) region
 #include <hip/hip_runtime.h>
 #include <cstdio>
 typedef unsigned long long u64;
@@ -17,7 +18,7 @@ template <int MODE>
 __global__ void __launch_bounds__(512) rd(const u64 *__restrict__ p, long long nsym, float *out) {
     const int w = threadIdx.x >> 6, t = threadIdx.x & 63;
     float acc = 0.f;
-    if (MODE == 0) {
+    if (MODE == 0 || MODE == 10) {
         for (long long q = (long long)blockIdx.x * 8 + w; q < nsym; q += (long long)gridDim.x * 8) {
             const u64 *s = p + q * 65536;  // 512 KB per symbol (u64 = 8 B)
             for (int r = 0; r < 64; ++r) {
@@ -25,6 +26,14 @@ __global__ void __launch_bounds__(512) rd(const u64 *__restrict__ p, long long n
                 for (int m = 0; m < 16; ++m) {
                     u64 v = __builtin_nontemporal_load(s + r * 1024 + t + 64 * m);
                     acc += __builtin_bit_cast(float, (unsigned)v);
+                }
+            }
+            if (MODE == 10) {
+                float2 *o = reinterpret_cast<float2 *>(out) + 16 + q * 1023;
+#pragma unroll
+                for (int k = 0; k < 16; ++k) {
+                    const int j = t + 64 * k;
+                    if (j < 1023) o[j] = float2{acc, (float)k};
                 }
             }
         }
@@ -39,7 +48,7 @@ __global__ void __launch_bounds__(512) rd(const u64 *__restrict__ p, long long n
                 }
             }
         }
-    } else if (MODE >= 3) {
+    } else if (MODE >= 3 && MODE != 10) {
         extern __shared__ float lds[];
         const long long pb = blockIdx.x, per_xcd = gridDim.x / 8;
         const long long lb = MODE == 4 ? pb : (pb & 7) * per_xcd + (pb >> 3);
@@ -57,7 +66,7 @@ __global__ void __launch_bounds__(512) rd(const u64 *__restrict__ p, long long n
         if (MODE != 5 && acc == 1234.5f) lds[threadIdx.x] = acc;
         if (MODE >= 6 && q < nsym) {  // 8 KB of output per wave, like the MRC epilogue
             const int pitch = (MODE == 7 || MODE == 8) ? 1024 : 1023;
-            float2 *o = reinterpret_cast<float2 *>(out) + 16 + q * pitch;
+            float2 *o = reinterpret_cast<float2 *>(out) + 16 + (MODE == 11 ? (q & 63) : q) * pitch;
             if (MODE == 8) {
                 float4 *o4 = reinterpret_cast<float4 *>(o);
 #pragma unroll
@@ -87,7 +96,7 @@ double run(const u64 *p, long long nsym, float *out, int blocks) {
     hipEvent_t a, b;
     hipEventCreate(&a); hipEventCreate(&b);
     size_t lds = 0;
-    if (MODE >= 3) { blocks = (int)(nsym / 8); lds = MODE == 5 ? 0 : 80768; }
+    if (MODE == 11 || (MODE >= 3 && MODE < 10)) { blocks = (int)(nsym / 8); lds = MODE == 5 ? 0 : 80768; }
     rd<MODE><<<blocks, 512, lds>>>(p, nsym, out);
     hipEventRecord(a);
     for (int i = 0; i < 3; ++i) rd<MODE><<<blocks, 512, lds>>>(p, nsym, out);
@@ -121,5 +130,7 @@ int main() {
         printf("%s +stores: pitch1023 %5.0f  pitch1024 %5.0f  pitch1024 x4 %5.0f  pitch1023 nt %5.0f GB/s\n",
                fill ? "random" : "zeros ", run<6>(p, nsym, out, 0), run<7>(p, nsym, out, 0), run<8>(p, nsym, out, 0),
                run<9>(p, nsym, out, 0));
+        printf("%s persistent 1024 blocks +stores %5.0f   one-shot stores into 512 KB %5.0f GB/s\n",
+               fill ? "random" : "zeros ", run<10>(p, nsym, out, 1024), run<11>(p, nsym, out, 0));
     }
 }
