@@ -1,0 +1,82 @@
+"""Antenna-split LS + MRC across ranks (BASELINE.json configs[4]).
+
+Each rank holds every frame/symbol/subcarrier of ITS antennas (R_g of R; for
+cfg5 256 antennas, 32 per GPU).  MRC is a sum over antennas, so
+
+  P[f][j]    = sum_g P_g[f][j]        (partial |H|^2, findDistSqrd gpuLS.cu:185-209)
+  N[f][s][j] = sum_g N_g[f][s][j]     (partial numerators, matrixMultThenSum
+                                       cpuLS.hpp:187-208)
+  out        = rotate(N / P)          (cpuLS.hpp:364-368, shiftOneRow 135-149)
+
+Data path per batch (one process per GPU, RCCL over xGMI):
+  1. ofdm_frame_ls_partial     -> P_g, Hc_g (workspace)          local
+  2. all_reduce(P)             F*K*4 B                           tiny
+  3. ofdm_frame_mrc_partial    -> N_g (F*(S-1)*K complex)        local, HBM-bound
+  4. reduce_scatter(N)         each rank receives 1/world of the flattened
+                               numerators, summed: the per-link traffic of a
+                               ring reduce-scatter is (world-1)/world * |N|/world
+                               per step, spread over the xGMI links, vs a full
+                               all-reduce's 2x
+  5. ofdm_mrc_finalize         divide + rotate of the rank's slice into `out`
+                               (elements of that slice only; other positions
+                               are left untouched)
+  optional 6. all_reduce(out)  (zeros elsewhere) when every rank needs all of it
+
+The kernel calls go through `ops` (default: the HIP library, ofdm_lsmrc).  A
+CPU stand-in with the same signatures is used by tests/test_antenna_split_cpu.py
+to check this orchestration over gloo; the product path has no CPU fallback.
+"""
+import ofdm_lsmrc
+
+
+class HipOps:
+    """The HIP library calls used by the antenna-split path."""
+    ls_partial = staticmethod(ofdm_lsmrc.frame_ls_partial)        # (shard, X, prefix) -> (P, ws)
+    mrc_partial = staticmethod(ofdm_lsmrc.frame_mrc_partial)      # (shard, ws, prefix) -> N
+    mrc_finalize = staticmethod(ofdm_lsmrc.mrc_finalize)          # (chunk, e0, nsym, K, P, out)
+
+
+def slice_bounds(n, world, rank):
+    """Flat element range [e0, e0 + count) that `rank` finalises when `n`
+    numerators are reduce-scattered in equal chunks of ceil(n / world)."""
+    per = -(-n // world) if n else 0
+    e0 = min(rank * per, n)
+    return per, e0, max(0, min(per, n - e0))
+
+
+def demod_antenna_split(shard, X, prefix=0, group=None, ops=HipOps, gather=False, out=None):
+    """LS + MRC of frames whose antennas are split across the ranks of `group`.
+
+    shard: (F, S, R_g, C + prefix) complex64, this rank's antennas (any R_g >= 1;
+           ranks may hold different counts).
+    X:     (K,) rotated pilots (matrix_readX), identical on every rank.
+    Returns (out, (e0, count)): out is (F, S-1, K) complex64 with this rank's
+    finalised flat numerator range [e0, e0 + count) written at its rotated
+    output positions (all positions when gather=True; a caller-supplied `out`
+    must then be zero-filled, since the gather is a sum over ranks).
+    """
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    F, S, _, Cp = shard.shape
+    K = Cp - prefix - 1
+    P, ws = ops.ls_partial(shard, X, prefix)
+    dist.all_reduce(P, group=group)
+    num = ops.mrc_partial(shard, ws, prefix)
+    n = num.numel()
+    per, e0, count = slice_bounds(n, world, rank)
+    flat = torch.view_as_real(num).reshape(-1)
+    if per * world != n:
+        flat = torch.cat([flat, flat.new_zeros(2 * (per * world - n))])
+    mine = flat.new_empty(2 * per)
+    dist.reduce_scatter_tensor(mine, flat, group=group)
+    if out is None:
+        out = torch.zeros((F, S - 1, K), dtype=torch.complex64, device=shard.device)
+    if count:
+        chunk = torch.view_as_complex(mine[:2 * count].view(count, 2))
+        ops.mrc_finalize(chunk, e0, S - 1, K, P, out)
+    if gather:
+        dist.all_reduce(torch.view_as_real(out), group=group)
+    return out, (e0, count)
