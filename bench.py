@@ -184,6 +184,8 @@ def main():
            "data_symbols_per_gpu": Q, "global_data_symbols": Q * world,
            "parallelism": f"frame-sharded x{world}, no collective"}
     b_sym = R * C * 8 + K * 8
+    kern = {1024: "k_mrc_td1024_hlds", 2048: "k_mrc_td2048"}.get(C)
+    mrc_name = f"{kern} (FFT+MRC+normalise+rotate)" if kern else "k_fft_rows + k_mrc_freq (staged)"
     achieved = Q * b_sym / (mrc_ms * 1e-3) / 1e9
     traffic, tsrc = pmc_traffic(args.pmc, cfg)
     step_bytes = F * S * R * C * 8 + Q * K * 8
@@ -201,12 +203,12 @@ def main():
         "dtype": "f32",
         "data": "synthetic (device-generated Rayleigh channel, QPSK, sigma=%g)" % args.noise,
         "config": cfg,
-        "roofline": {"kernel": "k_mrc_td1024_hlds (FFT+MRC+normalise+rotate)", "bound": "hbm",
+        "roofline": {"kernel": mrc_name, "bound": "hbm",
                      "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                      "traffic_source": tsrc,
                      "bytes_per_launch": Q * b_sym, "avg_launch_ms": mrc_ms},
-        "stages_ms": {"estimate_ls_td1024": ls_ms, "combine_mrc_td1024": mrc_ms},
+        "stages_ms": {"estimate_ls": ls_ms, "combine_mrc": mrc_ms},
         "step_algorithmic_GBps": step_bytes / (elapsed / args.steps) / 1e9,
         "check": {"qpsk_symbol_errors": errs},
         "cpu_baseline": None,

@@ -40,7 +40,19 @@ inline bool aligned(const void *p, size_t a) { return (reinterpret_cast<uintptr_
 size_t up256(size_t x) { return (x + 255) & ~size_t(255); }
 
 // fused one-pass kernels exist for these FFT sizes
-bool fused_c(int C) { return C == 1024; }
+bool fused_c(int C) { return C == 1024 || C == 2048; }
+
+// fused time-domain kernels by C (fused_c(C) must hold)
+hipError_t ls_fused(const float2 *iq, long long F, int S, int R, int C, int prefix, const float2 *X,
+                    float2 *Hc, float *P, int partial, hipStream_t s) {
+    return C == 1024 ? ofdm::launch_ls_td1024(iq, F, S, R, prefix, X, Hc, P, partial, s)
+                     : ofdm::launch_ls_td2048(iq, F, S, R, prefix, X, Hc, P, partial, s);
+}
+hipError_t mrc_fused(const float2 *iq, long long F, int S, int R, int C, int prefix, const float2 *Hc,
+                     const float *P, float2 *out, int mode, hipStream_t s) {
+    return C == 1024 ? ofdm::launch_mrc_td1024(iq, F, S, R, prefix, Hc, P, out, mode, s)
+                     : ofdm::launch_mrc_td2048(iq, F, S, R, prefix, Hc, P, out, mode, s);
+}
 
 long long staging_frames(long long nframes, int S, int R, int C) {
     const long long per = (long long)S * R * C * (long long)sizeof(float2);
@@ -272,8 +284,8 @@ int ofdm_frame_estimate(const ofdm_cf32 *d_iq, long long nframes, int S, int R, 
     if ((rc = carve(d_ws, ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
     hipStream_t s = hs(stream);
     if (fused_c(C))
-        return hip_check(ofdm::launch_ls_td1024(F2(d_iq), nframes, S, R, prefix, F2(d_X), w.Hc, w.P, 0, s),
-                         "ls_td1024");
+        return hip_check(ls_fused(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w.Hc, w.P, 0, s),
+                         "ls_fused");
     return td_staged(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w, nullptr, 2, s);
 }
 
@@ -286,9 +298,9 @@ int ofdm_frame_combine(const ofdm_cf32 *d_iq, long long nframes, int S, int R, i
     if ((rc = carve(d_ws, ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
     hipStream_t s = hs(stream);
     if (fused_c(C))
-        return hip_check(ofdm::launch_mrc_td1024(F2(d_iq), nframes, S, R, prefix, w.Hc, w.P,
+        return hip_check(mrc_fused(F2(d_iq), nframes, S, R, C, prefix, w.Hc, w.P,
                                                  F2(d_out), 0, s),
-                         "mrc_td1024");
+                         "mrc_fused");
     // staged path: the FFT of every chunk is redone here (estimate kept only Hc/P)
     return td_staged(F2(d_iq), nframes, S, R, C, prefix, nullptr, w, F2(d_out), 3, s);
 }
@@ -304,12 +316,12 @@ int ofdm_frame_demod(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int
     if ((rc = carve(d_ws, ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
     hipStream_t s = hs(stream);
     if (fused_c(C)) {
-        rc = hip_check(ofdm::launch_ls_td1024(F2(d_iq), nframes, S, R, prefix, F2(d_X), w.Hc, w.P, 0, s),
-                       "ls_td1024");
+        rc = hip_check(ls_fused(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w.Hc, w.P, 0, s),
+                       "ls_fused");
         if (rc) return rc;
-        return hip_check(ofdm::launch_mrc_td1024(F2(d_iq), nframes, S, R, prefix, w.Hc, w.P,
+        return hip_check(mrc_fused(F2(d_iq), nframes, S, R, C, prefix, w.Hc, w.P,
                                                  F2(d_out), 0, s),
-                         "mrc_td1024");
+                         "mrc_fused");
     }
     return td_staged(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w, F2(d_out), 0, s);
 }
@@ -346,8 +358,8 @@ int ofdm_frame_ls_partial(const ofdm_cf32 *d_iq, long long nframes, int S, int R
     if ((rc = carve(d_ws, ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
     hipStream_t s = hs(stream);
     if (fused_c(C))
-        rc = hip_check(ofdm::launch_ls_td1024(F2(d_iq), nframes, S, R, prefix, F2(d_X), w.Hc, w.P, 1, s),
-                       "ls_td1024");
+        rc = hip_check(ls_fused(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w.Hc, w.P, 1, s),
+                       "ls_fused");
     else
         rc = td_staged(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w, nullptr, 2, s);
     if (rc) return rc;
@@ -368,9 +380,9 @@ int ofdm_frame_mrc_partial(const ofdm_cf32 *d_iq, long long nframes, int S, int 
     if ((rc = carve(d_ws, ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
     hipStream_t s = hs(stream);
     if (fused_c(C))
-        return hip_check(ofdm::launch_mrc_td1024(F2(d_iq), nframes, S, R, prefix, w.Hc, w.P,
+        return hip_check(mrc_fused(F2(d_iq), nframes, S, R, C, prefix, w.Hc, w.P,
                                                  F2(d_num), 1, s),
-                         "mrc_td1024");
+                         "mrc_fused");
     return td_staged(F2(d_iq), nframes, S, R, C, prefix, nullptr, w, F2(d_num), 1, s);
 }
 

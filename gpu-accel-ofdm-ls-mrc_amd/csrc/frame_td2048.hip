@@ -1,0 +1,229 @@
+// frame_td2048.hip -- fused time-domain receiver for C = 2048 subcarriers
+// (BASELINE configs[2]: 2048 subcarriers x 64 antennas).
+//
+// Same flow as frame_td.hip (one HBM pass over the IQ: demodOneFrameCUDA,
+// gpuLS.cu:575-675, without its six re-reads), with a 2048-point FFT on one
+// 64-lane wave built from the 1024-point wave FFT (wave_fft1024.hpp) by one
+// decimation-in-frequency step done in registers:
+//   lane t loads x[t + 64 m] and x[1024 + t + 64 m], m < 16;
+//   u[n] = x[n] + x[n + 1024]               -> FFT1024 -> X[2 k]
+//   v[n] = (x[n] - x[n + 1024]) W2048^n     -> FFT1024 -> X[2 k + 1]
+// so lane (q, a) owns the bin pairs (2 b, 2 b + 1), b = b0(t) + 16 k.
+//
+// Hc "lane order" for C = 2048: per (frame, antenna) 1024 float4, float4
+// k*64 + t = (Hc[2 b], Hc[2 b + 1]) of lane t's k-th pair -- 16 coalesced
+// dwordx4 wave loads per row.  P stays bin-indexed [F][C].
+#include "launch.hpp"
+#include "wave_fft1024.hpp"
+
+#include <stdlib.h>
+
+namespace ofdm {
+namespace td2048 {
+
+using td1024::lane_bin0;
+using td1024::row_load;
+namespace hl = td1024::hlds;
+
+constexpr int C = 2048;
+constexpr int K = C - 1;
+constexpr int HALF = 1024;
+constexpr int TWV = 16 * 64;  // W2048^(t + 64 m), [m][t]
+// LDS: TW1s | TW2s | TWV | per-wave transpose images
+constexpr int TAB = hl::TW1S + hl::TW2S + TWV;
+constexpr size_t lds_bytes(int waves) { return (size_t)(TAB + waves * hl::TS) * sizeof(float2); }
+
+__device__ __forceinline__ void fill_tables(float2 *lds) {
+    hl::fill(lds, lds + hl::TW1S);
+    float2 *twv = lds + hl::TW1S + hl::TW2S;
+    for (int i = threadIdx.x; i < TWV; i += blockDim.x) {
+        const int m = i / 64, t = i % 64;
+        twv[i] = g_tw[(t + 64 * m) * (OFDM_TW_N / C)];
+    }
+}
+
+// FFT of one 2048-sample row (src) -> xe[k] = X[2 b], xo[k] = X[2 b + 1]
+template <bool NT>
+__device__ __forceinline__ void row_fft2048(const float2 *__restrict__ src, int t, float2 *T,
+                                            const float2 *lds, float2 (&xe)[16], float2 (&xo)[16]) {
+    const float2 *tw1 = lds, *tw2 = lds + hl::TW1S, *twv = lds + hl::TW1S + hl::TW2S;
+    float2 u[16], v[16];
+    row_load<NT>(src, t, u);
+    row_load<NT>(src + HALF, t, v);
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        const float2 d = csub(u[m], v[m]);
+        u[m] = cadd(u[m], v[m]);
+        v[m] = cmul(d, twv[m * 64 + t]);
+    }
+    hl::row_fft_a(u, t, T, tw1);
+    hl::row_fft_b(t, T, tw2, xe);
+    hl::row_fft_a(v, t, T, tw1);
+    hl::row_fft_b(t, T, tw2, xo);
+}
+
+// ---------------------------------------------------------------------------
+// LS: one workgroup (4 waves) per frame, wave w takes antenna rows w, w+4, ...
+// Pilots (K values) in LDS; partial |H|^2 per wave combined in wave order.
+// ---------------------------------------------------------------------------
+constexpr int LS_WAVES = 4;
+constexpr size_t LS_LDS = lds_bytes(LS_WAVES) + (size_t)C * sizeof(float2);
+
+__global__ void __launch_bounds__(256) k_ls_td2048(const float2 *__restrict__ iq, int S, int R,
+                                                   int prefix, const float2 *__restrict__ X,
+                                                   float2 *__restrict__ Hc, float *__restrict__ P,
+                                                   int partial) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int w = threadIdx.x >> 6, t = threadIdx.x & 63;
+    float2 *T = lds + TAB + w * hl::TS;
+    float2 *xs = lds + TAB + LS_WAVES * hl::TS;  // xs[b] = X[b - 1], xs[0] unused
+    fill_tables(lds);
+    for (int b = threadIdx.x; b < C; b += blockDim.x) xs[b] = b ? X[b - 1] : float2{1.f, 0.f};
+    __syncthreads();
+
+    const long long f = blockIdx.x;
+    const int Cp = C + prefix;
+    const float2 *pilot = iq + f * (long long)S * R * Cp + prefix;
+    float4 *Hf = reinterpret_cast<float4 *>(Hc + f * (long long)R * C);
+    const int b0 = lane_bin0(t);
+    float pe[16], po[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) pe[k] = po[k] = 0.f;
+    for (int r = w; r < R; r += LS_WAVES) {
+        float2 xe[16], xo[16];
+        row_fft2048<false>(pilot + (long long)r * Cp, t, T, lds, xe, xo);
+        float4 *hr = Hf + (long long)r * (C / 2);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int be = 2 * (b0 + 16 * k);
+            // divideOneRow + conj (cpuLS.hpp:233-244, 303-307); DC bin dropped
+            float2 he = ls_conj(xe[k], xs[be]);
+            if (be == 0) he = float2{0.f, 0.f};
+            const float2 ho = ls_conj(xo[k], xs[be + 1]);
+            pe[k] = pe[k] + (he.x * he.x) + (he.y * he.y);  // findDistSqrd order
+            po[k] = po[k] + (ho.x * ho.x) + (ho.y * ho.y);
+            hr[k * 64 + t] = float4{he.x, he.y, ho.x, ho.y};
+        }
+    }
+    __syncthreads();
+    float *pp = reinterpret_cast<float *>(lds + TAB);  // [LS_WAVES][C], reuses T
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int be = 2 * (b0 + 16 * k);
+        pp[w * C + be] = pe[k];
+        pp[w * C + be + 1] = po[k];
+    }
+    __syncthreads();
+    float *Pf = P + f * C;
+    for (int b = threadIdx.x; b < C; b += blockDim.x) {
+        float sum = pp[b];
+        for (int i = 1; i < LS_WAVES; ++i) sum = sum + pp[i * C + b];  // antennas in order
+        Pf[b] = b == 0 ? (partial ? 0.f : 1.f) : sum;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// MRC: one wave per data symbol, MRC_WAVES consecutive symbols per workgroup,
+// XCD-grouped block order (as k_mrc_td1024).  ~190 VGPRs -> 2 waves/SIMD.
+// mode 0: out[q][out_pos(j)] = acc / P;  mode 1: out[q][j] = acc (numerator)
+// ---------------------------------------------------------------------------
+constexpr int MRC_WAVES = 4;
+
+template <bool NT>
+__global__ void __attribute__((amdgpu_flat_work_group_size(256, 256), amdgpu_waves_per_eu(2, 2)))
+k_mrc_td2048(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
+             const float *__restrict__ P, float2 *__restrict__ out, long long nq, long long nblocks,
+             long long per_xcd, int mode) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int w = threadIdx.x >> 6, t = threadIdx.x & 63;
+    float2 *T = lds + TAB + w * hl::TS;
+    const long long pb = blockIdx.x;
+    const long long lb = (pb & 7) * per_xcd + (pb >> 3);
+    if (lb >= nblocks) return;
+    fill_tables(lds);
+    __syncthreads();
+    const long long q = lb * MRC_WAVES + w;
+    if (q >= nq) return;  // no block-level sync follows
+
+    const int nsym = S - 1;
+    const long long f = q / nsym;
+    const int s = 1 + (int)(q % nsym);
+    const int Cp = C + prefix;
+    const float2 *sym = iq + (f * S + s) * (long long)R * Cp + prefix;
+    const float4 *Hf = reinterpret_cast<const float4 *>(Hc + f * (long long)R * C);
+
+    float2 ae[16], ao[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) ae[k] = ao[k] = float2{0.f, 0.f};
+    for (int r = 0; r < R; ++r) {
+        float2 xe[16], xo[16];
+        row_fft2048<NT>(sym + (long long)r * Cp, t, T, lds, xe, xo);
+        __builtin_amdgcn_sched_barrier(0);
+        const float4 *hr = Hf + (long long)r * (C / 2);
+        // matrixMultThenSum (cpuLS.hpp:203-204), antennas in order
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const float4 h = hr[k * 64 + t];
+            ae[k].x = ae[k].x + (xe[k].x * h.x - xe[k].y * h.y);
+            ae[k].y = ae[k].y + (xe[k].x * h.y + xe[k].y * h.x);
+            ao[k].x = ao[k].x + (xo[k].x * h.z - xo[k].y * h.w);
+            ao[k].y = ao[k].y + (xo[k].x * h.w + xo[k].y * h.z);
+        }
+    }
+    const int b0 = lane_bin0(t);
+    float2 *o = out + q * K;
+    if ((mode & 1) == 0) {
+        const float *Pf = P + f * C;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int be = 2 * (b0 + 16 * k);
+            if (be > 0) {
+                const float pv = Pf[be];
+                o[out_pos(be - 1, K)] = float2{ae[k].x / pv, ae[k].y / pv};
+            }
+            const float pv = Pf[be + 1];
+            o[out_pos(be, K)] = float2{ao[k].x / pv, ao[k].y / pv};
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int be = 2 * (b0 + 16 * k);
+            if (be > 0) o[be - 1] = ae[k];
+            o[be] = ao[k];
+        }
+    }
+}
+
+}  // namespace td2048
+
+hipError_t launch_ls_td2048(const float2 *iq, long long nframes, int S, int R, int prefix,
+                            const float2 *X, float2 *Hc, float *P, int partial, hipStream_t s) {
+    using namespace td2048;
+    if (nframes <= 0) return hipSuccess;
+    if (nframes > 0x7fffffffll) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_ls_td2048, dim3((unsigned)nframes), dim3(64 * LS_WAVES), LS_LDS, s, iq, S, R,
+                       prefix, X, Hc, P, partial);
+    return hipGetLastError();
+}
+
+hipError_t launch_mrc_td2048(const float2 *iq, long long nframes, int S, int R, int prefix,
+                             const float2 *Hc, const float *P, float2 *out, int mode, hipStream_t s) {
+    using namespace td2048;
+    const long long nq = nframes * (S - 1);
+    if (nq <= 0) return hipSuccess;
+    const long long nblocks = (nq + MRC_WAVES - 1) / MRC_WAVES;
+    const long long per_xcd = (nblocks + 7) / 8;
+    const long long grid = per_xcd * 8;
+    if (grid > 0x7fffffffll) return hipErrorInvalidValue;
+    if (getenv("OFDM_MRC_NTLOAD") && getenv("OFDM_MRC_NTLOAD")[0] == '0')
+        hipLaunchKernelGGL((k_mrc_td2048<false>), dim3((unsigned)grid), dim3(64 * MRC_WAVES),
+                           lds_bytes(MRC_WAVES), s, iq, S, R, prefix, Hc, P, out, nq, nblocks, per_xcd,
+                           mode);
+    else
+        hipLaunchKernelGGL((k_mrc_td2048<true>), dim3((unsigned)grid), dim3(64 * MRC_WAVES),
+                           lds_bytes(MRC_WAVES), s, iq, S, R, prefix, Hc, P, out, nq, nblocks, per_xcd,
+                           mode);
+    return hipGetLastError();
+}
+
+}  // namespace ofdm

@@ -1,0 +1,246 @@
+// wave_fft1024.hpp -- 1024-point forward FFT on one 64-lane wave (CDNA4),
+// shared by the fused receiver kernels (frame_td.hip, frame_td2048.hip).
+//
+// Four-step, N = 64 x 16: lane t holds x[t + 64 m], m < 16.
+//   A[t][k2]  = FFT16_m(x[t + 64 m]) * W1024^(t k2)                 k2 < 16
+//   X[k2 + 16 k1] = DFT64_t(A[t][k2])                                k1 < 64
+// The 64-point DFTs run on lane quads after an LDS transpose: lane
+// t = 4 q + a (q = k2, a < 4) holds A[a + 4 l'][q], l' < 16, and
+//   B_a[k'] = FFT16_l'(A[a + 4 l'][q]) * W64^(a k')                   k' < 16
+//   X[q + 16 (k' + 16 c)] = sum_a B_a[k'] W4^(a c)                    c < 4
+// the last sum being a radix-2 x 2 exchange inside the quad (DPP).  Lane
+// (q, a) finally owns bins b = q + 256 c(a) + 16 k', c(a) = (a >> 1) + 2 (a & 1).
+#pragma once
+#include "common.hpp"
+
+namespace ofdm {
+namespace td1024 {
+
+constexpr int C = 1024;
+constexpr int K = C - 1;
+constexpr int TP = 68;              // pitch of the [16][64] transpose image (conflict free)
+constexpr int TBUF = 16 * TP;       // float2 per wave
+constexpr int TW1P = 17;            // pitch of TW1[t][k2] = W1024^(t k2)
+constexpr int TW1BUF = 64 * TW1P;
+constexpr int TW2P = 17;            // pitch of TW2[a][k'] = g(a) W64^(a k'): 4 rows on 4 banks
+constexpr int TW2BUF = 4 * TW2P;
+constexpr int TWBUF = TW1BUF + TW2BUF;
+
+__device__ __forceinline__ void wave_lds_sync() {
+    // LDS operations of one wave execute in order; this only stops the
+    // compiler from moving LDS accesses across the exchange point.
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Quad-DFT signs (found by exhaustive search, verified in tests): lane a of a
+// quad pre-scales its B_a by g(a) (folded into TW2) so that both radix-2
+// stages are one fma(dpp(x), S, x) per float with exact results:
+//   g = (1,-1,-1,1), S1 = (-1,-1,1,1) [partner a^2], S2 = (-1,1,-1,1) [a^1],
+//   lane 3 multiplies by -i between the stages.
+__device__ __forceinline__ float quad_g(int a) { return (a == 0 || a == 3) ? 1.f : -1.f; }
+
+__device__ __forceinline__ void fill_twiddles(float2 *tw) {
+    for (int i = threadIdx.x; i < TW1BUF; i += blockDim.x) {
+        const int t = i / TW1P, k2 = i % TW1P;
+        tw[i] = k2 < 16 ? g_tw[((t * k2) & (C - 1)) * (OFDM_TW_N / C)] : float2{0.f, 0.f};
+    }
+    for (int i = threadIdx.x; i < TW2BUF; i += blockDim.x) {
+        const int a = i / TW2P, k = i % TW2P;
+        const float2 w = g_tw[((16 * a * k) & (C - 1)) * (OFDM_TW_N / C)];
+        const float g = quad_g(a);
+        tw[TW1BUF + i] = k < 16 ? float2{g * w.x, g * w.y} : float2{0.f, 0.f};
+    }
+}
+
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL,
+                                                              0xF, 0xF, true));
+}
+constexpr int DPP_XOR1 = 0xB1;  // quad_perm [1,0,3,2]
+constexpr int DPP_XOR2 = 0x4E;  // quad_perm [2,3,0,1]
+
+// a[m] = src[t + 64 m]: 16 coalesced 512-byte wave loads.  NT: non-temporal
+// (streamed once; keeps L2 for the per-frame channel estimates).
+template <bool NT = false>
+__device__ __forceinline__ void row_load(const float2 *__restrict__ src, int t, float2 (&a)[16]) {
+    if (NT) {
+        const unsigned long long *p = reinterpret_cast<const unsigned long long *>(src) + t;
+#pragma unroll
+        for (int m = 0; m < 16; ++m)
+            a[m] = __builtin_bit_cast(float2, __builtin_nontemporal_load(p + 64 * m));
+    } else {
+#pragma unroll
+        for (int m = 0; m < 16; ++m) a[m] = src[t + 64 * m];
+    }
+}
+
+// v[k] = dpp(v[k]) * S + v[k] for 16 floats, one v_fmac_f32_dpp each (the
+// compiler would emit v_mov_dpp + fma + an s_nop per value).  The leading
+// s_nop 1 covers the "VALU writes VGPR -> DPP reads it" hazard (2 wait states)
+// for whatever the compiler computed last; inside the block no instruction
+// reads another's output (cdna_hip_programming.md 5.7).
+#define OFDM_DPP_Q(CTRL) "quad_perm:" CTRL " row_mask:0xf bank_mask:0xf"
+template <int CTRL>
+__device__ __forceinline__ void quad_fmac_dpp(float (&v)[16], float S) {
+#define OFDM_F(i) "v_fmac_f32_dpp %" #i ", %" #i ", %16 " OFDM_DPP_Q(QP) "\n\t"
+    if constexpr (CTRL == 0x4E) {
+#define QP "[2,3,0,1]"
+        asm("s_nop 1\n\t" OFDM_F(0) OFDM_F(1) OFDM_F(2) OFDM_F(3) OFDM_F(4) OFDM_F(5) OFDM_F(6)
+                OFDM_F(7) OFDM_F(8) OFDM_F(9) OFDM_F(10) OFDM_F(11) OFDM_F(12) OFDM_F(13) OFDM_F(14)
+                    OFDM_F(15)
+            : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),
+              "+v"(v[7]), "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]),
+              "+v"(v[13]), "+v"(v[14]), "+v"(v[15])
+            : "v"(S));
+#undef QP
+    } else {
+        static_assert(CTRL == 0xB1, "quad xor 1 or xor 2");
+#define QP "[1,0,3,2]"
+        asm("s_nop 1\n\t" OFDM_F(0) OFDM_F(1) OFDM_F(2) OFDM_F(3) OFDM_F(4) OFDM_F(5) OFDM_F(6)
+                OFDM_F(7) OFDM_F(8) OFDM_F(9) OFDM_F(10) OFDM_F(11) OFDM_F(12) OFDM_F(13) OFDM_F(14)
+                    OFDM_F(15)
+            : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),
+              "+v"(v[7]), "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]),
+              "+v"(v[13]), "+v"(v[14]), "+v"(v[15])
+            : "v"(S));
+#undef QP
+    }
+#undef OFDM_F
+}
+#undef OFDM_DPP_Q
+
+// 4-point DFT over the lanes of each quad (see header), in place.
+__device__ __forceinline__ void quad_dft(float2 (&x)[16], int qa) {
+    // two radix-2 stages, one fma per float each
+    const float S1 = (qa & 2) ? 1.f : -1.f;
+    const float S2 = (qa & 1) ? 1.f : -1.f;
+    // lanes with qa == 3 multiply by -i between the stages: (x, y) -> (y, -x)
+    const unsigned long long rot = __builtin_amdgcn_ballot_w64(qa == 3);
+    float xr[16], xi[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) { xr[k] = x[k].x; xi[k] = x[k].y; }
+    quad_fmac_dpp<DPP_XOR2>(xr, S1);
+    quad_fmac_dpp<DPP_XOR2>(xi, S1);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        float nx;
+        asm("v_cndmask_b32_e64 %0, %2, %3, %4\n\tv_cndmask_b32_e64 %1, %3, -%2, %4"
+            : "=&v"(nx), "=v"(xi[k])
+            : "v"(xr[k]), "v"(xi[k]), "s"(rot));
+        xr[k] = nx;
+    }
+    quad_fmac_dpp<DPP_XOR1>(xr, S2);
+    quad_fmac_dpp<DPP_XOR1>(xi, S2);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) x[k] = float2{xr[k], xi[k]};
+}
+
+// Forward 1024-point FFT of the row held in a[] (see header); T is this
+// wave's transpose region.  On return x[k'] = X[b0 + 16 k'],
+// b0 = (t >> 2) + 256 c(t & 3).
+__device__ __forceinline__ void row_fft(float2 (&a)[16], int t, float2 *T, const float2 *tw,
+                                        float2 (&x)[16]) {
+    fft_reg<16, false>(a);
+#pragma unroll
+    for (int k2 = 1; k2 < 16; ++k2) a[k2] = cmul(a[k2], tw[t * TW1P + k2]);
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2) T[k2 * TP + t] = a[k2];
+    wave_lds_sync();
+    const int q = t >> 2, qa = t & 3;
+#pragma unroll
+    for (int l = 0; l < 16; ++l) x[l] = T[q * TP + qa + 4 * l];
+    wave_lds_sync();
+    fft_reg<16, false>(x);
+    const float2 *tw2 = tw + TW1BUF + qa * TW2P;
+    const float g = quad_g(qa);
+    x[0] = float2{g * x[0].x, g * x[0].y};
+#pragma unroll
+    for (int k = 1; k < 16; ++k) x[k] = cmul(x[k], tw2[k]);
+    quad_dft(x, qa);
+}
+
+__device__ __forceinline__ int lane_bin0(int t) {
+    const int qa = t & 3;
+    return (t >> 2) + 256 * ((qa >> 1) + 2 * (qa & 1));
+}
+
+// Channel estimates of one (frame, antenna row) in "lane order": the 16 bins
+// lane t owns (b0(t) + 16 k) as 8 float4 pairs, pair i of lane t at float4
+// index i*64 + t -- one contiguous 1 KiB wave load per pair.  Same 8 KiB per
+// row as the bin layout; written by k_ls_td1024, read by k_mrc_td1024.
+__device__ __forceinline__ void hc_store(float4 *__restrict__ dst, int t, const float2 (&h)[16]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        dst[i * 64 + t] = float4{h[2 * i].x, h[2 * i].y, h[2 * i + 1].x, h[2 * i + 1].y};
+}
+__device__ __forceinline__ void hc_load(const float4 *__restrict__ src, int t, float2 (&h)[16]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const float4 v = src[i * 64 + t];
+        h[2 * i] = float2{v.x, v.y};
+        h[2 * i + 1] = float2{v.z, v.w};
+    }
+}
+
+// Twiddle tables and the two FFT halves in the LDS layout of the HLDS
+// kernels (k_mrc_td1024_hlds, frame_td2048.hip); see frame_td.hip.
+namespace hlds {
+constexpr int TW1S = 15 * 64;
+constexpr int TW2S = 16 * 4;
+constexpr int TP = 68;
+constexpr int TS = 16 * TP;
+constexpr int WAVES = 8;
+constexpr size_t LDS_BYTES = (TW1S + TW2S + WAVES * TS) * sizeof(float2) + 256 * sizeof(float4);
+static_assert(LDS_BYTES == 81920, "two workgroups per CU");
+
+// slot of Hc float4 j (0..511) of the staged row; T0 = first transpose image
+__device__ __forceinline__ float4 *hslot(float2 *T0, float4 *hfree, int j) {
+    if (j < 256) return hfree + j;
+    const int jj = j - 256;  // wave image jj>>5, row (jj>>1)&15, tail half jj&1
+    return reinterpret_cast<float4 *>(T0 + (jj >> 5) * TS + ((jj >> 1) & 15) * TP + 64 + 2 * (jj & 1));
+}
+
+__device__ __forceinline__ void fill(float2 *tw1, float2 *tw2) {
+    for (int i = threadIdx.x; i < TW1S; i += blockDim.x) {
+        const int k2 = 1 + i / 64, t = i % 64;
+        tw1[i] = g_tw[((t * k2) & (C - 1)) * (OFDM_TW_N / C)];
+    }
+    for (int i = threadIdx.x; i < TW2S; i += blockDim.x) {
+        const int k = i / 4, a = i % 4;
+        const float2 w = g_tw[((16 * a * k) & (C - 1)) * (OFDM_TW_N / C)];
+        const float g = quad_g(a);
+        tw2[i] = float2{g * w.x, g * w.y};
+    }
+}
+// index of (row, col) in a transpose image
+__device__ __forceinline__ int swz(int row, int col) { return row * TP + col; }
+
+// first half: radix-16 over m, twiddles, transpose write
+__device__ __forceinline__ void row_fft_a(float2 (&a)[16], int t, float2 *T, const float2 *tw1) {
+    fft_reg<16, false>(a);
+#pragma unroll
+    for (int k2 = 1; k2 < 16; ++k2) a[k2] = cmul(a[k2], tw1[(k2 - 1) * 64 + t]);
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2) T[swz(k2, t)] = a[k2];
+}
+// second half: transpose read, radix-16, twiddles, quad DFT
+__device__ __forceinline__ void row_fft_b(int t, float2 *T, const float2 *tw2, float2 (&x)[16]) {
+    wave_lds_sync();
+    const int q = t >> 2, qa = t & 3;
+#pragma unroll
+    for (int l = 0; l < 16; ++l) x[l] = T[swz(q, qa + 4 * l)];
+    wave_lds_sync();
+    fft_reg<16, false>(x);
+    const float g = quad_g(qa);
+    x[0] = float2{g * x[0].x, g * x[0].y};
+#pragma unroll
+    for (int k = 1; k < 16; ++k) x[k] = cmul(x[k], tw2[k * 4 + qa]);
+    quad_dft(x, qa);
+}
+}  // namespace hlds
+
+}  // namespace td1024
+}  // namespace ofdm

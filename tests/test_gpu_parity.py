@@ -147,7 +147,7 @@ def test_empty_batch_is_noop(ofdm, dev):
 
 # ------------------------------------------ antenna split (partial MRC path)
 
-@pytest.mark.parametrize("C,prefix", [(1024, 0), (1024, 16), (256, 0)])
+@pytest.mark.parametrize("C,prefix", [(1024, 0), (1024, 16), (2048, 0), (2048, 12), (256, 0)])
 def test_antenna_split_matches_full(ofdm, dev, C, prefix):
     """Two antenna shards: partial |H|^2 and partial numerators summed, then
     finalised == the single-GPU result on all antennas."""
