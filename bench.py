@@ -184,7 +184,7 @@ def main():
            "data_symbols_per_gpu": Q, "global_data_symbols": Q * world,
            "parallelism": f"frame-sharded x{world}, no collective"}
     b_sym = R * C * 8 + K * 8
-    kern = {1024: "k_mrc_td1024_hlds", 2048: "k_mrc_td2048"}.get(C)
+    kern = {1024: "k_mrc_td1024_hlds", 2048: "k_mrc_td2048", 4096: "k_mrc_td4096"}.get(C)
     mrc_name = f"{kern} (FFT+MRC+normalise+rotate)" if kern else "k_fft_rows + k_mrc_freq (staged)"
     achieved = Q * b_sym / (mrc_ms * 1e-3) / 1e9
     traffic, tsrc = pmc_traffic(args.pmc, cfg)

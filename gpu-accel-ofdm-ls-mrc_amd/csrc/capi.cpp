@@ -40,18 +40,20 @@ inline bool aligned(const void *p, size_t a) { return (reinterpret_cast<uintptr_
 size_t up256(size_t x) { return (x + 255) & ~size_t(255); }
 
 // fused one-pass kernels exist for these FFT sizes
-bool fused_c(int C) { return C == 1024 || C == 2048; }
+bool fused_c(int C) { return C == 1024 || C == 2048 || C == 4096; }
 
 // fused time-domain kernels by C (fused_c(C) must hold)
 hipError_t ls_fused(const float2 *iq, long long F, int S, int R, int C, int prefix, const float2 *X,
                     float2 *Hc, float *P, int partial, hipStream_t s) {
-    return C == 1024 ? ofdm::launch_ls_td1024(iq, F, S, R, prefix, X, Hc, P, partial, s)
-                     : ofdm::launch_ls_td2048(iq, F, S, R, prefix, X, Hc, P, partial, s);
+    if (C == 1024) return ofdm::launch_ls_td1024(iq, F, S, R, prefix, X, Hc, P, partial, s);
+    if (C == 2048) return ofdm::launch_ls_td2048(iq, F, S, R, prefix, X, Hc, P, partial, s);
+    return ofdm::launch_ls_td4096(iq, F, S, R, prefix, X, Hc, P, partial, s);
 }
 hipError_t mrc_fused(const float2 *iq, long long F, int S, int R, int C, int prefix, const float2 *Hc,
                      const float *P, float2 *out, int mode, hipStream_t s) {
-    return C == 1024 ? ofdm::launch_mrc_td1024(iq, F, S, R, prefix, Hc, P, out, mode, s)
-                     : ofdm::launch_mrc_td2048(iq, F, S, R, prefix, Hc, P, out, mode, s);
+    if (C == 1024) return ofdm::launch_mrc_td1024(iq, F, S, R, prefix, Hc, P, out, mode, s);
+    if (C == 2048) return ofdm::launch_mrc_td2048(iq, F, S, R, prefix, Hc, P, out, mode, s);
+    return ofdm::launch_mrc_td4096(iq, F, S, R, prefix, Hc, P, out, mode, s);
 }
 
 long long staging_frames(long long nframes, int S, int R, int C) {

@@ -1,0 +1,280 @@
+// frame_td4096.hip -- fused time-domain receiver for C = 4096 subcarriers
+// (BASELINE configs[4]: 4096 subcarriers, 256 antennas split 32 per GPU).
+//
+// A 4096-point row is shared by a PAIR of waves.  Wave e (0 or 1) of the
+// pair computes the bins X[2 k + e] by one decimation-in-frequency step:
+//   y_e[n] = (x[n] + (-1)^e x[n + 2048]) W4096^(e n),  n < 2048
+//   X[2 k + e] = FFT2048(y_e)[k]
+// and FFT2048 is done as in frame_td2048.hip (u/v split in registers + two
+// 1024-point wave FFTs).  Each wave reads the whole row; a workgroup barrier
+// per antenna row keeps the two waves of a pair together so that the
+// partner's read of the same 32 KiB hits L2 (without it the fabric carries
+// every row twice: profiles/, PMC ratio 2.02) -- no LDS exchange needed.
+// Lane (q, a) of wave e owns bins 4 b + e and 4 b + 2 + e, b = b0(t) + 16 k.
+//
+// Hc "lane order" for C = 4096: per (frame, antenna) 2048 float4; float4
+// e*1024 + k*64 + t = (Hc[4 b + e], Hc[4 b + 2 + e]).  P bin-indexed [F][C].
+#include "launch.hpp"
+#include "wave_fft1024.hpp"
+
+#include <stdlib.h>
+
+namespace ofdm {
+namespace td4096 {
+
+using td1024::lane_bin0;
+using td1024::row_load;
+namespace hl = td1024::hlds;
+
+constexpr int C = 4096;
+constexpr int K = C - 1;
+constexpr int TWV = 16 * 64;  // W2048^(t + 64 m), m < 16, [m][t]
+constexpr int TWE = 32 * 64;  // W4096^(t + 64 m), m < 32, [m][t]
+// LDS: TW1s | TW2s | TWV | TWE | per-wave transpose images
+constexpr int TAB = hl::TW1S + hl::TW2S + TWV + TWE;
+constexpr size_t lds_bytes(int waves) { return (size_t)(TAB + waves * hl::TS) * sizeof(float2); }
+
+__device__ __forceinline__ void fill_tables(float2 *lds) {
+    hl::fill(lds, lds + hl::TW1S);
+    float2 *twv = lds + hl::TW1S + hl::TW2S;
+    for (int i = threadIdx.x; i < TWV; i += blockDim.x) {
+        const int m = i / 64, t = i % 64;
+        twv[i] = g_tw[(t + 64 * m) * (OFDM_TW_N / 2048)];
+    }
+    float2 *twe = twv + TWV;
+    for (int i = threadIdx.x; i < TWE; i += blockDim.x) {
+        const int m = i / 64, t = i % 64;
+        twe[i] = g_tw[(t + 64 * m) * (OFDM_TW_N / C)];
+    }
+}
+
+// wave e's half of the FFT of one 4096-sample row:
+//   xe[k] = X[4 b + e], xo[k] = X[4 b + 2 + e]
+template <int E, bool NT>
+__device__ __forceinline__ void row_fft4096(const float2 *__restrict__ src, int t, float2 *T,
+                                            const float2 *lds, float2 (&xe)[16], float2 (&xo)[16]) {
+    const float2 *tw1 = lds, *tw2 = lds + hl::TW1S;
+    const float2 *twv = lds + hl::TW1S + hl::TW2S, *twe = twv + TWV;
+    float2 lo[16], hi[16];
+    {
+        float2 b[16];
+        row_load<NT>(src, t, lo);
+        row_load<NT>(src + 2048, t, b);
+#pragma unroll
+        for (int m = 0; m < 16; ++m)
+            lo[m] = E ? cmul(csub(lo[m], b[m]), twe[m * 64 + t]) : cadd(lo[m], b[m]);
+        row_load<NT>(src + 1024, t, hi);
+        row_load<NT>(src + 3072, t, b);
+#pragma unroll
+        for (int m = 0; m < 16; ++m)
+            hi[m] = E ? cmul(csub(hi[m], b[m]), twe[(m + 16) * 64 + t]) : cadd(hi[m], b[m]);
+    }
+    // FFT2048 of y = (lo, hi): u = lo + hi -> even bins, v = (lo - hi) W2048^n -> odd
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        const float2 d = csub(lo[m], hi[m]);
+        lo[m] = cadd(lo[m], hi[m]);
+        hi[m] = cmul(d, twv[m * 64 + t]);
+    }
+    hl::row_fft_a(lo, t, T, tw1);
+    hl::row_fft_b(t, T, tw2, xe);
+    hl::row_fft_a(hi, t, T, tw1);
+    hl::row_fft_b(t, T, tw2, xo);
+}
+
+// ---------------------------------------------------------------------------
+// LS: one workgroup (2 wave pairs) per frame; pair j takes antenna rows j,
+// j+2, ...  Pilots in LDS; partial |H|^2 per pair combined in pair order.
+// ---------------------------------------------------------------------------
+constexpr int LS_WAVES = 4;
+constexpr int LS_PAIRS = LS_WAVES / 2;
+constexpr size_t LS_LDS = lds_bytes(LS_WAVES) + (size_t)C * sizeof(float2);
+
+template <int E>
+__device__ __forceinline__ void ls_rows(const float2 *pilot, int Cp, int R, int j, int t, float2 *T,
+                                        const float2 *lds, const float2 *xs, float4 *Hf, float *pp) {
+    const int b0 = lane_bin0(t);
+    float pe[16], po[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) pe[k] = po[k] = 0.f;
+    for (int r = j; r < R; r += LS_PAIRS) {
+        float2 xe[16], xo[16];
+        row_fft4096<E, false>(pilot + (long long)r * Cp, t, T, lds, xe, xo);
+        float4 *hr = Hf + (long long)r * (C / 2) + E * 1024;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int be = 4 * (b0 + 16 * k) + E;
+            // divideOneRow + conj (cpuLS.hpp:233-244, 303-307); DC bin dropped
+            float2 he = ls_conj(xe[k], xs[be]);
+            if (be == 0) he = float2{0.f, 0.f};
+            const float2 ho = ls_conj(xo[k], xs[be + 2]);
+            pe[k] = pe[k] + (he.x * he.x) + (he.y * he.y);  // findDistSqrd order
+            po[k] = po[k] + (ho.x * ho.x) + (ho.y * ho.y);
+            hr[k * 64 + t] = float4{he.x, he.y, ho.x, ho.y};
+        }
+    }
+    __syncthreads();  // every wave is done with its transpose image (pp reuses it)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int be = 4 * (b0 + 16 * k) + E;
+        pp[j * C + be] = pe[k];
+        pp[j * C + be + 2] = po[k];
+    }
+}
+
+__global__ void __launch_bounds__(256) k_ls_td4096(const float2 *__restrict__ iq, int S, int R,
+                                                   int prefix, const float2 *__restrict__ X,
+                                                   float2 *__restrict__ Hc, float *__restrict__ P,
+                                                   int partial) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int w = threadIdx.x >> 6, t = threadIdx.x & 63;
+    float2 *T = lds + TAB + w * hl::TS;
+    float2 *xs = lds + TAB + LS_WAVES * hl::TS;  // xs[b] = X[b - 1], xs[0] unused
+    fill_tables(lds);
+    for (int b = threadIdx.x; b < C; b += blockDim.x) xs[b] = b ? X[b - 1] : float2{1.f, 0.f};
+    __syncthreads();
+
+    const long long f = blockIdx.x;
+    const int Cp = C + prefix;
+    const float2 *pilot = iq + f * (long long)S * R * Cp + prefix;
+    float4 *Hf = reinterpret_cast<float4 *>(Hc + f * (long long)R * C);
+    float *pp = reinterpret_cast<float *>(lds + TAB);  // [LS_PAIRS][C], reuses T
+    if (w & 1)
+        ls_rows<1>(pilot, Cp, R, w >> 1, t, T, lds, xs, Hf, pp);
+    else
+        ls_rows<0>(pilot, Cp, R, w >> 1, t, T, lds, xs, Hf, pp);
+    __syncthreads();
+    float *Pf = P + f * C;
+    for (int b = threadIdx.x; b < C; b += blockDim.x) {
+        float sum = pp[b];
+        for (int i = 1; i < LS_PAIRS; ++i) sum = sum + pp[i * C + b];  // antennas in order
+        Pf[b] = b == 0 ? (partial ? 0.f : 1.f) : sum;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// MRC: a wave pair per data symbol, 2 symbols per 4-wave workgroup,
+// XCD-grouped block order.  mode 0: out[q][out_pos(j)] = acc / P;
+// mode 1: out[q][j] = acc (numerator).
+// ---------------------------------------------------------------------------
+constexpr int MRC_WAVES = 4;
+constexpr int MRC_SYMS = MRC_WAVES / 2;
+
+template <int E, bool NT, bool SYNC>
+__device__ __forceinline__ void mrc_symbol(const float2 *sym, int Cp, int R, const float4 *Hf,
+                                           const float *Pf, float2 *o, int mode, int t, float2 *T,
+                                           const float2 *lds, bool store) {
+    float2 ae[16], ao[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) ae[k] = ao[k] = float2{0.f, 0.f};
+    for (int r = 0; r < R; ++r) {
+        float2 xe[16], xo[16];
+        // SYNC: both waves of a pair request the row's lines together, so the
+        // second request hits L2 instead of going to the fabric again
+        if (SYNC) __syncthreads();
+        row_fft4096<E, NT>(sym + (long long)r * Cp, t, T, lds, xe, xo);
+        __builtin_amdgcn_sched_barrier(0);
+        const float4 *hr = Hf + (long long)r * (C / 2) + E * 1024;
+        // matrixMultThenSum (cpuLS.hpp:203-204), antennas in order
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const float4 h = hr[k * 64 + t];
+            ae[k].x = ae[k].x + (xe[k].x * h.x - xe[k].y * h.y);
+            ae[k].y = ae[k].y + (xe[k].x * h.y + xe[k].y * h.x);
+            ao[k].x = ao[k].x + (xo[k].x * h.z - xo[k].y * h.w);
+            ao[k].y = ao[k].y + (xo[k].x * h.w + xo[k].y * h.z);
+        }
+    }
+    if (!store) return;
+    const int b0 = lane_bin0(t);
+    if ((mode & 1) == 0) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int be = 4 * (b0 + 16 * k) + E;
+            if (be > 0) {
+                const float pv = Pf[be];
+                o[out_pos(be - 1, K)] = float2{ae[k].x / pv, ae[k].y / pv};
+            }
+            const float pv = Pf[be + 2];
+            o[out_pos(be + 1, K)] = float2{ao[k].x / pv, ao[k].y / pv};
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int be = 4 * (b0 + 16 * k) + E;
+            if (be > 0) o[be - 1] = ae[k];
+            o[be + 1] = ao[k];
+        }
+    }
+}
+
+template <bool NT, bool SYNC>
+__global__ void __attribute__((amdgpu_flat_work_group_size(256, 256), amdgpu_waves_per_eu(2, 2)))
+k_mrc_td4096(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
+             const float *__restrict__ P, float2 *__restrict__ out, long long nq, long long nblocks,
+             long long per_xcd, int mode) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int w = threadIdx.x >> 6, t = threadIdx.x & 63;
+    float2 *T = lds + TAB + w * hl::TS;
+    const long long pb = blockIdx.x;
+    const long long lb = (pb & 7) * per_xcd + (pb >> 3);
+    if (lb >= nblocks) return;
+    fill_tables(lds);
+    __syncthreads();
+    const long long qw = lb * MRC_SYMS + (w >> 1);
+    const bool store = qw < nq;
+    if (!SYNC && !store) return;  // no block-level sync follows
+    // SYNC: tail pairs repeat the last symbol (without storing) so that every
+    // wave takes part in the per-row barriers
+    const long long q = store ? qw : nq - 1;
+
+    const int nsym = S - 1;
+    const long long f = q / nsym;
+    const int s = 1 + (int)(q % nsym);
+    const int Cp = C + prefix;
+    const float2 *sym = iq + (f * S + s) * (long long)R * Cp + prefix;
+    const float4 *Hf = reinterpret_cast<const float4 *>(Hc + f * (long long)R * C);
+    const float *Pf = P + f * C;
+    float2 *o = out + q * K;
+    if (w & 1)
+        mrc_symbol<1, NT, SYNC>(sym, Cp, R, Hf, Pf, o, mode, t, T, lds, store);
+    else
+        mrc_symbol<0, NT, SYNC>(sym, Cp, R, Hf, Pf, o, mode, t, T, lds, store);
+}
+
+}  // namespace td4096
+
+hipError_t launch_ls_td4096(const float2 *iq, long long nframes, int S, int R, int prefix,
+                            const float2 *X, float2 *Hc, float *P, int partial, hipStream_t s) {
+    using namespace td4096;
+    if (nframes <= 0) return hipSuccess;
+    if (nframes > 0x7fffffffll) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_ls_td4096, dim3((unsigned)nframes), dim3(64 * LS_WAVES), LS_LDS, s, iq, S, R,
+                       prefix, X, Hc, P, partial);
+    return hipGetLastError();
+}
+
+hipError_t launch_mrc_td4096(const float2 *iq, long long nframes, int S, int R, int prefix,
+                             const float2 *Hc, const float *P, float2 *out, int mode, hipStream_t s) {
+    using namespace td4096;
+    const long long nq = nframes * (S - 1);
+    if (nq <= 0) return hipSuccess;
+    const long long nblocks = (nq + MRC_SYMS - 1) / MRC_SYMS;
+    const long long per_xcd = (nblocks + 7) / 8;
+    const long long grid = per_xcd * 8;
+    if (grid > 0x7fffffffll) return hipErrorInvalidValue;
+    // nontemporal row loads would evict the row before the partner wave reads
+    // it.  OFDM_MRC4K_SYNC=0/1 (default 1): per-row workgroup barrier.
+    const char *e = getenv("OFDM_MRC4K_SYNC");
+    if (e && e[0] == '0')
+        hipLaunchKernelGGL((k_mrc_td4096<false, false>), dim3((unsigned)grid), dim3(64 * MRC_WAVES),
+                           lds_bytes(MRC_WAVES), s, iq, S, R, prefix, Hc, P, out, nq, nblocks, per_xcd,
+                           mode);
+    else
+        hipLaunchKernelGGL((k_mrc_td4096<false, true>), dim3((unsigned)grid), dim3(64 * MRC_WAVES),
+                           lds_bytes(MRC_WAVES), s, iq, S, R, prefix, Hc, P, out, nq, nblocks, per_xcd,
+                           mode);
+    return hipGetLastError();
+}
+
+}  // namespace ofdm

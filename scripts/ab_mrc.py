@@ -12,7 +12,9 @@ import ofdm_lsmrc as ofdm
 F = int(sys.argv[1]) if len(sys.argv) > 1 else 1250
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
 variants = sys.argv[3:] or ["default"]
-S, R, C = 101, 64, 1024
+S = 101
+R = int(os.environ.get('AB_R', 64))
+C = int(os.environ.get('AB_C', 1024))
 K = C - 1
 Q = F * (S - 1)
 dev = torch.device("cuda")

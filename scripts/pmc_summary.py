@@ -1,6 +1,6 @@
 """Summarise a scripts/gpu_profile.sh run into profiles/.
 
-usage: python scripts/pmc_summary.py gpurun_out/prof_<tag> <tag>
+usage: python scripts/pmc_summary.py gpurun_out/prof_<tag> <tag> [notraffic]
 
 Writes
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (copied)
@@ -23,15 +23,14 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-MRC = "k_mrc_td1024"
-LS = "k_ls_td1024"
+MRC = "k_mrc_td"
+LS = "k_ls_td"
 
 
 def short(name):
-    n = name.split("(")[0]
-    for p in ("void ", "ofdm::td1024::", "ofdm::"):
-        n = n.replace(p, "")
-    return n
+    n = name.split("(")[0].replace("void ", "")
+    base, sep, targs = n.partition("<")
+    return base.split("::")[-1] + sep + targs
 
 
 def pmc(path, counter):
@@ -82,7 +81,10 @@ def main():
            "ls_avg_ns_rocprof": float(ls_stat[0]["AverageNs"]) if ls_stat else None,
            "correction": "2*FETCH_SIZE + WRITE_SIZE (KiB->B); MI355X_MICROARCH.md HBM section",
            "source": f"profiles/{tag}_pmc.csv"}
-    with open(os.path.join(prof, "pmc_traffic.json"), "w") as fp:
+    if "notraffic" not in sys.argv[3:]:  # the default-config summary bench.py reads
+        with open(os.path.join(prof, "pmc_traffic.json"), "w") as fp:
+            json.dump(out, fp, indent=1)
+    with open(os.path.join(prof, f"{tag}_traffic.json"), "w") as fp:
         json.dump(out, fp, indent=1)
 
     md = [f"# Profile {tag}", "",

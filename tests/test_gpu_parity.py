@@ -114,6 +114,8 @@ CONFIGS = [
     (3, 4, 5, 1024, 7),
     (2, 3, 64, 2048, 0),
     (1, 2, 32, 4096, 0),
+    (2, 3, 8, 4096, 5),
+    (3, 4, 3, 2048, 9),
     (3, 6, 4, 256, 16),
     (2, 3, 2, 4, 1),
 ]
@@ -147,7 +149,7 @@ def test_empty_batch_is_noop(ofdm, dev):
 
 # ------------------------------------------ antenna split (partial MRC path)
 
-@pytest.mark.parametrize("C,prefix", [(1024, 0), (1024, 16), (2048, 0), (2048, 12), (256, 0)])
+@pytest.mark.parametrize("C,prefix", [(1024, 0), (1024, 16), (2048, 0), (2048, 12), (4096, 0), (4096, 3), (256, 0)])
 def test_antenna_split_matches_full(ofdm, dev, C, prefix):
     """Two antenna shards: partial |H|^2 and partial numerators summed, then
     finalised == the single-GPU result on all antennas."""
@@ -181,7 +183,8 @@ def test_antenna_split_matches_full(ofdm, dev, C, prefix):
 
 @pytest.mark.parametrize("F,S,R,C", [(100, 101, 16, 1024),   # cfg2: 10k-symbol batch
                                      (40, 101, 64, 1024),    # cfg4 shape per GPU (slice)
-                                     (20, 51, 64, 2048)])    # cfg3 shape (slice)
+                                     (20, 51, 64, 2048),     # cfg3 shape (slice)
+                                     (10, 51, 32, 4096)])    # cfg5 per-GPU antenna slice
 def test_full_size_properties(ofdm, dev, F, S, R, C):
     """At BASELINE shapes the oracle is too slow; check (1) zero QPSK decision
     errors at high SNR, (2) invariance of MRC to a common IQ scale (H scales
