@@ -396,6 +396,34 @@ k_mrc_td1024_hlds(const float2 *__restrict__ iq, int S, int R, int prefix,
     if (!store) return;
     const int b0 = lane_bin0(t);
     float2 *o = out + q * K;
+    if ((mode & 4) == 0) {
+        // Stage the K outputs in this wave's transpose image (free after the
+        // last row; its padding tails still hold other waves' Hc words, so
+        // index it as [16][TP]) at their final positions, then store them as
+        // 16 contiguous 512-B wave stores instead of 4 scattered 128-B runs
+        // per instruction.
+        const float *Pf = P + f * C + b0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int b = b0 + 16 * k;
+            if (b == 0) continue;
+            float2 v = acc[k];
+            int j = b - 1;
+            if ((mode & 1) == 0) {
+                const float pv = Pf[16 * k];
+                v = float2{acc[k].x / pv, acc[k].y / pv};
+                j = out_pos(b - 1, K);
+            }
+            T[(j >> 6) * hlds::TP + (j & 63)] = v;
+        }
+        wave_lds_sync();
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            const int j = t + 64 * m;
+            if (j < K) o[j] = T[m * hlds::TP + t];
+        }
+        return;
+    }
     if ((mode & 1) == 0) {
         const float *Pf = P + f * C + b0;
 #pragma unroll
@@ -468,6 +496,7 @@ hipError_t launch_mrc_td1024(const float2 *iq, long long nframes, int S, int R, 
     const int persist = knob("OFDM_MRC_PERSIST", 0), dbg = knob("OFDM_MRC_DEBUG", 0);
     const int sync = knob("OFDM_MRC_SYNC", 0), hlds_on = knob("OFDM_MRC_HLDS", 1);
     if (knob("OFDM_MRC_NTSTORE", 0)) mode |= 2;  // bit 1: nontemporal output stores
+    if (!knob("OFDM_MRC_OSTAGE", 1)) mode |= 4;  // bit 2: HLDS stores outputs without LDS staging
     const long long nblocks = (nq + W - 1) / W;
     const long long per_xcd = (nblocks + 7) / 8;
     long long grid = per_xcd * 8;

@@ -11,6 +11,7 @@
 //  mode 6: as 3 plus 8 KB of stores per wave at the end (pitch 1023 float2)
 //  mode 7: pitch 1024 (line aligned); 8: pitch 1024 with dwordx4; 9: mode 6 with nt stores
 //  mode 10: mode 0 (persistent) with the stores; 11: mode 6 into a 512 KB (L2-resident) region
+//  mode 12: mode 3 + one contiguous 64 KB float4 burst per workgroup after a barrier
 #include <hip/hip_runtime.h>
 #include <cstdio>
 typedef unsigned long long u64;
@@ -64,7 +65,13 @@ __global__ void __launch_bounds__(512) rd(const u64 *__restrict__ p, long long n
             }
         }
         if (MODE != 5 && acc == 1234.5f) lds[threadIdx.x] = acc;
-        if (MODE >= 6 && q < nsym) {  // 8 KB of output per wave, like the MRC epilogue
+        if (MODE == 12) {  // the workgroup's 8 x 8184 B written as one contiguous burst of float4
+            __syncthreads();
+            const long long base = (long long)lb * 8 * 1023 * 8 / 16;  // float4 index
+            float4 *o4 = reinterpret_cast<float4 *>(out) + 16 + base;
+            for (int i = threadIdx.x; i < 8 * 1023 / 2; i += 512) o4[i] = float4{acc, (float)i, acc, 1.f};
+        }
+        if (MODE >= 6 && MODE != 12 && q < nsym) {  // 8 KB of output per wave, like the MRC epilogue
             const int pitch = (MODE == 7 || MODE == 8) ? 1024 : 1023;
             float2 *o = reinterpret_cast<float2 *>(out) + 16 + (MODE == 11 ? (q & 63) : q) * pitch;
             if (MODE == 8) {
@@ -96,7 +103,7 @@ double run(const u64 *p, long long nsym, float *out, int blocks) {
     hipEvent_t a, b;
     hipEventCreate(&a); hipEventCreate(&b);
     size_t lds = 0;
-    if (MODE == 11 || (MODE >= 3 && MODE < 10)) { blocks = (int)(nsym / 8); lds = MODE == 5 ? 0 : 80768; }
+    if (MODE >= 11 || (MODE >= 3 && MODE < 10)) { blocks = (int)(nsym / 8); lds = MODE == 5 ? 0 : 80768; }
     rd<MODE><<<blocks, 512, lds>>>(p, nsym, out);
     hipEventRecord(a);
     for (int i = 0; i < 3; ++i) rd<MODE><<<blocks, 512, lds>>>(p, nsym, out);
@@ -130,7 +137,8 @@ int main() {
         printf("%s +stores: pitch1023 %5.0f  pitch1024 %5.0f  pitch1024 x4 %5.0f  pitch1023 nt %5.0f GB/s\n",
                fill ? "random" : "zeros ", run<6>(p, nsym, out, 0), run<7>(p, nsym, out, 0), run<8>(p, nsym, out, 0),
                run<9>(p, nsym, out, 0));
-        printf("%s persistent 1024 blocks +stores %5.0f   one-shot stores into 512 KB %5.0f GB/s\n",
-               fill ? "random" : "zeros ", run<10>(p, nsym, out, 1024), run<11>(p, nsym, out, 0));
+        printf("%s persistent 1024 blocks +stores %5.0f   one-shot stores into 512 KB %5.0f   64 KB block burst %5.0f GB/s\n",
+               fill ? "random" : "zeros ", run<10>(p, nsym, out, 1024), run<11>(p, nsym, out, 0),
+               run<12>(p, nsym, out, 0));
     }
 }
