@@ -255,33 +255,35 @@ __device__ __forceinline__ void mrc_body(const float2 *__restrict__ iq, int S, i
 // read with per-lane affine addresses and no bank conflicts.
 // ---------------------------------------------------------------------------
 
-// Workgroup barrier that orders LDS only: unlike __syncthreads() it does not
-// make the compiler drain outstanding global loads (vmcnt), so a prefetched
-// row stays in flight across it.
-__device__ __forceinline__ void lds_barrier() {
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-}
 
 // One antenna row of the PF loop: a[] holds this row on entry and the next
 // row (`next`, when PREF) on exit.
-template <bool NT, bool PREF>
+template <bool NT, bool PREF, int PK>
 __device__ __forceinline__ void hlds_row_pf(const float2 *next, const float4 *hrow, int t, float2 (&a)[16],
                                             float2 *T, const float2 *tw1, const float2 *tw2,
                                             const float4 *lo, const float4 *hi, float4 *mine,
                                             float2 (&acc)[16]) {
     using namespace hlds;
     float2 x[16];
-    row_fft_a(a, t, T, tw1);
+    row_fft_a<PK>(a, t, T, tw1);
     const float4 hreg = hrow[threadIdx.x];
     __builtin_amdgcn_sched_barrier(0);
     if (PREF) row_load<NT>(next, t, a);
-    row_fft_b(t, T, tw2, x);
+    row_fft_b<PK>(t, T, tw2, x);
     lds_barrier();  // every wave is done with the previous Hc row
     *mine = hreg;
     lds_barrier();
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         const float4 v = i < 4 ? lo[i * 64] : hi[(i - 4) * TS];  // 2 images = TS float4s
+        if constexpr (PK & 4) {
+            pk::v2f a0 = pk::V(acc[2 * i]), a1 = pk::V(acc[2 * i + 1]);
+            pk::mac(a0, pk::V(x[2 * i]), (pk::v2f){v.x, v.y});
+            pk::mac(a1, pk::V(x[2 * i + 1]), (pk::v2f){v.z, v.w});
+            acc[2 * i] = pk::F(a0);
+            acc[2 * i + 1] = pk::F(a1);
+            continue;
+        }
         acc[2 * i].x = acc[2 * i].x + (x[2 * i].x * v.x - x[2 * i].y * v.y);
         acc[2 * i].y = acc[2 * i].y + (x[2 * i].x * v.y + x[2 * i].y * v.x);
         acc[2 * i + 1].x = acc[2 * i + 1].x + (x[2 * i + 1].x * v.z - x[2 * i + 1].y * v.w);
@@ -296,7 +298,7 @@ __device__ __forceinline__ void hlds_row_pf(const float2 *next, const float4 *hr
 // FFT half has written a[] to the transpose image, so it is in flight during
 // the second FFT half, the Hc exchange and the MAC (no extra registers: a[]
 // is dead there).  The Hc prefetch is issued first: vmcnt retires in order.
-template <bool NT, bool SHARED, bool PF>
+template <bool NT, bool SHARED, bool PF, int PK = 0>
 __device__ __forceinline__ void hlds_rows(const float2 *sym, int Cp, int R, const float4 *Hf, int t,
                                           float2 *T, const float2 *tw1, const float2 *tw2,
                                           float2 *T0, float4 *hfree, float2 (&acc)[16]) {
@@ -312,9 +314,9 @@ __device__ __forceinline__ void hlds_rows(const float2 *sym, int Cp, int R, cons
         // the last row is peeled so that the prefetch is unconditional: the
         // wait for the Hc word before the exchange is then vmcnt(16), not 0
         for (int r = 0; r + 1 < R; ++r)
-            hlds_row_pf<NT, true>(sym + (long long)(r + 1) * Cp, Hf + (long long)r * (C / 2), t, a, T,
-                                  tw1, tw2, lo, hi, mine, acc);
-        hlds_row_pf<NT, false>(sym, Hf + (long long)(R - 1) * (C / 2), t, a, T, tw1, tw2, lo, hi, mine,
+            hlds_row_pf<NT, true, PK>(sym + (long long)(r + 1) * Cp, Hf + (long long)r * (C / 2), t, a, T,
+                                      tw1, tw2, lo, hi, mine, acc);
+        hlds_row_pf<NT, false, PK>(sym, Hf + (long long)(R - 1) * (C / 2), t, a, T, tw1, tw2, lo, hi, mine,
                                acc);
         return;
     }
@@ -351,7 +353,7 @@ __device__ __forceinline__ void hlds_rows(const float2 *sym, int Cp, int R, cons
     }
 }
 
-template <bool NT, bool PF>
+template <bool NT, bool PF, int PK>
 __global__ void __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 4)))
 k_mrc_td1024_hlds(const float2 *__restrict__ iq, int S, int R, int prefix,
                   const float2 *__restrict__ Hc, const float *__restrict__ P,
@@ -390,7 +392,7 @@ k_mrc_td1024_hlds(const float2 *__restrict__ iq, int S, int R, int prefix,
 
     float2 acc[16];
     if (shared)
-        hlds_rows<NT, true, PF>(sym, Cp, R, Hf0, t, T, tw1, tw2, T0, hfree, acc);
+        hlds_rows<NT, true, PF, PK>(sym, Cp, R, Hf0, t, T, tw1, tw2, T0, hfree, acc);
     else
         hlds_rows<NT, false, false>(sym, Cp, R, Hf, t, T, tw1, tw2, T0, hfree, acc);
     if (!store) return;
@@ -510,13 +512,22 @@ hipError_t launch_mrc_td1024(const float2 *iq, long long nframes, int S, int R, 
     if (grid > 0x7fffffffll) return hipErrorInvalidValue;
     if (W == 8 && hlds_on && !persist && !sync && !dbg) {
         const int pf = knob("OFDM_MRC_PF", 1);  // next-row prefetch into the dead a[]
-#define OFDM_HLDS_LAUNCH(NTV, PFV)                                                                  \
-    hipLaunchKernelGGL((k_mrc_td1024_hlds<NTV, PFV>), dim3((unsigned)grid), dim3(512), hlds::LDS_BYTES, \
-                       s, iq, S, R, prefix, Hc, P, out, nq, nblocks, per_xcd, mode)
-        if (nt && pf) OFDM_HLDS_LAUNCH(true, true);
-        else if (nt) OFDM_HLDS_LAUNCH(true, false);
-        else if (pf) OFDM_HLDS_LAUNCH(false, true);
-        else OFDM_HLDS_LAUNCH(false, false);
+        // packed-f32 FFT halves / MAC (pk.hpp): bit 0 first FFT half, bit 1
+        // second half, bit 2 MAC
+        const int pkm = knob("OFDM_PK", 0);  // measured: no gain at C = 1024 (memory-bound), spills with PF
+#define OFDM_HLDS_LAUNCH(NTV, PFV, PKV)                                                             \
+    hipLaunchKernelGGL((k_mrc_td1024_hlds<NTV, PFV, PKV>), dim3((unsigned)grid), dim3(512),         \
+                       hlds::LDS_BYTES, s, iq, S, R, prefix, Hc, P, out, nq, nblocks, per_xcd, mode)
+        if (nt && pf) {
+            if (pkm == 7) OFDM_HLDS_LAUNCH(true, true, 7);
+            else if (pkm == 3) OFDM_HLDS_LAUNCH(true, true, 3);
+            else OFDM_HLDS_LAUNCH(true, true, 0);
+        } else if (nt) {
+            if (pkm == 7) OFDM_HLDS_LAUNCH(true, false, 7);
+            else if (pkm == 3) OFDM_HLDS_LAUNCH(true, false, 3);
+            else OFDM_HLDS_LAUNCH(true, false, 0);
+        } else if (pf) OFDM_HLDS_LAUNCH(false, true, 0);
+        else OFDM_HLDS_LAUNCH(false, false, 0);
 #undef OFDM_HLDS_LAUNCH
         return hipGetLastError();
     }

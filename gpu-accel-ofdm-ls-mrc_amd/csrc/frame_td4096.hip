@@ -12,8 +12,19 @@
 // every row twice: profiles/, PMC ratio 2.02) -- no LDS exchange needed.
 // Lane (q, a) of wave e owns bins 4 b + e and 4 b + 2 + e, b = b0(t) + 16 k.
 //
-// Hc "lane order" for C = 4096: per (frame, antenna) 2048 float4; float4
-// e*1024 + k*64 + t = (Hc[4 b + e], Hc[4 b + 2 + e]).  P bin-indexed [F][C].
+// Hc "lane order" for C = 4096: per (frame, antenna) 4096 float2 in planes
+// [e][h][k][t]: float2 e*2048 + h*1024 + k*64 + t = Hc[4 b + 2 h + e] with
+// b = b0(t) + 16 k -- each plane one coalesced 512-B wave load per k.
+// P bin-indexed [F][C].
+//
+// k_mrc_td4096x (default) instead reads every row ONCE per pair: radix-4
+// decimation in frequency, n = n0 + 1024 n1, z_c[n0] = sum_n1 x[n0 + 1024 n1]
+// (-i)^(c n1) W4096^(c n0), X[4 k + c] = FFT1024(z_c)[k].  Wave e loads
+// quarters e and e + 2 and forms s = x_e + x_(e+2), d = x_e - x_(e+2); the
+// pair swaps one half through LDS (wave 0 sends d, wave 1 sends s), so wave 0
+// holds a = x0 + x2, c = x1 + x3 -> z0 = a + c, z2 = (a - c) W^(2 n0), and
+// wave 1 holds b = x0 - x2, d = x1 - x3 -> z1 = (b - i d) W^(n0),
+// z3 = (b + i d) W^(3 n0).  Same bin ownership as above.
 #include "launch.hpp"
 #include "wave_fft1024.hpp"
 
@@ -92,7 +103,7 @@ constexpr size_t LS_LDS = lds_bytes(LS_WAVES) + (size_t)C * sizeof(float2);
 
 template <int E>
 __device__ __forceinline__ void ls_rows(const float2 *pilot, int Cp, int R, int j, int t, float2 *T,
-                                        const float2 *lds, const float2 *xs, float4 *Hf, float *pp) {
+                                        const float2 *lds, const float2 *xs, float2 *Hf, float *pp) {
     const int b0 = lane_bin0(t);
     float pe[16], po[16];
 #pragma unroll
@@ -100,7 +111,7 @@ __device__ __forceinline__ void ls_rows(const float2 *pilot, int Cp, int R, int 
     for (int r = j; r < R; r += LS_PAIRS) {
         float2 xe[16], xo[16];
         row_fft4096<E, false>(pilot + (long long)r * Cp, t, T, lds, xe, xo);
-        float4 *hr = Hf + (long long)r * (C / 2) + E * 1024;
+        float2 *hr = Hf + (long long)r * C + E * 2048;
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             const int be = 4 * (b0 + 16 * k) + E;
@@ -110,7 +121,8 @@ __device__ __forceinline__ void ls_rows(const float2 *pilot, int Cp, int R, int 
             const float2 ho = ls_conj(xo[k], xs[be + 2]);
             pe[k] = pe[k] + (he.x * he.x) + (he.y * he.y);  // findDistSqrd order
             po[k] = po[k] + (ho.x * ho.x) + (ho.y * ho.y);
-            hr[k * 64 + t] = float4{he.x, he.y, ho.x, ho.y};
+            hr[k * 64 + t] = he;
+            hr[1024 + k * 64 + t] = ho;
         }
     }
     __syncthreads();  // every wave is done with its transpose image (pp reuses it)
@@ -137,7 +149,7 @@ __global__ void __launch_bounds__(256) k_ls_td4096(const float2 *__restrict__ iq
     const long long f = blockIdx.x;
     const int Cp = C + prefix;
     const float2 *pilot = iq + f * (long long)S * R * Cp + prefix;
-    float4 *Hf = reinterpret_cast<float4 *>(Hc + f * (long long)R * C);
+    float2 *Hf = Hc + f * (long long)R * C;
     float *pp = reinterpret_cast<float *>(lds + TAB);  // [LS_PAIRS][C], reuses T
     if (w & 1)
         ls_rows<1>(pilot, Cp, R, w >> 1, t, T, lds, xs, Hf, pp);
@@ -161,7 +173,7 @@ constexpr int MRC_WAVES = 4;
 constexpr int MRC_SYMS = MRC_WAVES / 2;
 
 template <int E, bool NT, bool SYNC>
-__device__ __forceinline__ void mrc_symbol(const float2 *sym, int Cp, int R, const float4 *Hf,
+__device__ __forceinline__ void mrc_symbol(const float2 *sym, int Cp, int R, const float2 *Hf,
                                            const float *Pf, float2 *o, int mode, int t, float2 *T,
                                            const float2 *lds, bool store) {
     float2 ae[16], ao[16];
@@ -174,11 +186,12 @@ __device__ __forceinline__ void mrc_symbol(const float2 *sym, int Cp, int R, con
         if (SYNC) __syncthreads();
         row_fft4096<E, NT>(sym + (long long)r * Cp, t, T, lds, xe, xo);
         __builtin_amdgcn_sched_barrier(0);
-        const float4 *hr = Hf + (long long)r * (C / 2) + E * 1024;
+        const float2 *hr = Hf + (long long)r * C + E * 2048;
         // matrixMultThenSum (cpuLS.hpp:203-204), antennas in order
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
-            const float4 h = hr[k * 64 + t];
+            const float2 h0 = hr[k * 64 + t], h1 = hr[1024 + k * 64 + t];
+            const float4 h = float4{h0.x, h0.y, h1.x, h1.y};
             ae[k].x = ae[k].x + (xe[k].x * h.x - xe[k].y * h.y);
             ae[k].y = ae[k].y + (xe[k].x * h.y + xe[k].y * h.x);
             ao[k].x = ao[k].x + (xo[k].x * h.z - xo[k].y * h.w);
@@ -233,13 +246,196 @@ k_mrc_td4096(const float2 *__restrict__ iq, int S, int R, int prefix, const floa
     const int s = 1 + (int)(q % nsym);
     const int Cp = C + prefix;
     const float2 *sym = iq + (f * S + s) * (long long)R * Cp + prefix;
-    const float4 *Hf = reinterpret_cast<const float4 *>(Hc + f * (long long)R * C);
+    const float2 *Hf = Hc + f * (long long)R * C;
     const float *Pf = P + f * C;
     float2 *o = out + q * K;
     if (w & 1)
         mrc_symbol<1, NT, SYNC>(sym, Cp, R, Hf, Pf, o, mode, t, T, lds, store);
     else
         mrc_symbol<0, NT, SYNC>(sym, Cp, R, Hf, Pf, o, mode, t, T, lds, store);
+}
+
+// ---------------------------------------------------------------------------
+// MRC, one read per row (k_mrc_td4096x): a workgroup is ONE wave pair = one
+// data symbol, so the two LDS barriers per row involve just the pair.  LDS:
+// the radix-16 twiddle tables + two transpose images (25.6 KiB: 6 groups per
+// CU); the DIF twiddles W4096^(c n0), n0 = t + 64 m, are the lane's
+// W4096^(c t) times the compile-time W64^(c m).  PK: packed-f32 arithmetic
+// (pk.hpp) in the split and both FFT halves.
+// ---------------------------------------------------------------------------
+constexpr int X_TAB = hl::TW1S + hl::TW2S;
+constexpr size_t X_LDS = (size_t)(X_TAB + 2 * hl::TS) * sizeof(float2);
+
+template <int CM, int M>
+__device__ __forceinline__ pk::v2f dif_tw(pk::v2f base) {  // base * W64^(CM * M)
+    if constexpr ((CM * M) % 64 == 0) return base;
+    constexpr float2 w = tw_const<64, CM * M>();
+    return pk::cmul_s_v(base, (pk::v2f){w.x, w.y});
+}
+
+// One antenna row for wave E of the pair.  On entry a/b hold the row's
+// quarters E and E + 2; with PREF the next row's quarters are loaded into
+// them after the first FFT (behind this row's Hc loads: loads retire in
+// order) and stay in flight through the second FFT and MAC.
+template <int E, bool NT, int PK, bool PREF>
+__device__ __forceinline__ void x_row(const float2 *__restrict__ next, const float2 *__restrict__ hr,
+                                      int t, float2 *T, const float2 *Tp, const float2 *tw1,
+                                      const float2 *tw2, pk::v2f wb0, pk::v2f wb1, float2 (&a)[16],
+                                      float2 (&b)[16], float2 (&ae)[16], float2 (&ao)[16]) {
+    using namespace pk;
+    v2f u[16], v[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        u[m] = add(V(a[m]), V(b[m]));  // s
+        v[m] = sub(V(a[m]), V(b[m]));  // d
+    }
+    float2 h[16], h1[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) h[k] = hr[k * 64 + t];  // plane 0: bins 4 b + E
+    // wave 0 sends d and keeps s (= a); wave 1 sends s (= c) and keeps d
+#pragma unroll
+    for (int m = 0; m < 16; ++m) T[hl::swz(m, t)] = F(E ? u[m] : v[m]);
+    td1024::lds_barrier();
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        if (E) u[m] = V(Tp[hl::swz(m, t)]);  // b
+        else v[m] = V(Tp[hl::swz(m, t)]);    // c
+    }
+    td1024::lds_barrier();  // the partner has read T before the FFT reuses it
+    // E = 0: u = a, v = c:  z0 = a + c, z2 = (a - c) W^(2 n0)
+    // E = 1: u = b, v = d:  z1 = (b + (-i) d) W^(n0), z3 = (b - (-i) d) W^(3 n0)
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        v2f p, q;
+        if (E) {
+            p = add_mi(u[m], v[m]);
+            q = sub_mi(u[m], v[m]);
+        } else {
+            p = add(u[m], v[m]);
+            q = sub(u[m], v[m]);
+        }
+        u[m] = p;
+        v[m] = q;
+    }
+#define OFDM_TWM(M)                                                                   \
+    if (E) {                                                                          \
+        u[M] = cmul(u[M], dif_tw<1, M>(wb0));                                         \
+        v[M] = cmul(v[M], dif_tw<3, M>(wb1));                                         \
+    } else {                                                                          \
+        v[M] = cmul(v[M], dif_tw<2, M>(wb0));                                         \
+    }
+    OFDM_TWM(0) OFDM_TWM(1) OFDM_TWM(2) OFDM_TWM(3) OFDM_TWM(4) OFDM_TWM(5) OFDM_TWM(6)
+    OFDM_TWM(7) OFDM_TWM(8) OFDM_TWM(9) OFDM_TWM(10) OFDM_TWM(11) OFDM_TWM(12) OFDM_TWM(13)
+    OFDM_TWM(14) OFDM_TWM(15)
+#undef OFDM_TWM
+    float2 z[16], x[16];
+    // matrixMultThenSum (cpuLS.hpp:203-204), antennas in order, per bin set
+    auto mac = [&](float2 (&acc)[16]) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            if (PK & 4) {
+                v2f a0 = V(acc[k]);
+                pk::mac(a0, V(x[k]), V(h[k]));
+                acc[k] = F(a0);
+            } else {
+                acc[k].x = acc[k].x + (x[k].x * h[k].x - x[k].y * h[k].y);
+                acc[k].y = acc[k].y + (x[k].x * h[k].y + x[k].y * h[k].x);
+            }
+        }
+    };
+#pragma unroll
+    for (int m = 0; m < 16; ++m) z[m] = F(u[m]);
+    hl::row_fft_a<PK>(z, t, T, tw1);
+    hl::row_fft_b<PK>(t, T, tw2, x);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) h1[k] = hr[1024 + k * 64 + t];  // plane 1: bins 4 b + 2 + E
+    mac(ae);
+    __builtin_amdgcn_sched_barrier(0);
+    // next row in flight during the second FFT and the next row's exchange
+    if (PREF) {
+        row_load<NT>(next + 1024 * E, t, a);
+        row_load<NT>(next + 1024 * (E + 2), t, b);
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) h[k] = h1[k];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) z[m] = F(v[m]);
+    hl::row_fft_a<PK>(z, t, T, tw1);
+    hl::row_fft_b<PK>(t, T, tw2, x);
+    mac(ao);
+}
+
+template <int E, bool NT, int PK>
+__device__ __forceinline__ void x_rows(const float2 *sym, int Cp, int R, const float2 *Hf, int t,
+                                       float2 *T, const float2 *Tp, const float2 *tw1,
+                                       const float2 *tw2, pk::v2f wb0, pk::v2f wb1,
+                                       float2 (&ae)[16], float2 (&ao)[16]) {
+    float2 a[16], b[16];
+    row_load<NT>(sym + 1024 * E, t, a);
+    row_load<NT>(sym + 1024 * (E + 2), t, b);
+    for (int r = 0; r + 1 < R; ++r)
+        x_row<E, NT, PK, true>(sym + (long long)(r + 1) * Cp, Hf + (long long)r * C, t, T, Tp, tw1,
+                               tw2, wb0, wb1, a, b, ae, ao);
+    x_row<E, NT, PK, false>(sym, Hf + (long long)(R - 1) * C, t, T, Tp, tw1, tw2, wb0, wb1, a, b,
+                            ae, ao);
+}
+
+template <bool NT, int PK, int WPE>
+__global__ void __attribute__((amdgpu_flat_work_group_size(128, 128), amdgpu_waves_per_eu(WPE, WPE)))
+k_mrc_td4096x(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
+              const float *__restrict__ P, float2 *__restrict__ out, long long nq, long long per_xcd,
+              int mode) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int e = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), t = threadIdx.x & 63;
+    const float2 *tw1 = lds, *tw2 = lds + hl::TW1S;
+    float2 *T = lds + X_TAB + e * hl::TS;
+    const float2 *Tp = lds + X_TAB + (e ^ 1) * hl::TS;
+    const long long pb = blockIdx.x;
+    const long long q = (pb & 7) * per_xcd + (pb >> 3);  // XCD-grouped symbol order
+    if (q >= nq) return;  // both waves of the pair leave together
+    hl::fill(lds, lds + hl::TW1S);
+    __syncthreads();
+
+    const int nsym = S - 1;
+    const long long f = q / nsym;
+    const int s = 1 + (int)(q % nsym);
+    const int Cp = C + prefix;
+    const float2 *sym = iq + (f * S + s) * (long long)R * Cp + prefix;
+    const float2 *Hf = Hc + f * (long long)R * C + e * 2048;
+    // lane bases of the DIF twiddles: wave 0 W4096^(2t); wave 1 W4096^t, W4096^(3t)
+    const pk::v2f wb0 = pk::V(g_tw[(e ? 1 : 2) * t]);
+    const pk::v2f wb1 = pk::V(g_tw[3 * t]);
+
+    float2 ae[16], ao[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) ae[k] = ao[k] = float2{0.f, 0.f};
+    if (e)
+        x_rows<1, NT, PK>(sym, Cp, R, Hf, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
+    else
+        x_rows<0, NT, PK>(sym, Cp, R, Hf, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
+    const int b0 = lane_bin0(t);
+    float2 *o = out + q * K;
+    const float *Pf = P + f * C;
+    if ((mode & 1) == 0) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int be = 4 * (b0 + 16 * k) + e;
+            if (be > 0) {
+                const float pv = Pf[be];
+                o[out_pos(be - 1, K)] = float2{ae[k].x / pv, ae[k].y / pv};
+            }
+            const float pv = Pf[be + 2];
+            o[out_pos(be + 1, K)] = float2{ao[k].x / pv, ao[k].y / pv};
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int be = 4 * (b0 + 16 * k) + e;
+            if (be > 0) o[be - 1] = ae[k];
+            o[be + 1] = ao[k];
+        }
+    }
 }
 
 }  // namespace td4096
@@ -263,6 +459,23 @@ hipError_t launch_mrc_td4096(const float2 *iq, long long nframes, int S, int R, 
     const long long per_xcd = (nblocks + 7) / 8;
     const long long grid = per_xcd * 8;
     if (grid > 0x7fffffffll) return hipErrorInvalidValue;
+    auto knob = [](const char *n, int d) { const char *v = getenv(n); return v ? atoi(v) : d; };
+    // OFDM_MRC4K_X=1 (default): k_mrc_td4096x, one row read per pair;
+    // OFDM_MRC4K_PK=0/7: scalar / packed-f32 (pk.hpp)
+    if (knob("OFDM_MRC4K_X", 1)) {
+        const long long xg = ((nq + 7) / 8) * 8;
+        if (xg > 0x7fffffffll) return hipErrorInvalidValue;
+        const int pkm = knob("OFDM_MRC4K_PK", 7);
+        const bool nt = knob("OFDM_MRC4K_NT", 1);
+#define OFDM_X_LAUNCH(NTV, PKV)                                                                 \
+    hipLaunchKernelGGL((k_mrc_td4096x<NTV, PKV, 2>), dim3((unsigned)xg), dim3(128), X_LDS, s, iq,   \
+                       S, R, prefix, Hc, P, out, nq, xg / 8, mode)
+        if (!nt) OFDM_X_LAUNCH(false, 7);
+        else if (pkm == 0) OFDM_X_LAUNCH(true, 0);
+        else OFDM_X_LAUNCH(true, 7);
+#undef OFDM_X_LAUNCH
+        return hipGetLastError();
+    }
     // nontemporal row loads would evict the row before the partner wave reads
     // it.  OFDM_MRC4K_SYNC=0/1 (default 1): per-row workgroup barrier.
     const char *e = getenv("OFDM_MRC4K_SYNC");

@@ -12,6 +12,7 @@
 // (q, a) finally owns bins b = q + 256 c(a) + 16 k', c(a) = (a >> 1) + 2 (a & 1).
 #pragma once
 #include "common.hpp"
+#include "pk.hpp"
 
 namespace ofdm {
 namespace td1024 {
@@ -32,6 +33,13 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Workgroup barrier that orders LDS only: unlike __syncthreads() it does not
+// make the compiler drain outstanding global loads (vmcnt), so a prefetched
+// row stays in flight across it.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 // Quad-DFT signs (found by exhaustive search, verified in tests): lane a of a
@@ -218,8 +226,21 @@ __device__ __forceinline__ void fill(float2 *tw1, float2 *tw2) {
 // index of (row, col) in a transpose image
 __device__ __forceinline__ int swz(int row, int col) { return row * TP + col; }
 
-// first half: radix-16 over m, twiddles, transpose write
+// first half: radix-16 over m, twiddles, transpose write.  PK: packed-f32
+// butterflies and twiddle multiplies (pk.hpp).
+template <int PK = 0>
 __device__ __forceinline__ void row_fft_a(float2 (&a)[16], int t, float2 *T, const float2 *tw1) {
+    if constexpr (PK & 1) {
+        pk::v2f v[16];
+#pragma unroll
+        for (int m = 0; m < 16; ++m) v[m] = pk::V(a[m]);
+        pk::fft_reg<16>(v);
+#pragma unroll
+        for (int k2 = 1; k2 < 16; ++k2) v[k2] = pk::cmul(v[k2], pk::V(tw1[(k2 - 1) * 64 + t]));
+#pragma unroll
+        for (int k2 = 0; k2 < 16; ++k2) T[swz(k2, t)] = pk::F(v[k2]);
+        return;
+    }
     fft_reg<16, false>(a);
 #pragma unroll
     for (int k2 = 1; k2 < 16; ++k2) a[k2] = cmul(a[k2], tw1[(k2 - 1) * 64 + t]);
@@ -227,17 +248,30 @@ __device__ __forceinline__ void row_fft_a(float2 (&a)[16], int t, float2 *T, con
     for (int k2 = 0; k2 < 16; ++k2) T[swz(k2, t)] = a[k2];
 }
 // second half: transpose read, radix-16, twiddles, quad DFT
+template <int PK = 0>
 __device__ __forceinline__ void row_fft_b(int t, float2 *T, const float2 *tw2, float2 (&x)[16]) {
     wave_lds_sync();
     const int q = t >> 2, qa = t & 3;
 #pragma unroll
     for (int l = 0; l < 16; ++l) x[l] = T[swz(q, qa + 4 * l)];
     wave_lds_sync();
-    fft_reg<16, false>(x);
     const float g = quad_g(qa);
-    x[0] = float2{g * x[0].x, g * x[0].y};
+    if constexpr (PK & 2) {
+        pk::v2f v[16];
 #pragma unroll
-    for (int k = 1; k < 16; ++k) x[k] = cmul(x[k], tw2[k * 4 + qa]);
+        for (int m = 0; m < 16; ++m) v[m] = pk::V(x[m]);
+        pk::fft_reg<16>(v);
+        v[0] = pk::scale(v[0], g);
+#pragma unroll
+        for (int k = 1; k < 16; ++k) v[k] = pk::cmul(v[k], pk::V(tw2[k * 4 + qa]));
+#pragma unroll
+        for (int m = 0; m < 16; ++m) x[m] = pk::F(v[m]);
+    } else {
+        fft_reg<16, false>(x);
+        x[0] = float2{g * x[0].x, g * x[0].y};
+#pragma unroll
+        for (int k = 1; k < 16; ++k) x[k] = cmul(x[k], tw2[k * 4 + qa]);
+    }
     quad_dft(x, qa);
 }
 }  // namespace hlds
