@@ -43,10 +43,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--frames", type=int, default=1250, help="frames per GPU")
+    ap.add_argument("--mode", choices=["frames", "split"], default="frames",
+                    help="frames: frame-sharded receiver (configs[3], the headline); split: "
+                         "antenna-split partial MRC + RCCL (configs[4]), --R antennas per GPU")
+    ap.add_argument("--frames", type=int, default=None, help="frames per GPU (1250; split: 400)")
     ap.add_argument("--S", type=int, default=101)
-    ap.add_argument("--R", type=int, default=64)
-    ap.add_argument("--C", type=int, default=1024)
+    ap.add_argument("--R", type=int, default=None, help="antennas per GPU (64; split: 32)")
+    ap.add_argument("--C", type=int, default=None, help="subcarriers (1024; split: 4096)")
+    ap.add_argument("--chunk", type=int, default=50, help="split: frames per pipelined chunk")
     ap.add_argument("--prefix", type=int, default=0)
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--noise", type=float, default=0.01)
@@ -55,7 +59,12 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="PMC traffic summary (profiles/) for roofline.traffic")
-    return ap.parse_args()
+    args = ap.parse_args()
+    split = args.mode == "split"
+    args.frames = args.frames or (400 if split else 1250)
+    args.R = args.R or (32 if split else 64)
+    args.C = args.C or (4096 if split else 1024)
+    return args
 
 
 def cpu_baseline(args, X, ofdm, torch, dev):
@@ -117,7 +126,12 @@ def main():
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    if world > 1 or args.mode == "split":
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29517")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group("nccl", device_id=dev)
 
     def barrier():
@@ -132,6 +146,9 @@ def main():
     a = np.float32(0.70710678)
     X = torch.from_numpy((rng.choice([-a, a], K) + 1j * rng.choice([-a, a], K))
                          .astype(np.complex64)).to(dev)
+
+    if args.mode == "split":
+        return bench_split(args, X, dev, world, rank, barrier)
 
     t = time.perf_counter()
     iq = ofdm.synth_frames(F, S, R, C, X, prefix=prefix, seed=args.seed, frame0=rank * F,
@@ -220,6 +237,96 @@ def main():
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def bench_split(args, X, dev, world, rank, barrier):
+    """configs[4]: every rank holds all frames of ITS --R antennas (global
+    antennas rank*R ...); step = SplitPipeline.run (partial LS, all_reduce of
+    |H|^2, partial FFT+MRC, reduce_scatter of the numerators over RCCL,
+    finalise of the rank's slice), chunked so the collectives overlap the
+    next chunk's kernels.  value = data symbols demodulated per second (every
+    rank covers the same symbols; the antenna count grows with N)."""
+    import torch
+    import torch.distributed as dist
+    import ofdm_lsmrc as ofdm
+    import antenna_split
+    F, S, R, C, prefix = args.frames, args.S, args.R, args.C, args.prefix
+    K = C - 1
+    Q = F * (S - 1)
+    t = time.perf_counter()
+    iq = ofdm.synth_frames(F, S, R, C, X, prefix=prefix, seed=args.seed, r0=rank * R,
+                           noise_std=args.noise)
+    out = ofdm.c64((F, S - 1, K), dev)
+    pipe = antenna_split.SplitPipeline(F, S, R, C, prefix, dev, chunk_frames=args.chunk)
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] synthesised {iq.numel() * 8 / 1e9:.1f} GB in {time.perf_counter() - t:.1f} s")
+    for _ in range(max(1, args.warmup)):
+        out.zero_()
+        pipe.run(iq, X, out)
+    if world > 1:  # every position written by exactly one rank
+        dist.all_reduce(torch.view_as_real(out))
+    torch.cuda.synchronize()
+    errs = int(ofdm.count_symbol_errors(out, S, seed=args.seed).item()) if rank == 0 else 0
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pipe.run(iq, X, out)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    barrier()
+    if world > 1:
+        mx = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        elapsed = float(mx[0])
+
+    # roofline of the dominant kernel: the partial FFT+MRC over the whole
+    # local batch, HIP events on its stream (outside the timed region)
+    stream = torch.cuda.current_stream()
+    _, ws = ofdm.frame_ls_partial(iq, X, prefix)
+    num = ofdm.c64((F, S - 1, K), dev)
+    reps = 5
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ofdm.frame_mrc_partial(iq, ws, prefix, num=num)
+    e0.record(stream)
+    for _ in range(reps):
+        ofdm.frame_mrc_partial(iq, ws, prefix, num=num)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    mrc_ms = e0.elapsed_time(e1) / reps
+    b_sym = R * C * 8 + K * 8
+    achieved = Q * b_sym / (mrc_ms * 1e-3) / 1e9
+    kern = {1024: "k_mrc_td1024_hlds", 2048: "k_mrc_td2048", 4096: "k_mrc_td4096x"}.get(C, "k_mrc_freq")
+    result = {
+        "metric": "OFDM symbols/s (LS+MRC) at 1024 subcarriers x 64 ant; achieved HBM GB/s vs peak",
+        "value": Q / (elapsed / args.steps),
+        "unit": "symbols/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (device-generated Rayleigh channel, QPSK, sigma=%g)" % args.noise,
+        "config": {"workload": f"OFDM uplink LS+MRC, antenna split: {F} frames x {S} symbols x "
+                               f"{R * world} antennas ({R} per GPU) x {C} subcarriers",
+                   "R_per_gpu": R, "R_total": R * world, "C": C, "S": S, "prefix": prefix,
+                   "frames": F, "data_symbols": Q, "chunk_frames": args.chunk,
+                   "parallelism": f"antenna-split x{world}, all_reduce(|H|^2) + "
+                                  f"reduce_scatter(numerators) over RCCL"},
+        "roofline": {"kernel": f"{kern} partial numerators (FFT+MRC)", "bound": "hbm",
+                     "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                     "bytes_per_launch": Q * b_sym, "avg_launch_ms": mrc_ms},
+        "check": {"qpsk_symbol_errors": errs},
+        "cpu_baseline": None,
+    }
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -80,3 +80,90 @@ def demod_antenna_split(shard, X, prefix=0, group=None, ops=HipOps, gather=False
     if gather:
         dist.all_reduce(torch.view_as_real(out), group=group)
     return out, (e0, count)
+
+
+class SplitPipeline:
+    """Chunked, overlapped antenna-split LS + MRC for a fixed batch shape
+    (bench.py --mode split).
+
+    The frames are cut into chunks of `chunk_frames`; per chunk, on the
+    caller's stream: partial LS -> async all_reduce(P) -> partial MRC ->
+    async reduce_scatter(numerators); the collectives of chunk c run on the
+    RCCL stream while chunk c+1 computes, and chunk c is finalised (divide +
+    rotate of this rank's slice) once both have landed.  Buffers are
+    allocated once and double-buffered, so a step issues no allocation.
+    `ops` as for demod_antenna_split (the kernel calls take the preallocated
+    ws / P / num and the stream as keyword arguments).
+    Each rank writes only its slices of `out` (see demod_antenna_split).
+    """
+
+    def __init__(self, F, S, R_local, C, prefix, device, group=None, chunk_frames=50, ops=HipOps):
+        import torch
+        import torch.distributed as dist
+        self.F, self.S, self.R, self.C, self.prefix = F, S, R_local, C, prefix
+        self.K = C - 1
+        self.group = group
+        self.ops = ops
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.chunk = max(1, min(chunk_frames, F))
+        fc = self.chunk
+        n = fc * (S - 1) * self.K
+        self.per = -(-n // self.world)
+        self.ws = [ofdm_lsmrc.workspace(fc, S, R_local, C, device) if ops is HipOps else None
+                   for _ in range(2)]
+        self.P = [torch.empty((fc, self.K), dtype=torch.float32, device=device) for _ in range(2)]
+        # numerators padded to world * per complex values (padding stays 0)
+        self.num = [torch.zeros(self.per * self.world, dtype=torch.complex64, device=device)
+                    for _ in range(2)]
+        self.mine = [torch.empty(self.per, dtype=torch.complex64, device=device) for _ in range(2)]
+
+    def run(self, shard, X, out, stream=None):
+        """shard: (F, S, R_local, C + prefix) on this rank; out: (F, S-1, K)."""
+        import torch.distributed as dist
+        F, S, K = self.F, self.S, self.K
+        pending = []
+
+        def finalize(c, b, wp, wn):
+            wp.wait()
+            wn.wait()
+            f0 = c * self.chunk
+            fc = min(self.chunk, F - f0)
+            n = fc * (S - 1) * K
+            e0 = min(self.rank * self.per, n)
+            count = max(0, min(self.per, n - e0))
+            if count:
+                self.ops.mrc_finalize(self.mine[b][:count], e0, S - 1, K, self.P[b][:fc],
+                                      out[f0:f0 + fc], stream=stream)
+
+        nchunks = -(-F // self.chunk)
+        for c in range(nchunks):
+            b = c & 1
+            f0 = c * self.chunk
+            fc = min(self.chunk, F - f0)
+            part = shard[f0:f0 + fc]
+            P = self.P[b][:fc]
+            _, self.ws[b] = self.ops.ls_partial(part, X, self.prefix, ws=self.ws[b], P=P, stream=stream)
+            wp = dist.all_reduce(P, group=self.group, async_op=True)
+            n = fc * (S - 1) * K
+            num = self.num[b][:n].view(fc, S - 1, K)
+            self.ops.mrc_partial(part, self.ws[b], self.prefix, num=num, stream=stream)
+            flat = self.num[b] if n == self.per * self.world else self._padded(b, n)
+            wn = dist.reduce_scatter_tensor(torch_real(self.mine[b]), torch_real(flat),
+                                            group=self.group, async_op=True)
+            pending.append((c, b, wp, wn))
+            if len(pending) == 2:
+                finalize(*pending.pop(0))
+        while pending:
+            finalize(*pending.pop(0))
+        return out
+
+    def _padded(self, b, n):
+        # a short last chunk: zero the tail so stale numerators are not summed
+        self.num[b][n:].zero_()
+        return self.num[b]
+
+
+def torch_real(t):
+    import torch
+    return torch.view_as_real(t).reshape(-1)

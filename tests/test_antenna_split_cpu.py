@@ -27,24 +27,31 @@ class NumpyOps:
     ofdm_mrc_finalize (same arguments and results; float64 FFT)."""
 
     @staticmethod
-    def ls_partial(shard, X, prefix):
+    def ls_partial(shard, X, prefix, ws=None, P=None, stream=None):
         import torch
         iq = shard.numpy()[:, 0, :, prefix:].astype(np.complex128)
         Y = np.fft.fft(iq, axis=-1)[..., 1:]
         Hc = np.conj(Y / X.numpy().astype(np.complex128)[None, None, :])
-        P = (np.abs(Hc) ** 2).sum(axis=1)
-        return torch.from_numpy(P.astype(np.float32)), Hc
+        p = (np.abs(Hc) ** 2).sum(axis=1).astype(np.float32)
+        if P is None:
+            P = torch.from_numpy(p)
+        else:
+            P.copy_(torch.from_numpy(p))
+        return P, Hc
 
     @staticmethod
-    def mrc_partial(shard, Hc, prefix):
+    def mrc_partial(shard, Hc, prefix, num=None, stream=None):
         import torch
         iq = shard.numpy()[:, 1:, :, prefix:].astype(np.complex128)
         Y = np.fft.fft(iq, axis=-1)[..., 1:]
-        N = (Y * Hc[:, None]).sum(axis=2)
-        return torch.from_numpy(N.astype(np.complex64))
+        N = torch.from_numpy((Y * Hc[:, None]).sum(axis=2).astype(np.complex64))
+        if num is None:
+            return N
+        num.copy_(N)
+        return num
 
     @staticmethod
-    def mrc_finalize(chunk, e0, nsym, K, P, out):
+    def mrc_finalize(chunk, e0, nsym, K, P, out, stream=None):
         c = chunk.numpy()
         e = e0 + np.arange(c.size)
         f, s, j = e // (nsym * K), (e // K) % nsym, e % K
@@ -60,7 +67,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, tmp, splits, prefix, gather):
+def _worker(rank, world, port, tmp, splits, prefix, gather, chunk=0):
     import torch
     import torch.distributed as dist
     import antenna_split
@@ -72,19 +79,34 @@ def _worker(rank, world, port, tmp, splits, prefix, gather):
         r0, r1 = splits[rank], splits[rank + 1]
         shard = torch.from_numpy(np.ascontiguousarray(z["iq"][:, :, r0:r1]))
         X = torch.from_numpy(z["X"])
-        out, (e0, count) = antenna_split.demod_antenna_split(shard, X, prefix, ops=NumpyOps,
-                                                             gather=gather)
+        if chunk:
+            F, S = shard.shape[:2]
+            K = shard.shape[-1] - prefix - 1
+            pipe = antenna_split.SplitPipeline(F, S, r1 - r0, K + 1, prefix, "cpu",
+                                               chunk_frames=chunk, ops=NumpyOps)
+            out = torch.zeros((F, S - 1, K), dtype=torch.complex64)
+            for _ in range(2):  # buffers reused across steps
+                out.zero_()
+                pipe.run(shard, X, out)
+            if gather:
+                dist.all_reduce(torch.view_as_real(out))
+            e0, count = 0, int((out != 0).sum())
+        else:
+            out, (e0, count) = antenna_split.demod_antenna_split(shard, X, prefix, ops=NumpyOps,
+                                                                 gather=gather)
         np.savez(os.path.join(tmp, f"out{rank}.npz"), out=out.numpy(), e0=e0, count=count)
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,R,F,S,C,prefix,gather", [
-    (2, 8, 2, 4, 64, 0, True),
-    (2, 5, 3, 3, 256, 4, False),    # uneven antenna split 3/2, CP dropped
-    (3, 6, 1, 5, 16, 0, False),     # element count not divisible by world
+@pytest.mark.parametrize("world,R,F,S,C,prefix,gather,chunk", [
+    (2, 8, 2, 4, 64, 0, True, 0),
+    (2, 5, 3, 3, 256, 4, False, 0),    # uneven antenna split 3/2, CP dropped
+    (3, 6, 1, 5, 16, 0, False, 0),     # element count not divisible by world
+    (2, 8, 5, 4, 64, 0, True, 2),      # SplitPipeline: chunks 2+2+1 (short last chunk)
+    (3, 7, 4, 3, 32, 2, False, 3),     # SplitPipeline: uneven split, padded chunks
 ])
-def test_antenna_split_gloo(oracle, world, R, F, S, C, prefix, gather):
+def test_antenna_split_gloo(oracle, world, R, F, S, C, prefix, gather, chunk):
     import torch.multiprocessing as mp
     rng = np.random.default_rng(world * 100 + R)
     K = C - 1
@@ -96,10 +118,12 @@ def test_antenna_split_gloo(oracle, world, R, F, S, C, prefix, gather):
     ref = oracle.frames_demod(iq, X, prefix)
     with tempfile.TemporaryDirectory() as tmp:
         np.savez(os.path.join(tmp, "in.npz"), iq=iq, X=X)
-        mp.spawn(_worker, args=(world, _free_port(), tmp, splits, prefix, gather), nprocs=world)
+        mp.spawn(_worker, args=(world, _free_port(), tmp, splits, prefix, gather, chunk),
+                 nprocs=world)
         res = [np.load(os.path.join(tmp, f"out{r}.npz")) for r in range(world)]
     n = F * (S - 1) * K
-    assert sum(int(r["count"]) for r in res) == n
+    if not (chunk and gather):
+        assert sum(int(r["count"]) for r in res) == n
     assert [int(r["e0"]) for r in res] == sorted(int(r["e0"]) for r in res)
     if gather:
         for r in res:

@@ -41,3 +41,23 @@ def test_antenna_split_rccl_matches_full(ofdm, dev, nccl_group, F, S, R, C, pref
     torch.cuda.synchronize()
     assert (e0, count) == (0, F * (S - 1) * (C - 1))
     parity(out.cpu().numpy(), ref.cpu().numpy())
+
+
+@pytest.mark.parametrize("F,S,R,C,prefix,chunk", [(5, 4, 32, 4096, 0, 2), (3, 6, 16, 1024, 8, 3)])
+def test_split_pipeline_rccl_matches_full(ofdm, dev, nccl_group, F, S, R, C, prefix, chunk):
+    """The chunked, overlapped pipeline bench.py --mode split times."""
+    import torch
+    import antenna_split
+    rng = np.random.default_rng(C + R + 1)
+    a = np.float32(0.70710678)
+    X = torch.from_numpy((rng.choice([-a, a], C - 1) + 1j * rng.choice([-a, a], C - 1))
+                         .astype(np.complex64)).to(dev)
+    iq = ofdm.synth_frames(F, S, R, C, X, prefix=prefix, seed=23, noise_std=0.02)
+    ref = ofdm.frame_demod(iq, X, prefix)
+    pipe = antenna_split.SplitPipeline(F, S, R, C, prefix, dev, group=nccl_group, chunk_frames=chunk)
+    out = ofdm.c64((F, S - 1, C - 1), dev)
+    for _ in range(2):
+        out.zero_()
+        pipe.run(iq, X, out)
+    torch.cuda.synchronize()
+    parity(out.cpu().numpy(), ref.cpu().numpy())
