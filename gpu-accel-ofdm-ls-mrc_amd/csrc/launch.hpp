@@ -35,6 +35,13 @@ hipError_t launch_mrc_freq(const float2 *Y, long long frame_stride, long long sy
                            long long p_fstride, int p_jofs, float2 *out, int mode,
                            hipStream_t s);
 
+// The same combine on the matrix cores (mrc_mfma.hip): bin-layout Hc
+// (hc_ld = C, DC slot zero), bin-indexed P (P[f*p_fstride + b]); C >= 64.
+hipError_t launch_mrc_freq_mfma(const float2 *Y, long long frame_stride, long long sym_stride,
+                                long long nframes, int nsym, int R, int C, const float2 *Hc,
+                                long long hc_fstride, const float *P, long long p_fstride,
+                                float2 *out, int mode, hipStream_t s);
+
 // Finalise antenna-split numerators: elements [e0, e0+count) of the flat
 // [nframes][nsym][K] numerator array (num points at element e0) are divided
 // by P[f][j] and stored rotated into out ([nframes][nsym][K], full array).

@@ -139,6 +139,19 @@ def test_frame_demod_freq_synth_vs_oracle(ofdm, oracle, dev, F, S, R, C):
     parity(out, ref)
 
 
+@pytest.mark.parametrize("F,S,R,C", [(2, 21, 16, 1024), (2, 18, 7, 256), (1, 5, 32, 4096),
+                                     (3, 17, 1, 64)])
+def test_frame_demod_freq_mfma_vs_oracle(ofdm, oracle, dev, monkeypatch, F, S, R, C):
+    """The matrix-core combine (OFDM_MRC_FREQ_MFMA=1, mrc_mfma.hip): partial
+    symbol tiles (S-1 not a multiple of 16), odd antenna counts."""
+    monkeypatch.setenv("OFDM_MRC_FREQ_MFMA", "1")
+    X = to_dev(qpsk_pilots(C - 1), dev)
+    Y = ofdm.synth_frames(F, S, R, C, X, seed=6, noise_std=0.05, freq_domain=True)
+    out = host(ofdm.frame_demod_freq(Y, X))
+    ref = oracle.frames_demod_freq(host(Y), host(X), nthreads=8)
+    parity(out, ref)
+
+
 def test_empty_batch_is_noop(ofdm, dev):
     import torch
     X = to_dev(qpsk_pilots(1023), dev)
