@@ -43,14 +43,18 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--mode", choices=["frames", "split"], default="frames",
+    ap.add_argument("--mode", choices=["frames", "split", "pcie"], default="frames",
                     help="frames: frame-sharded receiver (configs[3], the headline); split: "
-                         "antenna-split partial MRC + RCCL (configs[4]), --R antennas per GPU")
+                         "antenna-split partial MRC + RCCL (configs[4]), --R antennas per GPU; "
+                         "pcie: host-resident frames through ofdm_pipeline (H2D + receiver + "
+                         "D2H overlapped; PCIe-inclusive rate, never the headline)")
+    ap.add_argument("--depth", type=int, default=3, help="pcie: pipeline slots")
     ap.add_argument("--frames", type=int, default=None, help="frames per GPU (1250; split: 400)")
     ap.add_argument("--S", type=int, default=101)
     ap.add_argument("--R", type=int, default=None, help="antennas per GPU (64; split: 32)")
     ap.add_argument("--C", type=int, default=None, help="subcarriers (1024; split: 4096)")
-    ap.add_argument("--chunk", type=int, default=50, help="split: frames per pipelined chunk")
+    ap.add_argument("--chunk", type=int, default=None,
+                    help="frames per pipelined chunk (split: 50, pcie: 4)")
     ap.add_argument("--prefix", type=int, default=0)
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--noise", type=float, default=0.01)
@@ -61,7 +65,8 @@ def parse():
                     help="PMC traffic summary (profiles/) for roofline.traffic")
     args = ap.parse_args()
     split = args.mode == "split"
-    args.frames = args.frames or (400 if split else 1250)
+    args.chunk = args.chunk or (4 if args.mode == "pcie" else 50)
+    args.frames = args.frames or (400 if split else 48 if args.mode == "pcie" else 1250)
     args.R = args.R or (32 if split else 64)
     args.C = args.C or (4096 if split else 1024)
     return args
@@ -149,6 +154,8 @@ def main():
 
     if args.mode == "split":
         return bench_split(args, X, dev, world, rank, barrier)
+    if args.mode == "pcie":
+        return bench_pcie(args, X, dev, world, rank, barrier)
 
     t = time.perf_counter()
     iq = ofdm.synth_frames(F, S, R, C, X, prefix=prefix, seed=args.seed, frame0=rank * F,
@@ -233,6 +240,91 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(args, X, ofdm, torch, dev)
         result["speedup_vs_cpu_baseline"] = result["value"] / result["cpu_baseline"]["value"]
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def bench_pcie(args, X, dev, world, rank, barrier):
+    """PCIe-inclusive receiver: --frames frames in page-locked HOST memory
+    (what the ShMemSymBuff ring or a capture file hands over) streamed through
+    ofdm_pipeline (chunk frames per slot, --depth slots; H2D, fused LS+MRC and
+    D2H of the outputs on three HIP streams).  value = data symbols/s with
+    the PCIe transfers included; pcie.h2d_GBps_copy_only = the same bytes
+    copied with nothing else running (the bound of this mode)."""
+    import torch
+    import torch.distributed as dist
+    import ofdm_lsmrc as ofdm
+    F, S, R, C, prefix = args.frames, args.S, args.R, args.C, args.prefix
+    K = C - 1
+    Q = F * (S - 1)
+    iq_d = ofdm.synth_frames(F, S, R, C, X, prefix=prefix, seed=args.seed, frame0=rank * F,
+                             noise_std=args.noise)
+    iq = torch.empty(iq_d.shape, dtype=iq_d.dtype, pin_memory=True)
+    iq.copy_(iq_d)
+    del iq_d
+    out = torch.empty((F, S - 1, K), dtype=torch.complex64, pin_memory=True)
+    torch.cuda.synchronize()
+    in_bytes = iq.numel() * 8
+    # copy-only bound: the same bytes H2D in chunk-sized copies, nothing else running
+    scratch = torch.empty(args.chunk * S * R * (C + prefix), dtype=torch.complex64, device=dev)
+    flat = iq.view(-1)
+    n_el = scratch.numel()
+    for _ in range(2):  # the second pass is timed
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for lo in range(0, flat.numel(), n_el):
+            hi = min(lo + n_el, flat.numel())
+            scratch[:hi - lo].copy_(flat[lo:hi], non_blocking=True)
+        torch.cuda.synchronize()
+        copy_s = time.perf_counter() - t0
+    del scratch
+    pipe = ofdm.Pipeline(S, R, C, X, prefix, chunk_frames=args.chunk, depth=args.depth)
+    for _ in range(max(1, args.warmup)):
+        pipe.demod(iq, out)
+    pipe.sync()
+    errs = int(ofdm.count_symbol_errors(out.to(dev), S, seed=args.seed, frame0=rank * F).item())
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pipe.demod(iq, out)
+    pipe.sync()
+    elapsed = time.perf_counter() - t0
+    barrier()
+    if world > 1:
+        mx = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        elapsed = float(mx[0])
+    pipe.close()
+    per_step = elapsed / args.steps
+    result = {
+        "metric": "OFDM symbols/s (LS+MRC) at 1024 subcarriers x 64 ant, PCIe-inclusive "
+                  "(host-resident IQ and outputs)",
+        "value": Q * world / per_step,
+        "unit": "symbols/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": per_step * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (device-generated, staged to page-locked host memory)",
+        "config": {"workload": f"ofdm_pipeline: {F} host frames x {S} symbols x {R} antennas x "
+                               f"{C} subcarriers per GPU, {args.chunk} frames/slot, "
+                               f"{args.depth} slots",
+                   "R": R, "C": C, "S": S, "prefix": prefix, "frames_per_gpu": F,
+                   "chunk_frames": args.chunk, "depth": args.depth,
+                   "parallelism": f"frame-sharded x{world}, no collective"},
+        "pcie": {"h2d_GBps_pipeline": in_bytes / per_step / 1e9,
+                 "h2d_GBps_copy_only": in_bytes / copy_s / 1e9,
+                 "d2h_GBps_pipeline": Q * K * 8 / per_step / 1e9,
+                 "frac_of_copy_only": copy_s / per_step},
+        "check": {"qpsk_symbol_errors": errs},
+        "cpu_baseline": None,
+    }
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -146,6 +146,14 @@ int td_staged(const float2 *iq, long long F, int S, int R, int C, int prefix, co
 
 }  // namespace
 
+namespace ofdm {
+// error reporting for the other host-side translation units (pipeline.cpp)
+int set_error(int code, const char *msg) {
+    g_err = msg;
+    return code;
+}
+}  // namespace ofdm
+
 extern "C" {
 
 int ofdm_version(void) { return OFDM_LSMRC_VERSION; }

@@ -8,6 +8,9 @@
 
 namespace ofdm {
 
+// Sets ofdm_last_error() for the calling thread and returns `code`.
+int set_error(int code, const char *msg);
+
 // Generic batched row FFT (Stockham in LDS), in place or out of place.
 // Row i is read from in + i*in_stride + in_off and written to
 // out + i*out_stride + out_off.  C power of two, 4 <= C <= 4096.

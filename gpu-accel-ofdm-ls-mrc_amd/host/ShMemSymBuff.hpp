@@ -126,8 +126,10 @@ class ShMemSymBuff {
 
     ~ShMemSymBuff() {
 #ifdef OFDM_RING_HIP
-        for (int i = 0; i < lenOfBuffer; ++i)
+        for (int i = 0; i < lenOfBuffer; ++i) {
             if (streams_[i]) (void)hipStreamDestroy(streams_[i]);
+            if (events_[i]) (void)hipEventDestroy(events_[i]);
+        }
         if (registered_) (void)hipHostUnregister(buff_);
 #endif
         if (!master_) ofdm_ring::store(&buff_->size, -1);  // tell the writer we left
@@ -239,6 +241,60 @@ class ShMemSymBuff {
         toc(readT, numberOfSymbolsToTest - 1);
         advance_reader(r, /*last=*/true);
     }
+
+    // Bulk, pipelined form of readNextSymbolCUDA (no reference counterpart;
+    // SURVEY.md 8(f) rank 2): the next n symbols (whole slots, cyclic prefix
+    // included) are copied to dY + i * numOfRows * (dimension + prefix) on
+    // stream s as soon as the writer has filled them, without waiting for
+    // earlier copies.  The ring protocol is unchanged: readPtr only moves
+    // past a slot once that slot's copy has completed (so a WithWait writer
+    // never overwrites a slot in flight) and, as in readNextSymbol, only
+    // onto a slot the writer has already filled; the run's final symbol is
+    // released like readLastSymbol when `last` is set.  Returns once every
+    // slot of the run has been copied and released.
+    template <typename T>
+    void readSymbolsCUDA(T *dY, int n, hipStream_t s, bool last = false) {
+        static_assert(sizeof(T) == sizeof(complexF), "8-byte complex samples");
+        if (n <= 0) return;
+        register_ring();
+        if (!events_[0])
+            for (auto &e : events_)
+                if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) fail_copy();
+        const size_t bytes = kSymbolElems * sizeof(T);
+        while (ofdm_ring::load(&buff_->writePtr) == -1) ofdm_ring::relax();
+        int rp = ofdm_ring::load(&buff_->readPtr);  // slot of run index `released`
+        int issued = 0, released = 0;
+        while (released < n) {
+            bool progress = false;
+            // issue every filled slot ahead of the reader (at most lenOfBuffer - 1 in flight)
+            const int w = ofdm_ring::load(&buff_->writePtr);
+            const int filled = (w - rp + lenOfBuffer) % lenOfBuffer;  // slots [rp, w)
+            while (issued < n && issued - released < filled) {
+                const int slot = (rp + issued - released) % lenOfBuffer;
+                if (hipMemcpyAsync(reinterpret_cast<char *>(dY) + (size_t)issued * bytes,
+                                   buff_->symbols[slot].data, bytes, hipMemcpyHostToDevice,
+                                   s) != hipSuccess ||
+                    hipEventRecord(events_[issued % lenOfBuffer], s) != hipSuccess)
+                    fail_copy();
+                ++issued;
+                progress = true;
+            }
+            // release completed copies in order
+            while (released < issued) {
+                const hipError_t q = hipEventQuery(events_[released % lenOfBuffer]);
+                if (q == hipErrorNotReady) break;
+                if (q != hipSuccess) fail_copy();
+                const int p = (rp + 1) % lenOfBuffer;
+                const bool final_ = last && released == n - 1;
+                if (!final_ && ofdm_ring::load(&buff_->writePtr) == p) break;  // stay one behind
+                ofdm_ring::store(&buff_->readPtr, p);
+                rp = p;
+                ++released;
+                progress = true;
+            }
+            if (!progress) ofdm_ring::relax();
+        }
+    }
 #endif
 
     // ---- writer (ShMemSymBuff_gpu.hpp:447-503) ---------------------------
@@ -327,18 +383,25 @@ class ShMemSymBuff {
     template <typename T>
     void copy_to_device(T *dY, int slot, hipStream_t s) {
         static_assert(sizeof(T) == sizeof(complexF), "8-byte complex samples");
-        if (!registered_)  // page-lock the ring once: true async DMA from shm
-            registered_ = hipHostRegister(buff_, sizeof(symbolBuffer), hipHostRegisterDefault) ==
-                          hipSuccess;
+        register_ring();
         const size_t bytes = kSymbolElems * sizeof(T);
         if (hipMemcpyAsync(dY, buff_->symbols[slot].data, bytes, hipMemcpyHostToDevice, s) !=
                 hipSuccess ||
-            hipStreamSynchronize(s) != hipSuccess) {
-            std::fprintf(stderr, "ShMemSymBuff: device copy failed\n");
-            std::exit(EXIT_FAILURE);
-        }
+            hipStreamSynchronize(s) != hipSuccess)
+            fail_copy();
+    }
+    // page-lock the ring once: true async DMA from shm
+    void register_ring() {
+        if (!registered_)
+            registered_ = hipHostRegister(buff_, sizeof(symbolBuffer), hipHostRegisterDefault) ==
+                          hipSuccess;
+    }
+    [[noreturn]] static void fail_copy() {
+        std::fprintf(stderr, "ShMemSymBuff: device copy failed\n");
+        std::exit(EXIT_FAILURE);
     }
     hipStream_t streams_[lenOfBuffer] = {};
+    hipEvent_t events_[lenOfBuffer] = {};
     bool registered_ = false;
 #endif
 

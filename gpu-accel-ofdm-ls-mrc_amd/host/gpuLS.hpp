@@ -54,7 +54,10 @@ class gpuLS {
         ofdm::hcheck(hipGetDevice(&dev), "hipGetDevice");
         ofdm::hcheck(hipGetDeviceProperties(&devProp, dev), "hipGetDeviceProperties");
     }
-    ~gpuLS() { delete buffPtr; }
+    ~gpuLS() {
+        if (pipe_) (void)ofdm_pipeline_destroy(pipe_);
+        delete buffPtr;
+    }
 
     // K pilots from Pilots.dat, rotated; 1 + 1i if missing (gpuLS.cu:53-86)
     void matrix_readX(hipFloatComplex *X, int cols) {
@@ -219,7 +222,48 @@ class gpuLS {
         demodOneFrameCUDA(dY, Y, dX, Hconj, Hsqrd, rows1, cols1);
     }
 
+    // ---- streaming frames (the batched demod entry next to
+    // demodOneFrameCUDA; 8(f) rank 2: line-rate ingest) --------------------
+    // Reads nframes frames of lenOfBuffer symbols from the ring with the
+    // pipelined bulk reader (ShMemSymBuff::readSymbolsCUDA) straight into the
+    // device slots of an ofdm_pipeline: while chunk i streams in over PCIe,
+    // chunk i-1 is demodulated and chunk i-2's outputs stream out.  out (host
+    // or device; page-locked host memory for full overlap) receives
+    // nframes x (lenOfBuffer-1) x (cols1-1) rotated outputs, frames in order.
+    // dX: the pilots as copyPilotToGPU fills them (the first cols1-1 values).
+    // last: the run ends with these frames (readLastSymbol semantics for the
+    // final symbol).
+    void demodFrames(hipFloatComplex *out, int nframes, hipFloatComplex *dX, int rows1, int cols1,
+                     bool last = true, int framesPerChunk = 4, int depth = 3) {
+        const int K = cols1 - 1;
+        if (!pipe_ || pipeChunk_ != framesPerChunk || pipeDepth_ != depth || pipeX_ != dX) {
+            if (pipe_) ofdm::check(ofdm_pipeline_destroy(pipe_), "ofdm_pipeline_destroy");
+            pipe_ = nullptr;
+            ofdm::check(ofdm_pipeline_create(lenOfBuffer, rows1, cols1, prefix, C(dX), framesPerChunk,
+                                             depth, &pipe_),
+                        "ofdm_pipeline_create");
+            pipeChunk_ = framesPerChunk;
+            pipeDepth_ = depth;
+            pipeX_ = dX;
+        }
+        for (int f0 = 0; f0 < nframes; f0 += framesPerChunk) {
+            const int n = nframes - f0 < framesPerChunk ? nframes - f0 : framesPerChunk;
+            ofdm_cf32 *d = nullptr;
+            ofdm_stream_t cs = nullptr;
+            ofdm::check(ofdm_pipeline_acquire(pipe_, &d, &cs), "ofdm_pipeline_acquire");
+            buffPtr->readSymbolsCUDA(d, n * lenOfBuffer, reinterpret_cast<hipStream_t>(cs),
+                                     last && f0 + n == nframes);
+            ofdm::check(ofdm_pipeline_submit(pipe_, n, C(out + (size_t)f0 * (lenOfBuffer - 1) * K)),
+                        "ofdm_pipeline_submit");
+        }
+        ofdm::check(ofdm_pipeline_sync(pipe_), "ofdm_pipeline_sync");
+    }
+
   private:
+    ofdm_pipeline *pipe_ = nullptr;
+    int pipeChunk_ = 0, pipeDepth_ = 0;
+    const hipFloatComplex *pipeX_ = nullptr;
+
     static ofdm_cf32 *C(hipFloatComplex *p) { return reinterpret_cast<ofdm_cf32 *>(p); }
     static const ofdm_cf32 *C(const hipFloatComplex *p) {
         return reinterpret_cast<const ofdm_cf32 *>(p);

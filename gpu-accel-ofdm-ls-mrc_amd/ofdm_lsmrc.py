@@ -50,6 +50,14 @@ _SIGS = {
     "ofdm_synth_frames": (_I, [_P, _LL, _I, _I, _I, _I, _P, _c.c_ulonglong, _LL, _c.c_float,
                                _I, _I, _P]),
     "ofdm_count_symbol_errors": (_I, [_P, _LL, _I, _I, _c.c_ulonglong, _LL, _P, _P]),
+    "ofdm_pipeline_create": (_I, [_I, _I, _I, _I, _P, _I, _I, _c.POINTER(_P)]),
+    "ofdm_pipeline_destroy": (_I, [_P]),
+    "ofdm_pipeline_acquire": (_I, [_P, _c.POINTER(_P), _c.POINTER(_P)]),
+    "ofdm_pipeline_submit": (_I, [_P, _LL, _P]),
+    "ofdm_pipeline_demod": (_I, [_P, _P, _LL, _P]),
+    "ofdm_pipeline_sync": (_I, [_P]),
+    "ofdm_host_register": (_I, [_P, _c.c_size_t]),
+    "ofdm_host_unregister": (_I, [_P]),
 }
 
 _lib = None
@@ -301,6 +309,79 @@ def count_symbol_errors(out, S, seed=1234, frame0=0, stream=None):
     _check(lib().ofdm_count_symbol_errors(_dptr(out), F, S, K + 1, seed, frame0, _dptr(err),
                                           _stream(stream)), "ofdm_count_symbol_errors")
     return err
+
+
+class Pipeline:
+    """Streaming receiver over host-resident frames (ofdm_pipeline_*):
+    `depth` device slots of `chunk_frames` frames, copy-in / compute /
+    copy-out on three HIP streams.  demod() is asynchronous: keep `iq` and
+    `out` alive until sync()."""
+
+    def __init__(self, S, R, C, X, prefix=0, chunk_frames=4, depth=3):
+        self.S, self.R, self.C, self.prefix = S, R, C, prefix
+        Xp = X.data_ptr() if hasattr(X, "data_ptr") else np.ascontiguousarray(
+            X, np.complex64).ctypes.data
+        h = _P()
+        _check(lib().ofdm_pipeline_create(S, R, C, prefix, _P(Xp), chunk_frames, depth,
+                                          _c.byref(h)), "ofdm_pipeline_create")
+        self._h = h
+
+    @staticmethod
+    def _ptr(a):
+        return _P(a.data_ptr() if hasattr(a, "data_ptr") else a.ctypes.data)
+
+    def demod(self, iq, out):
+        """iq: (F, S, R, C+prefix) complex64, out: (F, S-1, K) complex64 --
+        numpy arrays or tensors (host or device), contiguous."""
+        F = iq.shape[0]
+        assert tuple(iq.shape[1:]) == (self.S, self.R, self.C + self.prefix), iq.shape
+        assert tuple(out.shape) == (F, self.S - 1, self.C - 1), out.shape
+        _check(lib().ofdm_pipeline_demod(self._h, self._ptr(iq), F, self._ptr(out)),
+               "ofdm_pipeline_demod")
+        return out
+
+    def acquire(self):
+        d, s = _P(), _P()
+        _check(lib().ofdm_pipeline_acquire(self._h, _c.byref(d), _c.byref(s)),
+               "ofdm_pipeline_acquire")
+        return d.value, s.value
+
+    def submit(self, nframes, out=None):
+        _check(lib().ofdm_pipeline_submit(self._h, nframes,
+                                          None if out is None else self._ptr(out)),
+               "ofdm_pipeline_submit")
+
+    def sync(self):
+        _check(lib().ofdm_pipeline_sync(self._h), "ofdm_pipeline_sync")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            h, self._h = self._h, None
+            _check(lib().ofdm_pipeline_destroy(h), "ofdm_pipeline_destroy")
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def host_register(a):
+    """Page-lock a host numpy array / CPU tensor for asynchronous DMA."""
+    p = a.data_ptr() if hasattr(a, "data_ptr") else a.ctypes.data
+    n = a.numel() * a.element_size() if hasattr(a, "numel") else a.nbytes
+    _check(lib().ofdm_host_register(_P(p), n), "ofdm_host_register")
+
+
+def host_unregister(a):
+    p = a.data_ptr() if hasattr(a, "data_ptr") else a.ctypes.data
+    _check(lib().ofdm_host_unregister(_P(p)), "ofdm_host_unregister")
 
 
 def header_symbols(path=HEADER_PATH):

@@ -172,6 +172,43 @@ int ofdm_frame_mrc_partial(const ofdm_cf32 *d_iq, long long nframes, int S, int 
                            int cp_len, void *d_ws, size_t ws_bytes, ofdm_cf32 *d_num,
                            ofdm_stream_t stream);
 
+/* ---------------------------------------------------- streaming ingest --- */
+
+/* Pipelined receiver for IQ that lives in HOST memory (the ShMemSymBuff ring,
+ * a capture file): SURVEY.md 8(f) rank 2.  `depth` device slots of
+ * `chunk_frames` frames each cycle through three HIP streams -- host->device
+ * copy, compute (ofdm_frame_demod), device->host copy of the outputs -- so
+ * PCIe traffic in both directions overlaps the kernels.  Replaces the
+ * reference's per-symbol copy + sync on a fresh stream
+ * (readNextSymbolCUDA, ShMemSymBuff_gpu.hpp:375-447; createStream 364-368)
+ * and the host staging of demodOneFrame (gpuLS.cu:475-573).
+ *   ofdm_pipeline_create: geometry as ofdm_frame_demod; X = the K rotated
+ *       pilots (host or device pointer, copied).  Device = the current one.
+ *   ofdm_pipeline_acquire: the next slot's device IQ buffer (chunk_frames x S
+ *       x R x (C+cp_len)) and the copy stream; the caller enqueues its own
+ *       host->device copies on that stream (the ring reader does), then
+ *   ofdm_pipeline_submit: demodulates the first nframes frames of that slot
+ *       and copies the nframes x (S-1) x K outputs to `out` (host or device;
+ *       NULL = leave them in the slot) on the output stream.
+ *   ofdm_pipeline_demod: acquire + copy + submit over nframes host frames.
+ *   ofdm_pipeline_sync: waits for everything submitted.
+ * Calls return before the copies finish: `iq` and `out` must stay valid until
+ * ofdm_pipeline_sync.  For copies that overlap, host buffers must be
+ * page-locked (ofdm_host_register); pageable buffers work but serialise. */
+typedef struct ofdm_pipeline ofdm_pipeline;
+int ofdm_pipeline_create(int S, int R, int C, int cp_len, const ofdm_cf32 *X, int chunk_frames,
+                         int depth, ofdm_pipeline **out);
+int ofdm_pipeline_destroy(ofdm_pipeline *p);
+int ofdm_pipeline_acquire(ofdm_pipeline *p, ofdm_cf32 **d_iq, ofdm_stream_t *copy_stream);
+int ofdm_pipeline_submit(ofdm_pipeline *p, long long nframes, ofdm_cf32 *out);
+int ofdm_pipeline_demod(ofdm_pipeline *p, const ofdm_cf32 *iq, long long nframes,
+                        ofdm_cf32 *out);
+int ofdm_pipeline_sync(ofdm_pipeline *p);
+
+/* Page-lock / release a host range for asynchronous DMA (hipHostRegister). */
+int ofdm_host_register(void *p, size_t bytes);
+int ofdm_host_unregister(void *p);
+
 /* --------------------------------------------------- synthetic frames --- */
 
 /* Deterministic synthetic frames for tests and benchmarks:

@@ -73,3 +73,24 @@ def test_workspace_sizes(ofdm):
     b2 = ofdm.workspace_bytes(F, S, 64, 2048)
     assert b2 - (F * 64 * 2048 * 8 + F * 2048 * 4) <= max(256 << 20, S * 64 * 2048 * 8) + 512
     assert ofdm.workspace_bytes(F, S, R, 1000) == 0
+
+
+def test_pipeline_argument_validation_without_device(ofdm):
+    """ofdm_pipeline_* reject bad geometry / null handles before any HIP call."""
+    L = ofdm.lib()
+    P = ctypes.c_void_p
+    X = np.ones(1023, np.complex64)
+    h = P()
+    assert L.ofdm_pipeline_create(101, 64, 1024, 0, None, 4, 3, ctypes.byref(h)) == -1
+    assert L.ofdm_pipeline_create(101, 64, 1024, 0, X.ctypes.data_as(P), 0, 3, ctypes.byref(h)) == -1
+    assert L.ofdm_pipeline_create(101, 64, 1024, 0, X.ctypes.data_as(P), 4, 0, ctypes.byref(h)) == -1
+    assert L.ofdm_pipeline_create(101, 64, 1000, 0, X.ctypes.data_as(P), 4, 3, ctypes.byref(h)) == -3
+    assert L.ofdm_pipeline_create(1, 64, 1024, 0, X.ctypes.data_as(P), 4, 3, ctypes.byref(h)) == -3
+    assert L.ofdm_pipeline_create(101, 64, 1024, 2000, X.ctypes.data_as(P), 4, 3,
+                                  ctypes.byref(h)) == -1
+    assert h.value is None
+    assert L.ofdm_pipeline_submit(None, 1, None) == -1
+    assert L.ofdm_pipeline_demod(None, None, 1, None) == -1
+    assert L.ofdm_pipeline_sync(None) == -1
+    assert L.ofdm_pipeline_destroy(None) == 0
+    assert L.ofdm_host_register(None, 10) == -1
