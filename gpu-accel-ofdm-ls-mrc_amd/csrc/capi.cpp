@@ -417,4 +417,30 @@ int ofdm_count_symbol_errors(const ofdm_cf32 *d_out, long long nframes, int S, i
                      "ofdm_count_symbol_errors");
 }
 
+int ofdm_pn_correlate(const ofdm_cf32 *d_buf, int R, long long N, const ofdm_cf32 *d_pn, int L,
+                      float thres, long long *d_pos, float *d_mag, ofdm_stream_t stream) {
+    if (!d_pos) return fail(OFDM_E_ARG, "ofdm_pn_correlate: null d_pos");
+    if (R < 0 || N < 0 || L < 1) return fail(OFDM_E_ARG, "ofdm_pn_correlate: R >= 0, N >= 0, L >= 1 required");
+    if (R > 0 && N >= L && (!d_buf || !d_pn))
+        return fail(OFDM_E_ARG, "ofdm_pn_correlate: null buffer");
+    return hip_check(ofdm::launch_pn_correlate(F2(d_buf), R, N, F2(d_pn), L, thres, d_pos, d_mag,
+                                               hs(stream)),
+                     "ofdm_pn_correlate");
+}
+
+int ofdm_pn_extract(const ofdm_cf32 *d_buf1, const ofdm_cf32 *d_buf2, int R, long long N, int L,
+                    const long long *d_pos, int C, int cp, int nsym, ofdm_cf32 *d_sym,
+                    ofdm_stream_t stream) {
+    if (R < 1 || L < 1 || C < 1 || cp < 0 || nsym < 0 || N < L)
+        return fail(OFDM_E_ARG, "ofdm_pn_extract: bad geometry");
+    if ((long long)nsym * (C + cp) > N - L)
+        return fail(OFDM_E_ARG, "ofdm_pn_extract: nsym*(C+cp)=%lld exceeds the N-L=%lld samples after the PN",
+                    (long long)nsym * (C + cp), N - L);
+    if (!d_buf1 || !d_buf2 || !d_pos || (nsym > 0 && !d_sym))
+        return fail(OFDM_E_ARG, "ofdm_pn_extract: null pointer");
+    return hip_check(ofdm::launch_pn_extract(F2(d_buf1), F2(d_buf2), R, N, L, d_pos, C, cp, nsym,
+                                             F2(d_sym), hs(stream)),
+                     "ofdm_pn_extract");
+}
+
 }  // extern "C"

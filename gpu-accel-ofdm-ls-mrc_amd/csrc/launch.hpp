@@ -89,4 +89,12 @@ hipError_t launch_count_errors(const float2 *out, long long nframes, int S, int 
                                uint64_t seed, long long frame0, unsigned long long *errors,
                                hipStream_t s);
 
+// PN frame sync (pn_sync.hip): first (channel, lag) whose |correlation| / L
+// reaches thres, as ch * (N-L+1) + lag in *pos (-1: none); mag optional.
+hipError_t launch_pn_correlate(const float2 *buf, int R, long long N, const float2 *pn, int L,
+                               float thres, long long *pos, float *mag, hipStream_t s);
+hipError_t launch_pn_extract(const float2 *buf1, const float2 *buf2, int R, long long N, int L,
+                             const long long *pos, int C, int cp, int nsym, float2 *sym,
+                             hipStream_t s);
+
 }  // namespace ofdm

@@ -58,6 +58,8 @@ _SIGS = {
     "ofdm_pipeline_sync": (_I, [_P]),
     "ofdm_host_register": (_I, [_P, _c.c_size_t]),
     "ofdm_host_unregister": (_I, [_P]),
+    "ofdm_pn_correlate": (_I, [_P, _I, _LL, _P, _I, _c.c_float, _P, _P, _P]),
+    "ofdm_pn_extract": (_I, [_P, _P, _I, _LL, _I, _P, _I, _I, _I, _P, _P]),
 }
 
 _lib = None
@@ -309,6 +311,32 @@ def count_symbol_errors(out, S, seed=1234, frame0=0, stream=None):
     _check(lib().ofdm_count_symbol_errors(_dptr(out), F, S, K + 1, seed, frame0, _dptr(err),
                                           _stream(stream)), "ofdm_count_symbol_errors")
     return err
+
+
+def pn_correlate(buf, pn, thres, mag=False, stream=None):
+    """PN frame sync (rx_and_corr.cpp:332-360): buf (R, N), pn (L,) device
+    complex64 -> (pos, mag): pos = device int64 tensor [ch*(N-L+1) + lag] or
+    [-1]; mag = (R, N-L+1) float32 |corr|/L for every lag if requested."""
+    import torch
+    R, N = buf.shape
+    L = pn.shape[0]
+    pos = torch.empty(1, dtype=torch.int64, device=buf.device)
+    m = torch.empty((R, max(N - L + 1, 0)), dtype=torch.float32, device=buf.device) if mag else None
+    _check(lib().ofdm_pn_correlate(_dptr(buf), R, N, _dptr(pn), L, thres, _dptr(pos),
+                                   _dptr(m) if mag else None, _stream(stream)),
+           "ofdm_pn_correlate")
+    return pos, m
+
+
+def pn_extract(buf1, buf2, L, pos, C, cp, nsym, out=None, stream=None):
+    """Frame after the PN (rx_and_corr.cpp:370-392 + copy_to_shared_mem):
+    -> (nsym, R, C) symbols, cyclic prefix dropped."""
+    R, N = buf1.shape
+    if out is None:
+        out = c64((nsym, R, C), buf1.device)
+    _check(lib().ofdm_pn_extract(_dptr(buf1), _dptr(buf2), R, N, L, _dptr(pos), C, cp, nsym,
+                                 _dptr(out), _stream(stream)), "ofdm_pn_extract")
+    return out
 
 
 class Pipeline:

@@ -209,6 +209,31 @@ int ofdm_pipeline_sync(ofdm_pipeline *p);
 int ofdm_host_register(void *p, size_t bytes);
 int ofdm_host_unregister(void *p);
 
+/* ------------------------------------------------------ PN frame sync --- */
+
+/* Frame synchronisation of the receive driver, on
+ * the device.  ofdm_pn_correlate replaces the sliding correlator of
+ * rx_and_corr.cpp:332-360: for channel ch = 0..R-1 and lag i = 0..N-L in that
+ * order, v = |sum_j pn[j] * buf[ch][i+j]| / L (no conjugate, as the
+ * reference); the first (ch, i) with v >= thres is the hit.  d_buf: R rows of
+ * N samples; d_pn: L samples.  *d_pos (device) = ch * (N-L+1) + i, or -1 if
+ * no lag reaches thres.  d_mag (optional, R x (N-L+1) floats, NULL = not
+ * stored) receives v for every lag (then no lag is skipped).  The index is
+ * bit-exact with the reference: each lag is summed in its f32 order.
+ *
+ * ofdm_pn_extract replaces the copy_buff assembly (rx_and_corr.cpp:370-392)
+ * and copy_to_shared_mem (64-87): with lag = *d_pos mod (N-L+1), each
+ * channel's N-L samples after the PN -- d_buf1[ch][lag+L..N) then
+ * d_buf2[ch][0..lag) -- are cut into nsym symbols of C+cp samples with the
+ * cyclic prefix dropped, d_sym[s][ch][k] = seq[s*(C+cp)+cp+k]: the ring's
+ * symbol layout, ready for ofdm_frame_demod (cp_len 0).  Nothing is written
+ * when *d_pos < 0.  nsym*(C+cp) <= N-L. */
+int ofdm_pn_correlate(const ofdm_cf32 *d_buf, int R, long long N, const ofdm_cf32 *d_pn, int L,
+                      float thres, long long *d_pos, float *d_mag, ofdm_stream_t stream);
+int ofdm_pn_extract(const ofdm_cf32 *d_buf1, const ofdm_cf32 *d_buf2, int R, long long N, int L,
+                    const long long *d_pos, int C, int cp, int nsym, ofdm_cf32 *d_sym,
+                    ofdm_stream_t stream);
+
 /* --------------------------------------------------- synthetic frames --- */
 
 /* Deterministic synthetic frames for tests and benchmarks:

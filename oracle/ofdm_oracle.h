@@ -84,6 +84,28 @@ void oracle_frames_demod_freq(const oracle_cf32 *yf, long long nframes, int S,
 
 int oracle_max_threads(void);
 
+/* ---- PN frame-sync correlator (pn_oracle.c; rx_and_corr.cpp) ----------- */
+
+/* rx_and_corr.cpp:332-360: for channel ch = 0.. and lag i = 0..N-L, in that
+ * order, temp = sum_j pn[j] * buf[ch][i+j] (std::complex<float>, sequential
+ * j), v = std::abs(temp) / (float)L; the first (ch, i) with v >= thres stops
+ * the search.  *pos = ch * (N-L+1) + i, or -1 if no lag reaches thres.  If
+ * mag != NULL every lag of every channel is evaluated (no early exit) and
+ * mag[ch * (N-L+1) + i] = v; *pos is the same. */
+void oracle_pn_correlate(const oracle_cf32 *buf, int R, long long N,
+                         const oracle_cf32 *pn, int L, float thres,
+                         long long *pos, float *mag);
+
+/* Frame extraction after a hit at lag `lag` (rx_and_corr.cpp:370-392, then
+ * copy_to_shared_mem 64-87): per channel the sequence seq = buf1[ch][lag+L ..
+ * N) followed by buf2[ch][0 .. lag) (N-L samples) is cut into nsym symbols of
+ * C+cp samples with the cyclic prefix dropped:
+ *   sym[s][ch][k] = seq[s*(C+cp) + cp + k],  s < nsym, k < C.
+ * Requires nsym*(C+cp) <= N-L. */
+void oracle_pn_extract(const oracle_cf32 *buf1, const oracle_cf32 *buf2, int R,
+                       long long N, int L, long long lag, int C, int cp,
+                       int nsym, oracle_cf32 *sym);
+
 #ifdef __cplusplus
 }
 #endif

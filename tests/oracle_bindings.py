@@ -45,6 +45,27 @@ class Oracle:
         L.oracle_frames_demod_freq.argtypes = [_P, _c.c_longlong, _c.c_int, _c.c_int,
                                                _c.c_int, _P, _P, _c.c_int]
         L.oracle_max_threads.restype = _c.c_int
+        L.oracle_pn_correlate.argtypes = [_P, _c.c_int, _c.c_longlong, _P, _c.c_int, _c.c_float,
+                                          _P, _P]
+        L.oracle_pn_extract.argtypes = [_P, _P, _c.c_int, _c.c_longlong, _c.c_int, _c.c_longlong,
+                                        _c.c_int, _c.c_int, _c.c_int, _P]
+
+    def pn_correlate(self, buf, pn, thres, mag=False):
+        """rx_and_corr.cpp:332-360 -> (pos, mag or None)."""
+        buf, pn = c64(buf), c64(pn)
+        R, N = buf.shape
+        pos = _c.c_longlong(0)
+        m = np.empty((R, max(N - pn.size + 1, 0)), np.float32) if mag else None
+        self.lib.oracle_pn_correlate(_ptr(buf), R, N, _ptr(pn), pn.size, float(thres),
+                                     _c.byref(pos), _ptr(m) if mag else None)
+        return pos.value, m
+
+    def pn_extract(self, buf1, buf2, L, lag, C, cp, nsym):
+        buf1, buf2 = c64(buf1), c64(buf2)
+        R, N = buf1.shape
+        out = np.empty((nsym, R, C), np.complex64)
+        self.lib.oracle_pn_extract(_ptr(buf1), _ptr(buf2), R, N, L, lag, C, cp, nsym, _ptr(out))
+        return out
 
     def pilot_rotate(self, raw):
         raw = c64(raw)
