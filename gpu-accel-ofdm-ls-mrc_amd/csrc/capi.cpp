@@ -443,4 +443,53 @@ int ofdm_pn_extract(const ofdm_cf32 *d_buf1, const ofdm_cf32 *d_buf2, int R, lon
                      "ofdm_pn_extract");
 }
 
+static int zf_geometry(int users, int rows, int K, const char *fn) {
+    if (users < 1 || users > OFDM_ZF_MAX_USERS)
+        return fail(OFDM_E_UNSUPPORTED, "%s: users=%d outside [1, %d]", fn, users, OFDM_ZF_MAX_USERS);
+    if (rows < 1 || K < 0) return fail(OFDM_E_ARG, "%s: rows=%d, K=%d", fn, rows, K);
+    if ((long long)users * rows > OFDM_ZF_MAX_USERS_X_ROWS)
+        return fail(OFDM_E_UNSUPPORTED, "%s: users*rows=%lld > %d", fn, (long long)users * rows,
+                    OFDM_ZF_MAX_USERS_X_ROWS);
+    return OFDM_OK;
+}
+
+int ofdm_zf_precoder(const ofdm_cf32 *d_H, int users, int rows, int K, ofdm_cf32 *d_W, ofdm_cf32 *d_Wt,
+                     ofdm_stream_t stream) {
+    int rc = zf_geometry(users, rows, K, "ofdm_zf_precoder");
+    if (rc) return rc;
+    if (K > 0 && (!d_H || (!d_W && !d_Wt))) return fail(OFDM_E_ARG, "ofdm_zf_precoder: null pointer");
+    return hip_check(ofdm::launch_zf_precoder(F2(d_H), users, rows, K, F2(d_W), F2(d_Wt), hs(stream)),
+                     "ofdm_zf_precoder");
+}
+
+int ofdm_zf_transpose(const ofdm_cf32 *d_W, int users, int rows, int K, ofdm_cf32 *d_Wt,
+                      ofdm_stream_t stream) {
+    int rc = zf_geometry(users, rows, K, "ofdm_zf_transpose");
+    if (rc) return rc;
+    if (K > 0 && (!d_W || !d_Wt || d_W == d_Wt))
+        return fail(OFDM_E_ARG, "ofdm_zf_transpose: null or aliased pointers");
+    return hip_check(ofdm::launch_zf_transpose(F2(d_W), users, rows, K, F2(d_Wt), hs(stream)),
+                     "ofdm_zf_transpose");
+}
+
+int ofdm_zf_apply(const ofdm_cf32 *d_Wt, const ofdm_cf32 *d_X, int users, int rows, int K, long long nsym,
+                  ofdm_cf32 *d_Y, ofdm_stream_t stream) {
+    int rc = zf_geometry(users, rows, K, "ofdm_zf_apply");
+    if (rc) return rc;
+    if (nsym < 0) return fail(OFDM_E_ARG, "ofdm_zf_apply: nsym < 0");
+    if (K > 0 && nsym > 0 && (!d_Wt || !d_X || !d_Y)) return fail(OFDM_E_ARG, "ofdm_zf_apply: null pointer");
+    return hip_check(ofdm::launch_zf_apply(F2(d_Wt), F2(d_X), users, rows, K, nsym, F2(d_Y), hs(stream)),
+                     "ofdm_zf_apply");
+}
+
+int ofdm_zf_detect(const ofdm_cf32 *d_Wt, const ofdm_cf32 *d_Y, int users, int rows, int K, long long nsym,
+                   ofdm_cf32 *d_X, ofdm_stream_t stream) {
+    int rc = zf_geometry(users, rows, K, "ofdm_zf_detect");
+    if (rc) return rc;
+    if (nsym < 0) return fail(OFDM_E_ARG, "ofdm_zf_detect: nsym < 0");
+    if (K > 0 && nsym > 0 && (!d_Wt || !d_X || !d_Y)) return fail(OFDM_E_ARG, "ofdm_zf_detect: null pointer");
+    return hip_check(ofdm::launch_zf_detect(F2(d_Wt), F2(d_Y), users, rows, K, nsym, F2(d_X), hs(stream)),
+                     "ofdm_zf_detect");
+}
+
 }  // extern "C"

@@ -97,4 +97,17 @@ hipError_t launch_pn_extract(const float2 *buf1, const float2 *buf2, int R, long
                              const long long *pos, int C, int cp, int nsym, float2 *sym,
                              hipStream_t s);
 
+// Zero forcing (zf.hip).  Hin [U][R][K]; W [K][U][R] (reference layout, may be
+// null); Wt [U][R][K] (subcarrier-fastest, may be null).  1 <= U <= 32,
+// U*R <= 8192 (checked by capi.cpp).
+size_t zf_precoder_lds_bytes(int U, int R);
+hipError_t launch_zf_precoder(const float2 *Hin, int U, int R, int K, float2 *W, float2 *Wt,
+                              hipStream_t s);
+hipError_t launch_zf_transpose(const float2 *W, int U, int R, int K, float2 *Wt, hipStream_t s);
+// apply: Y[s][r][k] = sum_u W(r,u) X[s][u][k]; detect: X[s][u][k] = sum_r conj(W(r,u)) Y[s][r][k]
+hipError_t launch_zf_apply(const float2 *Wt, const float2 *X, int U, int R, int K, long long nsym,
+                           float2 *Y, hipStream_t s);
+hipError_t launch_zf_detect(const float2 *Wt, const float2 *Y, int U, int R, int K, long long nsym,
+                            float2 *X, hipStream_t s);
+
 }  // namespace ofdm

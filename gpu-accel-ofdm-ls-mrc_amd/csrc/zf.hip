@@ -1,0 +1,323 @@
+// zf.hip -- multi-user zero-forcing on the GPU:
+// the reference's precoder createZeroForcingMatrix (cpuLS.hpp:415-447:
+// rotCube, per-subcarrier cgemm A A^H, cgetrf + cgetri, cgemm A^H G^-1),
+// multiplyWithChannelInv (449-463, per-subcarrier cgemv) and the uplink
+// counterpart, ZF detection with the same matrix.
+//
+// Per subcarrier k the shapes are small (users U <= 32, antennas R,
+// U*R <= 8192): G = A A^H is U x U x R, the inverse U^3, W = A^H G^-1 is
+// R x U x U.  One 1023-subcarrier channel set at U = 16, R = 64 is ~0.3 GFLOP
+// -- a few microseconds of VALU next to ~16 MB of HBM traffic.
+//   k_zf_precoder: one 256-thread workgroup per subcarrier; A (U x R) and the
+//     augmented [G | I] in LDS; Gauss-Jordan with partial pivoting (pivot =
+//     first max of |re| + |im|, LAPACK's icamax in cgetrf).  W is written in
+//     the reference's layout W[k][u][r] (per subcarrier R x U column-major)
+//     and/or the subcarrier-fastest layout Wt[u][r][k] the apply / detect
+//     kernels read with coalesced loads.
+//   k_zf_gemm: the symbol-batched application -- for every subcarrier a small
+//     complex GEMM out_k (M x nsym) = A_k (M x N) . in_k (N x nsym), A_k = W
+//     (apply: M = R, N = U) or W^H (detect: M = U, N = R).  Lanes = 64
+//     consecutive subcarriers (the fastest axis of every operand, so each load
+//     and store is one coalesced 512 B wave access); each wave accumulates an
+//     MT x ST (rows x symbols) register tile, so per n it loads MT + ST values
+//     for MT * ST complex MACs.  At U = 16, R = 64 the work is ~13 flop per HBM
+//     byte, under the FP32 ridge (~20): HBM-bound.  MFMA is not used: the f32
+//     matrix peak of gfx950 equals its f32 vector peak (MI355X_MICROARCH.md),
+//     so v_mfma_f32_16x16x4f32 would only add the complex-to-real expansion.
+//     The W tile of a (subcarrier block, row block) is re-read for every symbol
+//     step; block ids are mapped so that all workgroups of one XCD share the
+//     same few tiles (dispatch is round-robin over the 8 XCDs), keeping those
+//     re-reads in that XCD's 4 MB L2 instead of HBM.
+#include <hip/hip_runtime.h>
+
+#include "launch.hpp"
+
+namespace ofdm {
+namespace zf {
+
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+    return float2{a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x};
+}
+__device__ __forceinline__ float2 cmulc(float2 a, float2 b) {  // conj(a) * b
+    return float2{a.x * b.x + a.y * b.y, a.x * b.y - a.y * b.x};
+}
+__device__ __forceinline__ float cabs1(float2 a) { return fabsf(a.x) + fabsf(a.y); }
+__device__ __forceinline__ float2 crcp(float2 a) {  // 1 / a
+    const float d = a.x * a.x + a.y * a.y;
+    return float2{a.x / d, -a.y / d};
+}
+
+constexpr int MAXU = 32;
+
+__global__ void __launch_bounds__(256) k_zf_precoder(const float2 *__restrict__ Hin, int U, int R, int K,
+                                                     float2 *__restrict__ W, float2 *__restrict__ Wt) {
+    extern __shared__ float2 sm[];
+    float2 *A = sm;          // A(u, r) at A[r*U + u]: X[col] after rotCube (cpuLS.hpp:404-410)
+    float2 *M = sm + U * R;  // [U][2U] augmented [G | I], row-major
+    __shared__ float2 fac[MAXU];
+    __shared__ int piv;
+    const int t = threadIdx.x, k = blockIdx.x, U2 = 2 * U;
+
+    for (int e = t; e < U * R; e += 256) {
+        const int u = e / R, r = e - u * R;
+        A[r * U + u] = Hin[((long long)u * R + r) * K + k];
+    }
+    __syncthreads();
+    // G(a, b) = sum_r A(a, r) conj(A(b, r))   (cgemm NoTrans / ConjTrans, 437)
+    for (int e = t; e < U * U; e += 256) {
+        const int a = e % U, b = e / U;
+        float2 s{0.f, 0.f};
+        for (int r = 0; r < R; ++r) {
+            const float2 x = A[r * U + a], y = A[r * U + b];
+            s.x += x.x * y.x + x.y * y.y;
+            s.y += x.y * y.x - x.x * y.y;
+        }
+        M[a * U2 + b] = s;
+        M[a * U2 + U + b] = float2{a == b ? 1.f : 0.f, 0.f};
+    }
+    __syncthreads();
+    // Gauss-Jordan with partial pivoting: [G | I] -> [I | G^-1]  (cgetrf + cgetri, 438-439)
+    for (int j = 0; j < U; ++j) {
+        if (t == 0) {
+            int p = j;
+            float best = cabs1(M[j * U2 + j]);
+            for (int i = j + 1; i < U; ++i) {
+                const float v = cabs1(M[i * U2 + j]);
+                if (v > best) { best = v; p = i; }
+            }
+            piv = p;
+        }
+        __syncthreads();
+        const int p = piv;
+        if (p != j)
+            for (int c = t; c < U2; c += 256) {
+                const float2 tmp = M[j * U2 + c];
+                M[j * U2 + c] = M[p * U2 + c];
+                M[p * U2 + c] = tmp;
+            }
+        __syncthreads();
+        const float2 inv = crcp(M[j * U2 + j]);
+        for (int i = t; i < U; i += 256) fac[i] = M[i * U2 + j];
+        __syncthreads();  // pivot and column j read before row j is scaled
+        for (int c = t; c < U2; c += 256) M[j * U2 + c] = cmul(M[j * U2 + c], inv);
+        __syncthreads();
+        for (int e = t; e < U * U2; e += 256) {
+            const int i = e / U2, c = e - i * U2;
+            if (i == j) continue;
+            const float2 f = fac[i], m = M[j * U2 + c];
+            M[i * U2 + c] = float2{M[i * U2 + c].x - (f.x * m.x - f.y * m.y),
+                                   M[i * U2 + c].y - (f.x * m.y + f.y * m.x)};
+        }
+        __syncthreads();
+    }
+    // W(r, u) = sum_a conj(A(a, r)) Ginv(a, u)   (cgemm ConjTrans / NoTrans, 440)
+    for (int e = t; e < R * U; e += 256) {
+        const int u = e / R, r = e - u * R;
+        float2 s{0.f, 0.f};
+        for (int a = 0; a < U; ++a) {
+            const float2 c = cmulc(A[r * U + a], M[a * U2 + U + u]);
+            s.x += c.x;
+            s.y += c.y;
+        }
+        if (W) W[(long long)k * R * U + u * R + r] = s;
+        if (Wt) Wt[((long long)u * R + r) * K + k] = s;
+    }
+}
+
+// Reference layout W[k][u][r] -> Wt[u][r][k] through a 64 x 64 LDS tile
+// (k block x (u,r) block); both the global read and write are coalesced.
+__global__ void __launch_bounds__(256) k_zf_transpose(const float2 *__restrict__ W, int UR, int K,
+                                                      float2 *__restrict__ Wt) {
+    __shared__ float2 tile[64][65];
+    const int k0 = blockIdx.x * 64, e0 = blockIdx.y * 64;
+    const int lx = threadIdx.x & 63, ly = threadIdx.x >> 6;
+    for (int i = ly; i < 64; i += 4) {
+        const int k = k0 + i, e = e0 + lx;
+        if (k < K && e < UR) tile[i][lx] = W[(long long)k * UR + e];
+    }
+    __syncthreads();
+    for (int i = ly; i < 64; i += 4) {
+        const int e = e0 + i, k = k0 + lx;
+        if (k < K && e < UR) Wt[(long long)e * K + k] = tile[lx][i];
+    }
+}
+
+// out[s][m][k] = sum_n A_k(m, n) in[s][n][k],
+// A_k(m, n) = Wt[(m*a_m + n*a_n)*K + k] (conjugated if CONJ).
+// Workgroup = 4 waves = MG row groups x (4/MG) symbol groups; it owns the
+// rows [mb*MG*MT, +MG*MT) of a 64-subcarrier block and walks its symbol chunk
+// in steps of (4/MG)*ST symbols.
+// PF: the loads of step n+1 are issued before the MACs of step n (register
+// double buffering), so a wave's memory latency overlaps its own arithmetic.
+template <int MT, int ST, int MG, bool CONJ, bool PF>
+__global__ void __launch_bounds__(256) k_zf_gemm(const float2 *__restrict__ Wt, int a_m, int a_n,
+                                                 const float2 *__restrict__ in, int N, int M, int K,
+                                                 long long nsym, float2 *__restrict__ out, int ntile,
+                                                 int tpx, int nkb, long long chunk_steps) {
+    constexpr int SG = 4 / MG, SBLK = SG * ST;
+    // XCD-aware block mapping: block b runs on XCD b % 8; XCD x owns tiles
+    // x, x+8, x+16, ... and walks all symbol chunks of them.
+    const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
+    const int tile = xcd + 8 * (j % tpx);
+    if (tile >= ntile) return;
+    const long long chunk = j / tpx;
+    const int kb = tile % nkb, mb = tile / nkb;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
+    const int k = kb * 64 + lane;
+    if (k >= K) return;  // no barriers below
+    const int m0 = (mb * MG + (w % MG)) * MT;
+    if (m0 >= M) return;
+    const long long step0 = chunk * chunk_steps;
+    const long long nsteps_total = (nsym + SBLK - 1) / SBLK;
+    const long long step1 = min(step0 + chunk_steps, nsteps_total);
+
+    // one 64-bit base per operand; row / symbol offsets are wave-uniform ints
+    // (clamped to the last valid row / symbol: those lanes compute, never store)
+    const float2 *wb = Wt + (long long)m0 * a_m * K + k;
+    const int amK = a_m * K, anK = a_n * K, NK = N * K, mlast = M - 1 - m0;
+
+    for (long long st = step0; st < step1; ++st) {
+        const long long s0 = st * SBLK + (w / MG) * ST;
+        const int slast = (int)min((long long)ST - 1, nsym - 1 - s0);
+        const float2 *xb = in + s0 * NK + k;
+        float2 acc[MT][ST];
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int jj = 0; jj < ST; ++jj) acc[i][jj] = float2{0.f, 0.f};
+        float2 a[MT], x[ST];
+        auto load = [&](int n, float2 *av, float2 *xv) {
+            const float2 *wn = wb + n * anK, *xn = xb + n * K;
+#pragma unroll
+            for (int i = 0; i < MT; ++i) av[i] = wn[min(i, mlast) * amK];
+#pragma unroll
+            for (int jj = 0; jj < ST; ++jj) xv[jj] = xn[min(jj, slast) * NK];
+        };
+        if (PF) load(0, a, x);
+#pragma unroll 2
+        for (int n = 0; n < N; ++n) {
+            float2 an[MT], xnx[ST];
+            if (PF)
+                load(min(n + 1, N - 1), an, xnx);  // the last one is a redundant reload
+            else
+                load(n, a, x);
+            // complex MAC as 4 FMAs straight into the accumulator
+#pragma unroll
+            for (int i = 0; i < MT; ++i) {
+                const float ar = a[i].x, ai = CONJ ? -a[i].y : a[i].y;
+#pragma unroll
+                for (int jj = 0; jj < ST; ++jj) {
+                    acc[i][jj].x = fmaf(ar, x[jj].x, fmaf(-ai, x[jj].y, acc[i][jj].x));
+                    acc[i][jj].y = fmaf(ar, x[jj].y, fmaf(ai, x[jj].x, acc[i][jj].y));
+                }
+            }
+            if (PF) {
+#pragma unroll
+                for (int i = 0; i < MT; ++i) a[i] = an[i];
+#pragma unroll
+                for (int jj = 0; jj < ST; ++jj) x[jj] = xnx[jj];
+            }
+        }
+#pragma unroll
+        for (int jj = 0; jj < ST; ++jj) {
+            if (s0 + jj >= nsym) break;
+            float2 *o = out + ((s0 + jj) * M) * (long long)K + k;
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+                if (m0 + i < M) o[(long long)(m0 + i) * K] = acc[i][jj];
+        }
+    }
+}
+
+}  // namespace zf
+
+size_t zf_precoder_lds_bytes(int U, int R) {
+    return ((size_t)U * R + (size_t)U * 2 * U) * sizeof(float2);
+}
+
+hipError_t launch_zf_precoder(const float2 *Hin, int U, int R, int K, float2 *W, float2 *Wt,
+                              hipStream_t s) {
+    if (K == 0) return hipSuccess;
+    const size_t lds = zf_precoder_lds_bytes(U, R);
+    if (lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&zf::k_zf_precoder),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(zf::k_zf_precoder, dim3(K), dim3(256), lds, s, Hin, U, R, K, W, Wt);
+    return hipGetLastError();
+}
+
+hipError_t launch_zf_transpose(const float2 *W, int U, int R, int K, float2 *Wt, hipStream_t s) {
+    if (K == 0) return hipSuccess;
+    const int UR = U * R;
+    hipLaunchKernelGGL(zf::k_zf_transpose, dim3((K + 63) / 64, (UR + 63) / 64), dim3(256), 0, s, W, UR,
+                       K, Wt);
+    return hipGetLastError();
+}
+
+namespace {
+
+template <int MT, int ST, int MG, bool CONJ, bool PF>
+hipError_t gemm_launch(const float2 *Wt, int a_m, int a_n, const float2 *in, int N, int M, int K,
+                       long long nsym, float2 *out, hipStream_t s) {
+    constexpr int SBLK = (4 / MG) * ST;
+    const int nkb = (K + 63) / 64, nmb = (M + MG * MT - 1) / (MG * MT);
+    const int ntile = nkb * nmb, tpx = (ntile + 7) / 8;
+    const long long nsteps = (nsym + SBLK - 1) / SBLK;
+    // ~8 workgroups per CU (256 CUs) over all tiles, at least 4 steps per chunk
+    long long nchunk = (2048 + 8LL * tpx - 1) / (8LL * tpx);
+    long long chunk_steps = (nsteps + nchunk - 1) / nchunk;
+    if (chunk_steps < 4) chunk_steps = 4;
+    nchunk = (nsteps + chunk_steps - 1) / chunk_steps;
+    const long long blocks = 8LL * tpx * nchunk;
+    hipLaunchKernelGGL((zf::k_zf_gemm<MT, ST, MG, CONJ, PF>), dim3((unsigned)blocks), dim3(256), 0, s,
+                       Wt, a_m, a_n, in, N, M, K, nsym, out, ntile, tpx, nkb, chunk_steps);
+    return hipGetLastError();
+}
+
+// A/B knobs, read per launch: OFDM_ZF_ST (symbols per register tile, 4 or 8)
+// and OFDM_ZF_PF (0 = no register double buffering).
+int env_int(const char *name, int def) {
+    const char *v = getenv(name);
+    return v && *v ? atoi(v) : def;
+}
+
+template <int MT, int MG, bool CONJ>
+hipError_t gemm_variant(const float2 *Wt, int a_m, int a_n, const float2 *in, int N, int M, int K,
+                        long long nsym, float2 *out, hipStream_t s) {
+    const bool st4 = env_int("OFDM_ZF_ST", 8) == 4, pf = env_int("OFDM_ZF_PF", 1) != 0;
+    if (st4) return pf ? gemm_launch<MT, 4, MG, CONJ, true>(Wt, a_m, a_n, in, N, M, K, nsym, out, s)
+                       : gemm_launch<MT, 4, MG, CONJ, false>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+    return pf ? gemm_launch<MT, 8, MG, CONJ, true>(Wt, a_m, a_n, in, N, M, K, nsym, out, s)
+              : gemm_launch<MT, 8, MG, CONJ, false>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+}
+
+template <bool CONJ>
+hipError_t gemm_dispatch(const float2 *Wt, int a_m, int a_n, const float2 *in, int N, int M, int K,
+                         long long nsym, float2 *out, hipStream_t s) {
+    if (M <= 2) return gemm_variant<2, 1, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+    if (M <= 4) return gemm_variant<4, 1, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+    if (M <= 8) return gemm_variant<8, 1, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+    if (M <= 16) return gemm_variant<8, 2, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+    return gemm_variant<8, 4, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+}
+
+}  // namespace
+
+// Y[s][r][k] = sum_u W(r, u) X[s][u][k];  W(r, u) = Wt[(u*R + r)*K + k]
+hipError_t launch_zf_apply(const float2 *Wt, const float2 *X, int U, int R, int K, long long nsym,
+                           float2 *Y, hipStream_t s) {
+    if (K == 0 || nsym == 0) return hipSuccess;
+    return gemm_dispatch<false>(Wt, 1, R, X, U, R, K, nsym, Y, s);
+}
+
+// X[s][u][k] = sum_r conj(W(r, u)) Y[s][r][k]
+hipError_t launch_zf_detect(const float2 *Wt, const float2 *Y, int U, int R, int K, long long nsym,
+                            float2 *X, hipStream_t s) {
+    if (K == 0 || nsym == 0) return hipSuccess;
+    return gemm_dispatch<true>(Wt, R, 1, Y, R, U, K, nsym, X, s);
+}
+
+}  // namespace ofdm

@@ -17,12 +17,16 @@
 //     becomes NaN (cpuLS.hpp:251-272);
 //   * a missing Pilots.dat fills 0.707 + 0.707i, as cpuLS.hpp:84-90 does;
 //   * the FFT plan is not rebuilt per row and doOneSymbol does not leak.
-// The TX-side helpers (ifftShiftOneRow, addPrefix, rotCube, the zero-forcing
-// precoder, modRefSymbol, modOneSymbol; cpuLS.hpp:119-132, 391-529) are not
-// part of the receiver path and are not provided.
+// The multi-user zero-forcing helpers (rotCube, createZeroForcingMatrix,
+// multiplyWithChannelInv; cpuLS.hpp:400-463) are provided, computed by the
+// library's ZF kernels.  The remaining TX-side
+// helpers (ifftShiftOneRow, addPrefix, modRefSymbol, modOneSymbol;
+// cpuLS.hpp:119-132, 391-398, 466-529) are not part of the receiver path and
+// are not provided.
 #ifndef _CPULS_HPP_
 #define _CPULS_HPP_
 
+#include <algorithm>
 #include <csignal>
 #include <cmath>
 #include <cstdlib>
@@ -198,6 +202,36 @@ inline void doOneSymbol(complexF *Y, complexF *Hconj, complexF *Hsqrd, int rows,
                                        : (std::ofstream::binary | std::ofstream::app));
     outfile.write(reinterpret_cast<const char *>(Yf.data()), (std::streamsize)K * sizeof(complexF));
     outfile.close();
+}
+
+// rotCube (cpuLS.hpp:400-413): X[user][row][col] -> X[col][row][user], in
+// place (a layout permutation, no arithmetic).
+inline void rotCube(complexF *X, int rows, int cols, int users) {
+    std::vector<complexF> t((size_t)rows * cols * users);
+    for (int col = 0; col < cols; col++)
+        for (int row = 0; row < rows; row++)
+            for (int user = 0; user < users; user++)
+                t[((size_t)col * rows + row) * users + user] = X[((size_t)user * rows + row) * cols + col];
+    std::memcpy(X, t.data(), t.size() * sizeof(complexF));
+}
+
+// createZeroForcingMatrix (cpuLS.hpp:415-447): X is the users x rows x K
+// channel cube (K = max(1, cols-1)); H receives, per subcarrier, the rows x
+// users matrix A^H (A A^H)^-1, column-major (H[k*rows*users + u*rows + r]).
+// As in the reference, X is left rotated (rotCube) on return.  The
+// reference's debug print of the first six rotated values (431-434) is
+// omitted.
+inline void createZeroForcingMatrix(complexF *H, complexF *X, int rows, int cols, int users) {
+    const int K = std::max(1, cols - 1);
+    ofdm::HostEngine::get().zf_precoder(X, users, rows, K, H);
+    rotCube(X, rows, K, users);
+}
+
+// multiplyWithChannelInv (cpuLS.hpp:449-463): for each subcarrier i < cols-1,
+// HX[r*(cols-1) + i] = sum_u H[i*rows*users + u*rows + r] X[u*(cols-1) + i].
+inline void multiplyWithChannelInv(complexF *HX, complexF *X, complexF *H, int rows, int cols,
+                                   int users) {
+    ofdm::HostEngine::get().zf_apply(H, X, users, rows, cols - 1, HX);
 }
 
 #endif  // _CPULS_HPP_

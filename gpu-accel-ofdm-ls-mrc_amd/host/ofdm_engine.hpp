@@ -150,6 +150,29 @@ class HostEngine {
         down(A, dH, (size_t)K * 8);
     }
 
+    // zero-forcing matrix of a U x R x K channel cube -> W [K][U][R] (host)
+    void zf_precoder(const void *Hin, int U, int R, int K, void *W) {
+        const size_t b = (size_t)U * R * K * 8;
+        auto *dH = a_.get<ofdm_cf32>(b);
+        auto *dW = c_.get<ofdm_cf32>(b);
+        up(dH, Hin, b);
+        check(ofdm_zf_precoder(dH, U, R, K, dW, nullptr, s_), "ofdm_zf_precoder");
+        down(W, dW, b);
+    }
+    // one symbol: Y[r][k] = sum_u W[k][u][r] X[u][k]  (W in the reference layout)
+    void zf_apply(const void *W, const void *X, int U, int R, int K, void *Y) {
+        const size_t bw = (size_t)U * R * K * 8;
+        auto *dW = a_.get<ofdm_cf32>(bw);
+        auto *dWt = c_.get<ofdm_cf32>(bw);
+        auto *dX = b_.get<ofdm_cf32>((size_t)U * K * 8);
+        auto *dY = d_.get<ofdm_cf32>((size_t)R * K * 8);
+        up(dW, W, bw);
+        up(dX, X, (size_t)U * K * 8);
+        check(ofdm_zf_transpose(dW, U, R, K, dWt, s_), "ofdm_zf_transpose");
+        check(ofdm_zf_apply(dWt, dX, U, R, K, 1, dY, s_), "ofdm_zf_apply");
+        down(Y, dY, (size_t)R * K * 8);
+    }
+
   private:
     HostEngine() { hcheck(hipStreamCreate(&s_), "hipStreamCreate"); }
     void up(void *d, const void *h, size_t b) {

@@ -60,6 +60,10 @@ _SIGS = {
     "ofdm_host_unregister": (_I, [_P]),
     "ofdm_pn_correlate": (_I, [_P, _I, _LL, _P, _I, _c.c_float, _P, _P, _P]),
     "ofdm_pn_extract": (_I, [_P, _P, _I, _LL, _I, _P, _I, _I, _I, _P, _P]),
+    "ofdm_zf_precoder": (_I, [_P, _I, _I, _I, _P, _P, _P]),
+    "ofdm_zf_transpose": (_I, [_P, _I, _I, _I, _P, _P]),
+    "ofdm_zf_apply": (_I, [_P, _P, _I, _I, _I, _LL, _P, _P]),
+    "ofdm_zf_detect": (_I, [_P, _P, _I, _I, _I, _LL, _P, _P]),
 }
 
 _lib = None
@@ -336,6 +340,54 @@ def pn_extract(buf1, buf2, L, pos, C, cp, nsym, out=None, stream=None):
         out = c64((nsym, R, C), buf1.device)
     _check(lib().ofdm_pn_extract(_dptr(buf1), _dptr(buf2), R, N, L, _dptr(pos), C, cp, nsym,
                                  _dptr(out), _stream(stream)), "ofdm_pn_extract")
+    return out
+
+
+def _opt_ptr(t, name):
+    return None if t is None else _dptr(t, name)
+
+
+def zf_precoder(H, W=True, Wt=True, stream=None):
+    """createZeroForcingMatrix (cpuLS.hpp:415-447): H (U, R, K) device
+    complex64 -> (W (K, U, R) reference layout or None, Wt (U, R, K) or None)."""
+    U, R, K = H.shape
+    W = c64((K, U, R), H.device) if W is True else (None if W is False else W)
+    Wt = c64((U, R, K), H.device) if Wt is True else (None if Wt is False else Wt)
+    _check(lib().ofdm_zf_precoder(_dptr(H, "H"), U, R, K, _opt_ptr(W, "W"), _opt_ptr(Wt, "Wt"),
+                                  _stream(stream)), "ofdm_zf_precoder")
+    return W, Wt
+
+
+def zf_transpose(W, stream=None):
+    """(K, U, R) reference layout -> (U, R, K)."""
+    K, U, R = W.shape
+    Wt = c64((U, R, K), W.device)
+    _check(lib().ofdm_zf_transpose(_dptr(W, "W"), U, R, K, _dptr(Wt, "Wt"), _stream(stream)),
+           "ofdm_zf_transpose")
+    return Wt
+
+
+def zf_apply(Wt, X, out=None, stream=None):
+    """multiplyWithChannelInv (cpuLS.hpp:449-463) over symbols: X (nsym, U, K) -> (nsym, R, K)."""
+    U, R, K = Wt.shape
+    n = X.shape[0]
+    assert tuple(X.shape) == (n, U, K), X.shape
+    if out is None:
+        out = c64((n, R, K), X.device)
+    _check(lib().ofdm_zf_apply(_dptr(Wt, "Wt"), _dptr(X, "X"), U, R, K, n, _dptr(out, "out"),
+                               _stream(stream)), "ofdm_zf_apply")
+    return out
+
+
+def zf_detect(Wt, Y, out=None, stream=None):
+    """ZF detection with the same matrix: Y (nsym, R, K) -> (nsym, U, K)."""
+    U, R, K = Wt.shape
+    n = Y.shape[0]
+    assert tuple(Y.shape) == (n, R, K), Y.shape
+    if out is None:
+        out = c64((n, U, K), Y.device)
+    _check(lib().ofdm_zf_detect(_dptr(Wt, "Wt"), _dptr(Y, "Y"), U, R, K, n, _dptr(out, "out"),
+                                _stream(stream)), "ofdm_zf_detect")
     return out
 
 

@@ -234,6 +234,42 @@ int ofdm_pn_extract(const ofdm_cf32 *d_buf1, const ofdm_cf32 *d_buf2, int R, lon
                     const long long *d_pos, int C, int cp, int nsym, ofdm_cf32 *d_sym,
                     ofdm_stream_t stream);
 
+/* ------------------------------------------------------ zero forcing --- */
+
+/* Multi-user zero forcing, U users x R antennas per
+ * subcarrier, K subcarriers (the reference passes cols and uses K = cols-1).
+ *
+ * ofdm_zf_precoder replaces createZeroForcingMatrix (cpuLS.hpp:415-447):
+ *   d_H: users x rows x K channel cube, the layout the reference hands to
+ *   rotCube (cpuLS.hpp:400-413, X[user*rows*cols + row*cols + col]); it is
+ *   not modified (the reference rotates it in place).  Per subcarrier k,
+ *   A(u, r) = H[u][r][k], G = A A^H, W = A^H G^-1 (R x U), inverted by
+ *   Gauss-Jordan with partial pivoting in f32 (the reference: cgetrf +
+ *   cgetri; results agree to f32 rounding of a well-conditioned G, not
+ *   bit-for-bit).  Outputs (either may be NULL, not both):
+ *     d_W  [K][U][R]: W(r, u) at d_W[k*R*U + u*R + r] -- the reference's H
+ *          output (cgemm ldc = rows, cpuLS.hpp:440);
+ *     d_Wt [U][R][K]: W(r, u) at d_Wt[(u*R + r)*K + k] -- the layout
+ *          ofdm_zf_apply / ofdm_zf_detect read (subcarrier-fastest).
+ * ofdm_zf_transpose: d_W (reference layout) -> d_Wt.
+ * ofdm_zf_apply replaces multiplyWithChannelInv (cpuLS.hpp:449-463, cgemv
+ *   per subcarrier) for nsym symbols at once: d_Y[s][r][k] = sum_u W(r, u)
+ *   d_X[s][u][k]  (X: nsym x U x K, Y: nsym x R x K).
+ * ofdm_zf_detect (uplink counterpart, no reference function):
+ *   d_X[s][u][k] = sum_r conj(W(r, u)) d_Y[s][r][k] -- W^H = G^-1 A is the
+ *   pseudo-inverse of the R x U uplink channel A^H.
+ * Limits: 1 <= users <= OFDM_ZF_MAX_USERS, users*rows <= OFDM_ZF_MAX_USERS_X_ROWS. */
+#define OFDM_ZF_MAX_USERS 32
+#define OFDM_ZF_MAX_USERS_X_ROWS 8192
+int ofdm_zf_precoder(const ofdm_cf32 *d_H, int users, int rows, int K, ofdm_cf32 *d_W, ofdm_cf32 *d_Wt,
+                     ofdm_stream_t stream);
+int ofdm_zf_transpose(const ofdm_cf32 *d_W, int users, int rows, int K, ofdm_cf32 *d_Wt,
+                      ofdm_stream_t stream);
+int ofdm_zf_apply(const ofdm_cf32 *d_Wt, const ofdm_cf32 *d_X, int users, int rows, int K, long long nsym,
+                  ofdm_cf32 *d_Y, ofdm_stream_t stream);
+int ofdm_zf_detect(const ofdm_cf32 *d_Wt, const ofdm_cf32 *d_Y, int users, int rows, int K, long long nsym,
+                   ofdm_cf32 *d_X, ofdm_stream_t stream);
+
 /* --------------------------------------------------- synthetic frames --- */
 
 /* Deterministic synthetic frames for tests and benchmarks:

@@ -19,7 +19,7 @@ if [ ! -f "$REF/cpuLS.hpp" ]; then
   exit 0
 fi
 mkdir -p "$OUT"
-FUNCS="matrix_readX shiftOneRow matrixMultThenSum findDistSqrd divideOneRow"
+FUNCS="matrix_readX shiftOneRow matrixMultThenSum findDistSqrd divideOneRow rotCube"
 {
   for f in $FUNCS; do
     # from the definition line to the first closing brace in column 0

@@ -106,6 +106,29 @@ void oracle_pn_extract(const oracle_cf32 *buf1, const oracle_cf32 *buf2, int R,
                        long long N, int L, long long lag, int C, int cp,
                        int nsym, oracle_cf32 *sym);
 
+/* ---- zero-forcing precoder (zf_oracle.c; cpuLS.hpp:401-466) ------------ */
+
+/* createZeroForcingMatrix (cpuLS.hpp:415-449) for K = cols-1 subcarriers:
+ * Hin: users x rows x K channel cube (the layout before rotCube, 401-413; not
+ * modified here).  Per subcarrier A[u][r] = Hin[u][r][k], G = A A^H
+ * (cblas_cgemm NoTrans/ConjTrans), G^-1 by LU with partial pivoting (cgetrf:
+ * unblocked, pivot = max |re|+|im|) and the LU inverse (cgetri), then
+ * W = A^H G^-1 (cgemm ConjTrans/NoTrans) stored as the reference's H:
+ * W[k*rows*users + u*rows + r]. */
+void oracle_zf_precoder(const oracle_cf32 *Hin, int users, int rows, int K, oracle_cf32 *W);
+
+/* multiplyWithChannelInv (cpuLS.hpp:451-466, cblas_cgemv per subcarrier) with
+ * the intended operands (modOneSymbol passes them swapped, 494): for nsym
+ * symbols, Y[s][r][k] = sum_u W[k][u][r] X[s][u][k]. */
+void oracle_zf_apply(const oracle_cf32 *W, const oracle_cf32 *X, int users, int rows, int K,
+                     int nsym, oracle_cf32 *Y);
+
+/* The uplink counterpart (no reference function): ZF detection with the same
+ * W, x[s][u][k] = sum_r conj(W[k][u][r]) Y[s][r][k] (W^H = G^-1 A, the
+ * pseudo-inverse of the R x U uplink channel A^H). */
+void oracle_zf_detect(const oracle_cf32 *W, const oracle_cf32 *Y, int users, int rows, int K,
+                      int nsym, oracle_cf32 *X);
+
 #ifdef __cplusplus
 }
 #endif

@@ -17,6 +17,10 @@ void ref_matrix_readX(complexF *X, int K, const char *path) {
     matrix_readX(X, K);
 }
 
+/* rotCube (cpuLS.hpp:400-413): the layout change createZeroForcingMatrix
+ * applies to its channel cube before the per-subcarrier cgemm calls. */
+void ref_rot_cube(complexF *X, int rows, int cols, int users) { rotCube(X, rows, cols, users); }
+
 /* shiftOneRow (cpuLS.hpp:135-149). */
 void ref_shift_one_row(complexF *Y, int K) { shiftOneRow(Y, K, 0); }
 

@@ -49,6 +49,35 @@ class Oracle:
                                           _P, _P]
         L.oracle_pn_extract.argtypes = [_P, _P, _c.c_int, _c.c_longlong, _c.c_int, _c.c_longlong,
                                         _c.c_int, _c.c_int, _c.c_int, _P]
+        L.oracle_zf_precoder.argtypes = [_P, _c.c_int, _c.c_int, _c.c_int, _P]
+        L.oracle_zf_apply.argtypes = [_P, _P, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _P]
+        L.oracle_zf_detect.argtypes = [_P, _P, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _P]
+
+    def zf_precoder(self, H):
+        """createZeroForcingMatrix (cpuLS.hpp:415-447): H (U, R, K) -> W (K, U, R)."""
+        H = c64(H)
+        U, R, K = H.shape
+        W = np.empty((K, U, R), np.complex64)
+        self.lib.oracle_zf_precoder(_ptr(H), U, R, K, _ptr(W))
+        return W
+
+    def zf_apply(self, W, X):
+        """multiplyWithChannelInv per symbol: W (K, U, R), X (n, U, K) -> (n, R, K)."""
+        W, X = c64(W), c64(X)
+        K, U, R = W.shape
+        n = X.shape[0]
+        Y = np.empty((n, R, K), np.complex64)
+        self.lib.oracle_zf_apply(_ptr(W), _ptr(X), U, R, K, n, _ptr(Y))
+        return Y
+
+    def zf_detect(self, W, Y):
+        """W^H y per subcarrier: Y (n, R, K) -> (n, U, K)."""
+        W, Y = c64(W), c64(Y)
+        K, U, R = W.shape
+        n = Y.shape[0]
+        X = np.empty((n, U, K), np.complex64)
+        self.lib.oracle_zf_detect(_ptr(W), _ptr(Y), U, R, K, n, _ptr(X))
+        return X
 
     def pn_correlate(self, buf, pn, thres, mag=False):
         """rx_and_corr.cpp:332-360 -> (pos, mag or None)."""
@@ -155,6 +184,15 @@ class Reference:
         L.ref_shift_one_row.argtypes = [_P, _c.c_int]
         L.ref_ls_post_fft.argtypes = [_P, _P, _c.c_int, _c.c_int, _P, _P]
         L.ref_mrc_post_fft.argtypes = [_P, _P, _P, _c.c_int, _c.c_int, _P]
+        L.ref_rot_cube.argtypes = [_P, _c.c_int, _c.c_int, _c.c_int]
+
+    def rot_cube(self, X):
+        """rotCube (cpuLS.hpp:400-413) in place on a copy: X (users, rows, cols)
+        -> the rotated buffer, returned flat."""
+        X = c64(X).copy()
+        users, rows, cols = X.shape
+        self.lib.ref_rot_cube(_ptr(X), rows, cols, users)
+        return X.ravel()
 
     def matrix_readX(self, path, K):
         X = np.zeros(K, np.complex64)
