@@ -28,6 +28,8 @@
 
 #include <stdlib.h>
 
+#include <type_traits>
+
 namespace ofdm {
 namespace td1024 {
 
@@ -256,9 +258,29 @@ __device__ __forceinline__ void mrc_body(const float2 *__restrict__ iq, int S, i
 // ---------------------------------------------------------------------------
 
 
+// HW = 16 (1024-thread workgroups, one per CU, 144 KiB of LDS): the 16
+// transpose images' row tails hold the whole 8 KiB Hc row (512 float4), so
+// float4 j lives at image j>>5, row (j>>1)&15, tail half j&1 -- and lane t's
+// eight words j = t + 64 i are one affine stride of 2 images (TS float4s).
+// Half the Hc L2 traffic and half the per-row barriers per symbol.
+template <int HW>
+constexpr size_t hlds_lds_bytes() {
+    return (hlds::TW1S + hlds::TW2S + HW * hlds::TS) * sizeof(float2) + (HW == 8 ? 256 * sizeof(float4) : 0);
+}
+static_assert(hlds_lds_bytes<8>() == hlds::LDS_BYTES, "8-wave layout");
+static_assert(hlds_lds_bytes<16>() <= 160 * 1024, "16-wave layout fits one CU");
+template <int HW>
+__device__ __forceinline__ float4 *hslot_hw(float2 *T0, float4 *hfree, int j) {
+    if constexpr (HW == 16)
+        return reinterpret_cast<float4 *>(T0 + (j >> 5) * hlds::TS + ((j >> 1) & 15) * hlds::TP + 64 +
+                                          2 * (j & 1));
+    else
+        return hlds::hslot(T0, hfree, j);
+}
+
 // One antenna row of the PF loop: a[] holds this row on entry and the next
 // row (`next`, when PREF) on exit.
-template <bool NT, bool PREF, int PK>
+template <bool NT, bool PREF, int PK, int HW = 8>
 __device__ __forceinline__ void hlds_row_pf(const float2 *next, const float4 *hrow, int t, float2 (&a)[16],
                                             float2 *T, const float2 *tw1, const float2 *tw2,
                                             const float4 *lo, const float4 *hi, float4 *mine,
@@ -266,16 +288,19 @@ __device__ __forceinline__ void hlds_row_pf(const float2 *next, const float4 *hr
     using namespace hlds;
     float2 x[16];
     row_fft_a<PK>(a, t, T, tw1);
-    const float4 hreg = hrow[threadIdx.x];
+    // a row is 512 float4 = 1024 float2: 1024 threads move 8 B each
+    using HV = typename std::conditional<HW == 16, float2, float4>::type;
+    const HV hreg = reinterpret_cast<const HV *>(hrow)[threadIdx.x];
     __builtin_amdgcn_sched_barrier(0);
     if (PREF) row_load<NT>(next, t, a);
     row_fft_b<PK>(t, T, tw2, x);
     lds_barrier();  // every wave is done with the previous Hc row
-    *mine = hreg;
+    *reinterpret_cast<HV *>(mine) = hreg;
     lds_barrier();
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        const float4 v = i < 4 ? lo[i * 64] : hi[(i - 4) * TS];  // 2 images = TS float4s
+        // HW 8: 2 images = TS float4s; HW 16: hi = lo + 4 TS (ds_read offsets < 64 KiB)
+        const float4 v = i < 4 ? lo[i * (HW == 16 ? TS : 64)] : hi[(i - 4) * TS];
         if constexpr (PK & 4) {
             pk::v2f a0 = pk::V(acc[2 * i]), a1 = pk::V(acc[2 * i + 1]);
             pk::mac(a0, pk::V(x[2 * i]), (pk::v2f){v.x, v.y});
@@ -298,7 +323,7 @@ __device__ __forceinline__ void hlds_row_pf(const float2 *next, const float4 *hr
 // FFT half has written a[] to the transpose image, so it is in flight during
 // the second FFT half, the Hc exchange and the MAC (no extra registers: a[]
 // is dead there).  The Hc prefetch is issued first: vmcnt retires in order.
-template <bool NT, bool SHARED, bool PF, int PK = 0>
+template <bool NT, bool SHARED, bool PF, int PK = 0, int HW = 8>
 __device__ __forceinline__ void hlds_rows(const float2 *sym, int Cp, int R, const float4 *Hf, int t,
                                           float2 *T, const float2 *tw1, const float2 *tw2,
                                           float2 *T0, float4 *hfree, float2 (&acc)[16]) {
@@ -308,18 +333,22 @@ __device__ __forceinline__ void hlds_rows(const float2 *sym, int Cp, int R, cons
     if constexpr (SHARED && PF) {
         float2 a[16];
         row_load<NT>(sym, t, a);
-        const float4 *lo = hfree + t;
-        const float4 *hi = hslot(T0, hfree, 256 + t);
-        float4 *mine = hslot(T0, hfree, threadIdx.x);
+        const float4 *lo = HW == 16 ? hslot_hw<16>(T0, hfree, t) : hfree + t;
+        const float4 *hi = HW == 16 ? lo + 4 * TS : hslot_hw<HW>(T0, hfree, 256 + t);
+        // HW 16: thread i moves float2 i = half (i & 1) of float4 i >> 1
+        float4 *mine = HW == 16 ? reinterpret_cast<float4 *>(reinterpret_cast<float2 *>(
+                                      hslot_hw<16>(T0, hfree, threadIdx.x >> 1)) + (threadIdx.x & 1))
+                                : hslot_hw<HW>(T0, hfree, threadIdx.x);
         // the last row is peeled so that the prefetch is unconditional: the
         // wait for the Hc word before the exchange is then vmcnt(16), not 0
         for (int r = 0; r + 1 < R; ++r)
-            hlds_row_pf<NT, true, PK>(sym + (long long)(r + 1) * Cp, Hf + (long long)r * (C / 2), t, a, T,
-                                      tw1, tw2, lo, hi, mine, acc);
-        hlds_row_pf<NT, false, PK>(sym, Hf + (long long)(R - 1) * (C / 2), t, a, T, tw1, tw2, lo, hi, mine,
-                               acc);
+            hlds_row_pf<NT, true, PK, HW>(sym + (long long)(r + 1) * Cp, Hf + (long long)r * (C / 2), t, a,
+                                          T, tw1, tw2, lo, hi, mine, acc);
+        hlds_row_pf<NT, false, PK, HW>(sym, Hf + (long long)(R - 1) * (C / 2), t, a, T, tw1, tw2, lo, hi,
+                                       mine, acc);
         return;
     }
+    static_assert(!SHARED || PF || HW == 8, "the 16-wave kernel stages Hc with PF only");
     for (int r = 0; r < R; ++r) {
         float2 a[16], x[16], h[16];
         row_load<NT>(sym + (long long)r * Cp, t, a);
@@ -353,8 +382,14 @@ __device__ __forceinline__ void hlds_rows(const float2 *sym, int Cp, int R, cons
     }
 }
 
-template <bool NT, bool PF, int PK>
-__global__ void __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 4)))
+// HW waves (= HW consecutive data symbols) per workgroup.  align != 0:
+// workgroups never straddle frames -- frame f owns logical blocks
+// [f*bpf, (f+1)*bpf), bpf = ceil((S-1)/HW), so every workgroup stages its
+// Hc rows through LDS (the last block of a frame has idle waves) -- instead
+// of packing symbols densely and falling back to per-wave L2 loads of Hc in
+// the workgroups that straddle two frames.
+template <bool NT, bool PF, int PK, int HW = 8, bool ALIGN = false>
+__global__ void __attribute__((amdgpu_flat_work_group_size(64 * HW, 64 * HW), amdgpu_waves_per_eu(4, 4)))
 k_mrc_td1024_hlds(const float2 *__restrict__ iq, int S, int R, int prefix,
                   const float2 *__restrict__ Hc, const float *__restrict__ P,
                   float2 *__restrict__ out, long long nq, long long nblocks, long long per_xcd,
@@ -365,7 +400,7 @@ k_mrc_td1024_hlds(const float2 *__restrict__ iq, int S, int R, int prefix,
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), t = threadIdx.x & 63;
     float2 *T = lds + TW1S + TW2S + w * TS;
     float2 *T0 = lds + TW1S + TW2S;
-    float4 *hfree = reinterpret_cast<float4 *>(T0 + WAVES * TS);
+    float4 *hfree = reinterpret_cast<float4 *>(T0 + HW * TS);
     const long long pb = blockIdx.x;
     const long long lb = (pb & 7) * per_xcd + (pb >> 3);  // XCD-grouped logical block
     if (lb >= nblocks) return;
@@ -374,16 +409,28 @@ k_mrc_td1024_hlds(const float2 *__restrict__ iq, int S, int R, int prefix,
 
     // every wave takes part in the per-row barriers: tail waves duplicate the
     // last symbol and do not store
-    const long long qw = lb * WAVES + w;
-    const bool store = qw < nq;
-    const long long q = store ? qw : nq - 1;
-    // the workgroup's Hc rows come from the frame of its first symbol; a
-    // workgroup straddling two frames falls back to per-wave L2 loads
     const int nsym = S - 1;
-    const long long f = q / nsym;
-    const long long f0 = (lb * WAVES) / nsym;
-    const long long fl = ((lb * WAVES + WAVES - 1 < nq ? lb * WAVES + WAVES - 1 : nq - 1)) / nsym;
-    const bool shared = (f0 == fl);
+    long long q, f, f0;
+    bool store, shared;
+    if constexpr (ALIGN) {
+        const long long bpf = (nsym + HW - 1) / HW;
+        f = lb / bpf;
+        const int j = (int)(lb - f * bpf) * HW + w;  // symbol index within the frame
+        store = j < nsym;
+        q = f * nsym + (store ? j : nsym - 1);
+        f0 = f;
+        shared = true;
+    } else {
+        const long long qw = lb * HW + w;
+        store = qw < nq;
+        q = store ? qw : nq - 1;
+        // the workgroup's Hc rows come from the frame of its first symbol; a
+        // workgroup straddling two frames falls back to per-wave L2 loads
+        f = q / nsym;
+        f0 = (lb * HW) / nsym;
+        const long long fl = ((lb * HW + HW - 1 < nq ? lb * HW + HW - 1 : nq - 1)) / nsym;
+        shared = (f0 == fl);
+    }
     const int s = 1 + (int)(q % nsym);
     const int Cp = C + prefix;
     const float2 *sym = iq + (f * S + s) * (long long)R * Cp + prefix;
@@ -392,9 +439,9 @@ k_mrc_td1024_hlds(const float2 *__restrict__ iq, int S, int R, int prefix,
 
     float2 acc[16];
     if (shared)
-        hlds_rows<NT, true, PF, PK>(sym, Cp, R, Hf0, t, T, tw1, tw2, T0, hfree, acc);
+        hlds_rows<NT, true, PF, PK, HW>(sym, Cp, R, Hf0, t, T, tw1, tw2, T0, hfree, acc);
     else
-        hlds_rows<NT, false, false>(sym, Cp, R, Hf, t, T, tw1, tw2, T0, hfree, acc);
+        hlds_rows<NT, false, false, 0, HW>(sym, Cp, R, Hf, t, T, tw1, tw2, T0, hfree, acc);
     if (!store) return;
     const int b0 = lane_bin0(t);
     float2 *o = out + q * K;
@@ -515,9 +562,43 @@ hipError_t launch_mrc_td1024(const float2 *iq, long long nframes, int S, int R, 
         // packed-f32 FFT halves / MAC (pk.hpp): bit 0 first FFT half, bit 1
         // second half, bit 2 MAC
         const int pkm = knob("OFDM_PK", 0);  // measured: no gain at C = 1024 (memory-bound), spills with PF
+        // OFDM_MRC_ALIGN=1: frame-aligned workgroups; OFDM_MRC_HW=16: 16-wave
+        // workgroups (one per CU, Hc row in the transpose-image tails)
+        const int align = knob("OFDM_MRC_ALIGN", 0);
+        const int hw = knob("OFDM_MRC_HW", 8) == 16 && nt && pf && pkm == 0 ? 16 : 8;
+        const long long nsym = S - 1, bpf = (nsym + hw - 1) / hw;
+        const long long nb = align && nt && pf && pkm == 0 ? nframes * bpf : (nq + hw - 1) / hw;
+        const long long pxcd = (nb + 7) / 8;
+        if (pxcd * 8 > 0x7fffffffll) return hipErrorInvalidValue;
+        if (hw == 16) {
+            static bool attr = false;  // > 64 KiB of dynamic LDS must be opted into once
+            if (!attr) {
+                for (const void *k : {reinterpret_cast<const void *>(&k_mrc_td1024_hlds<true, true, 0, 16, false>),
+                                      reinterpret_cast<const void *>(&k_mrc_td1024_hlds<true, true, 0, 16, true>)}) {
+                    hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       (int)hlds_lds_bytes<16>());
+                    if (e != hipSuccess) return e;
+                }
+                attr = true;
+            }
+            if (align)
+                hipLaunchKernelGGL((k_mrc_td1024_hlds<true, true, 0, 16, true>), dim3((unsigned)(pxcd * 8)),
+                                   dim3(1024), hlds_lds_bytes<16>(), s, iq, S, R, prefix, Hc, P, out, nq, nb,
+                                   pxcd, mode);
+            else
+                hipLaunchKernelGGL((k_mrc_td1024_hlds<true, true, 0, 16, false>), dim3((unsigned)(pxcd * 8)),
+                                   dim3(1024), hlds_lds_bytes<16>(), s, iq, S, R, prefix, Hc, P, out, nq, nb,
+                                   pxcd, mode);
+            return hipGetLastError();
+        }
 #define OFDM_HLDS_LAUNCH(NTV, PFV, PKV)                                                             \
-    hipLaunchKernelGGL((k_mrc_td1024_hlds<NTV, PFV, PKV>), dim3((unsigned)grid), dim3(512),         \
-                       hlds::LDS_BYTES, s, iq, S, R, prefix, Hc, P, out, nq, nblocks, per_xcd, mode)
+    hipLaunchKernelGGL((k_mrc_td1024_hlds<NTV, PFV, PKV>), dim3((unsigned)(pxcd * 8)), dim3(512),   \
+                       hlds::LDS_BYTES, s, iq, S, R, prefix, Hc, P, out, nq, nb, pxcd, mode)
+        if (align && nt && pf && pkm == 0) {
+            hipLaunchKernelGGL((k_mrc_td1024_hlds<true, true, 0, 8, true>), dim3((unsigned)(pxcd * 8)), dim3(512),
+                               hlds::LDS_BYTES, s, iq, S, R, prefix, Hc, P, out, nq, nb, pxcd, mode);
+            return hipGetLastError();
+        }
         if (nt && pf) {
             if (pkm == 7) OFDM_HLDS_LAUNCH(true, true, 7);
             else if (pkm == 3) OFDM_HLDS_LAUNCH(true, true, 3);

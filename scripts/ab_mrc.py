@@ -30,6 +30,7 @@ for v in variants:
     if v != "default":
         keys |= {kv.split("=")[0] for kv in v.split(",")}
 res = {v: [] for v in variants}
+ref_out = None
 for rep in range(reps):           # interleave variants across reps
     for v in variants:
         for k in keys:
@@ -51,6 +52,11 @@ for rep in range(reps):           # interleave variants across reps
             err = int(ofdm.count_symbol_errors(out, S, seed=1).item())
             if err:
                 print(f"{v}: {err} symbol errors!")
+            if ref_out is None:
+                ref_out = out.clone()
+            elif not torch.equal(out, ref_out):
+                print(f"{v}: output differs from {variants[0]} "
+                      f"(max |d| {(out - ref_out).abs().max().item():.3e})")
 b = Q * (R * C * 8 + K * 8)
 for v in variants:
     ms = min(res[v])
