@@ -230,6 +230,116 @@ __global__ void __launch_bounds__(256) k_zf_gemm(const float2 *__restrict__ Wt, 
     }
 }
 
+// The same GEMM with the operand tiles shared through LDS (default for M > 4,
+// N >= 8).
+// Each wave of k_zf_gemm loads its own 8 + 8 operand rows per n, so at U = 16
+// the per-CU L1 path (64 B/clk) had to carry twice the unique bytes and capped
+// the kernel at ~37 % of HBM.  Here the workgroup stages each chunk of NC
+// n-steps -- the MB = MG*8 rows of A and the SB = (4/MG)*8 symbols of the
+// input, 64 subcarriers each -- once, with plain coalesced loads into
+// registers, and every wave reads its 8 + 8 rows per n from LDS (128 B/clk,
+// conflict free: 64 lanes x 8 B contiguous).  The loads of chunk c+1 are in
+// flight while chunk c is computed; two LDS buffers, one barrier per chunk.
+template <int MG, bool CONJ>
+__global__ void __launch_bounds__(256) k_zf_gemm_lds(const float2 *__restrict__ Wt, int a_m, int a_n,
+                                                     const float2 *__restrict__ in, int N, int M, int K,
+                                                     long long nsym, float2 *__restrict__ out, int ntile,
+                                                     int tpx, int nkb, long long chunk_steps) {
+    constexpr int MT = 8, ST = 8, SG = 4 / MG, MB = MG * MT, SB = SG * ST, NC = 2;
+    constexpr int AROWS = NC * MB, ROWS = NC * (MB + SB), RPT = ROWS / 4, AI = AROWS / 4;
+    static_assert(AROWS % 4 == 0 && ROWS % 4 == 0, "rows split evenly over the 4 waves");
+    __shared__ float2 sm[2][ROWS * 64];
+    const int b = blockIdx.x, xcd = b & 7, j = b >> 3;  // XCD-aware mapping as k_zf_gemm
+    const int tile = xcd + 8 * (j % tpx);
+    if (tile >= ntile) return;  // whole workgroup
+    const long long chunk = j / tpx;
+    const int kb = tile % nkb, mb = tile / nkb;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int k = kb * 64 + lane, kc = min(k, K - 1);  // lanes past K load a valid bin, never store
+    const int mg = w % MG, sg = w / MG, mb0 = mb * MB;
+    const long long nsteps_total = (nsym + SB - 1) / SB;
+    const long long step0 = chunk * chunk_steps, step1 = min(step0 + chunk_steps, nsteps_total);
+    const int nnc = (N + NC - 1) / NC;
+    const long long nseq = (step1 - step0) * nnc;
+    if (nseq <= 0) return;  // whole workgroup
+
+    float2 stg[RPT];
+    auto load = [&](long long c) {
+        const long long s0 = (step0 + c / nnc) * SB;
+        const int n0 = (int)(c % nnc) * NC;
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) {
+            const int row = w + 4 * i;
+            if (i < AI) {  // A rows: (n, m) = (n0 + row / MB, mb0 + row % MB)
+                const int n = min(n0 + row / MB, N - 1), m = min(mb0 + row % MB, M - 1);
+                stg[i] = Wt[((long long)m * a_m + (long long)n * a_n) * K + kc];
+            } else {  // input rows: (n, s) = (n0 + rr / SB, s0 + rr % SB)
+                const int rr = row - AROWS;
+                const int n = min(n0 + rr / SB, N - 1);
+                const long long s = min(s0 + rr % SB, nsym - 1);
+                stg[i] = in[(s * N + n) * (long long)K + kc];
+            }
+        }
+    };
+    auto put = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) sm[buf][(w + 4 * i) * 64 + lane] = stg[i];
+    };
+
+    float2 acc[MT][ST];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int jj = 0; jj < ST; ++jj) acc[i][jj] = float2{0.f, 0.f};
+    load(0);
+    put(0);
+    __syncthreads();
+    for (long long c = 0; c < nseq; ++c) {
+        const bool more = c + 1 < nseq;
+        if (more) load(c + 1);  // in flight during this chunk's MACs
+        const float2 *sa = sm[c & 1] + (mg * MT) * 64 + lane;
+        const float2 *sx = sm[c & 1] + (AROWS + sg * ST) * 64 + lane;
+        const int n0 = (int)(c % nnc) * NC, nn = min(NC, N - n0);
+        for (int n = 0; n < nn; ++n) {
+            float2 a[MT], x[ST];
+#pragma unroll
+            for (int i = 0; i < MT; ++i) a[i] = sa[(n * MB + i) * 64];
+#pragma unroll
+            for (int jj = 0; jj < ST; ++jj) x[jj] = sx[(n * SB + jj) * 64];
+#pragma unroll
+            for (int i = 0; i < MT; ++i) {
+                const float ar = a[i].x, ai = CONJ ? -a[i].y : a[i].y;
+#pragma unroll
+                for (int jj = 0; jj < ST; ++jj) {
+                    acc[i][jj].x = fmaf(ar, x[jj].x, fmaf(-ai, x[jj].y, acc[i][jj].x));
+                    acc[i][jj].y = fmaf(ar, x[jj].y, fmaf(ai, x[jj].x, acc[i][jj].y));
+                }
+            }
+        }
+        if (c % nnc == nnc - 1) {  // last n-chunk of a symbol step: store, reset
+            const long long s0 = (step0 + c / nnc) * SB + sg * ST;
+            const int m0 = mb0 + mg * MT;
+            if (k < K) {
+#pragma unroll
+                for (int jj = 0; jj < ST; ++jj) {
+                    if (s0 + jj >= nsym) break;
+                    float2 *o = out + ((s0 + jj) * M) * (long long)K + k;
+#pragma unroll
+                    for (int i = 0; i < MT; ++i)
+                        if (m0 + i < M) o[(long long)(m0 + i) * K] = acc[i][jj];
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int jj = 0; jj < ST; ++jj) acc[i][jj] = float2{0.f, 0.f};
+        }
+        if (more) put((c + 1) & 1);  // that buffer was last read in chunk c - 1
+        __syncthreads();
+    }
+}
+
 }  // namespace zf
 
 size_t zf_precoder_lds_bytes(int U, int R) {
@@ -294,9 +404,34 @@ hipError_t gemm_variant(const float2 *Wt, int a_m, int a_n, const float2 *in, in
               : gemm_launch<MT, 8, MG, CONJ, false>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
 }
 
+template <int MG, bool CONJ>
+hipError_t gemm_lds_launch(const float2 *Wt, int a_m, int a_n, const float2 *in, int N, int M, int K,
+                           long long nsym, float2 *out, hipStream_t s) {
+    constexpr int SB = (4 / MG) * 8;
+    const int nkb = (K + 63) / 64, nmb = (M + MG * 8 - 1) / (MG * 8);
+    const int ntile = nkb * nmb, tpx = (ntile + 7) / 8;
+    const long long nsteps = (nsym + SB - 1) / SB;
+    long long nchunk = (2048 + 8LL * tpx - 1) / (8LL * tpx);
+    long long chunk_steps = (nsteps + nchunk - 1) / nchunk;
+    if (chunk_steps < 4) chunk_steps = 4;
+    nchunk = (nsteps + chunk_steps - 1) / chunk_steps;
+    const long long blocks = 8LL * tpx * nchunk;
+    hipLaunchKernelGGL((zf::k_zf_gemm_lds<MG, CONJ>), dim3((unsigned)blocks), dim3(256), 0, s, Wt, a_m,
+                       a_n, in, N, M, K, nsym, out, ntile, tpx, nkb, chunk_steps);
+    return hipGetLastError();
+}
+
 template <bool CONJ>
 hipError_t gemm_dispatch(const float2 *Wt, int a_m, int a_n, const float2 *in, int N, int M, int K,
                          long long nsym, float2 *out, hipStream_t s) {
+    // LDS-shared tiles when both operands are wide enough (measured: at N = 4
+    // the per-chunk barriers and stores dominate); OFDM_ZF_LDS=0: the
+    // per-wave register-tiled kernel for every shape
+    if (M > 4 && N >= 8 && env_int("OFDM_ZF_LDS", 1)) {
+        if (M <= 8) return gemm_lds_launch<1, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+        if (M <= 16) return gemm_lds_launch<2, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+        return gemm_lds_launch<4, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+    }
     if (M <= 2) return gemm_variant<2, 1, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
     if (M <= 4) return gemm_variant<4, 1, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
     if (M <= 8) return gemm_variant<8, 1, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);

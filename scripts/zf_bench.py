@@ -69,16 +69,16 @@ def main():
         ab = {}
         if a.ab:  # same-process A/B of the register tile / prefetch knobs
             for rnd in range(2):
-                for st in ("8", "4"):
-                    for pf in ("1", "0"):
+                for st, pf, lds in (("8", "1", "1"), ("8", "1", "0"), ("4", "1", "0")):
                         os.environ["OFDM_ZF_ST"], os.environ["OFDM_ZF_PF"] = st, pf
-                        key = f"st{st}_pf{pf}"
+                        os.environ["OFDM_ZF_LDS"] = lds
+                        key = "lds" if lds == "1" else f"regtile_st{st}"
                         d = timed(lambda: ofdm.zf_detect(Wt, Y, out=Xo), a.reps)
                         p = timed(lambda: ofdm.zf_apply(Wt, X, out=Yo), a.reps)
                         old = ab.get(key, (1e9, 1e9))
                         ab[key] = (min(old[0], d), min(old[1], p))
-            os.environ.pop("OFDM_ZF_ST")
-            os.environ.pop("OFDM_ZF_PF")
+            for v in ("OFDM_ZF_ST", "OFDM_ZF_PF", "OFDM_ZF_LDS"):
+                os.environ.pop(v)
         t_det = timed(lambda: ofdm.zf_detect(Wt, Y, out=Xo), a.reps)
         t_app = timed(lambda: ofdm.zf_apply(Wt, X, out=Yo), a.reps)
         byt = n * (U + R) * K * 8.0
