@@ -240,12 +240,13 @@ __global__ void __launch_bounds__(256) k_zf_gemm(const float2 *__restrict__ Wt, 
 // registers, and every wave reads its 8 + 8 rows per n from LDS (128 B/clk,
 // conflict free: 64 lanes x 8 B contiguous).  The loads of chunk c+1 are in
 // flight while chunk c is computed; two LDS buffers, one barrier per chunk.
-template <int MG, bool CONJ>
-__global__ void __launch_bounds__(256) k_zf_gemm_lds(const float2 *__restrict__ Wt, int a_m, int a_n,
-                                                     const float2 *__restrict__ in, int N, int M, int K,
-                                                     long long nsym, float2 *__restrict__ out, int ntile,
-                                                     int tpx, int nkb, long long chunk_steps) {
-    constexpr int MT = 8, ST = 8, SG = 4 / MG, MB = MG * MT, SB = SG * ST, NC = 2;
+// ST = 4, NC = 1 (OFDM_ZF_ST=4): 8x4 tiles, 64 accumulator VGPRs, 4 waves/SIMD.
+template <int MG, bool CONJ, bool NTIN = false, int ST = 8, int NC = 2>
+__global__ void __attribute__((amdgpu_flat_work_group_size(256, 256), amdgpu_waves_per_eu(ST == 4 ? 4 : 1)))
+k_zf_gemm_lds(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__restrict__ in, int N, int M,
+              int K, long long nsym, float2 *__restrict__ out, int ntile, int tpx, int nkb,
+              long long chunk_steps) {
+    constexpr int MT = 8, SG = 4 / MG, MB = MG * MT, SB = SG * ST;
     constexpr int AROWS = NC * MB, ROWS = NC * (MB + SB), RPT = ROWS / 4, AI = AROWS / 4;
     static_assert(AROWS % 4 == 0 && ROWS % 4 == 0, "rows split evenly over the 4 waves");
     __shared__ float2 sm[2][ROWS * 64];
@@ -278,7 +279,12 @@ __global__ void __launch_bounds__(256) k_zf_gemm_lds(const float2 *__restrict__ 
                 const int rr = row - AROWS;
                 const int n = min(n0 + rr / SB, N - 1);
                 const long long s = min(s0 + rr % SB, nsym - 1);
-                stg[i] = in[(s * N + n) * (long long)K + kc];
+                const float2 *p = in + (s * N + n) * (long long)K + kc;
+                if constexpr (NTIN)  // streamed once: keep it from evicting the re-read W tiles
+                    stg[i] = __builtin_bit_cast(
+                        float2, __builtin_nontemporal_load(reinterpret_cast<const unsigned long long *>(p)));
+                else
+                    stg[i] = *p;
             }
         }
     };
@@ -338,6 +344,131 @@ __global__ void __launch_bounds__(256) k_zf_gemm_lds(const float2 *__restrict__ 
         if (more) put((c + 1) & 1);  // that buffer was last read in chunk c - 1
         __syncthreads();
     }
+}
+
+// The same GEMM with the chunks DMA'd straight into LDS (global_load_lds_dword:
+// lane l of an instruction moves dword l of a 256-B half row, so rows of
+// 64 subcarriers land in LDS in their natural float2 order; 4-B granules
+// because a row starts at an odd multiple of 8 B when K is odd).  No VGPR
+// staging, so NB = 4 LDS buffers of one n-step each keep three steps of
+// loads in flight behind the MACs.  Per step: wait until this wave's loads of
+// step c have landed (vmcnt = the two younger steps' loads), one barrier
+// (everyone's rows of step c visible, everyone done with step c - 1), issue
+// step c + 3 into step c - 1's buffer, MACs.
+typedef __attribute__((address_space(3))) void lvoid_t;
+
+// One global_load_lds_dword: lane l's dword lands at LDS byte lds + 4 l.  In
+// inline asm on purpose: through __builtin_amdgcn_global_load_lds the
+// compiler cannot tell which buffer a ds_read may alias and puts
+// s_waitcnt vmcnt(0) in front of every LDS read, draining the prefetch.  The
+// loop's own s_waitcnt vmcnt(N) + s_barrier publish the data instead.  M0 is
+// compiler-reserved: saved and restored in the same statement, with the
+// s_nop the M0 write -> LDS-DMA hazard needs (cdna_hip_programming.md).
+__device__ __forceinline__ void dma_dword(const float *g, unsigned lds) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(g), "s"(lds)
+                 : "memory");
+}
+
+template <int MG, bool CONJ>
+__global__ void __launch_bounds__(256) k_zf_gemm_dma(const float2 *__restrict__ Wt, int a_m, int a_n,
+                                                     const float2 *__restrict__ in, int N, int M, int K,
+                                                     long long nsym, float2 *__restrict__ out, int ntile,
+                                                     int tpx, int nkb, long long chunk_steps) {
+    constexpr int MT = 8, ST = 8, SG = 4 / MG, MB = MG * MT, SB = SG * ST, NB = 4;
+    constexpr int ROWS = MB + SB, RPW = ROWS / 4, LPW = 2 * RPW;
+    static_assert(ROWS % 4 == 0 && (NB - 2) * LPW <= 63, "rows per wave / vmcnt range");
+    __shared__ float2 sm[NB][ROWS * 64];
+    const int b = blockIdx.x, xcd = b & 7, j = b >> 3;  // XCD-aware mapping as k_zf_gemm
+    const int tile = xcd + 8 * (j % tpx);
+    if (tile >= ntile) return;  // whole workgroup
+    const long long chunk = j / tpx;
+    const int kb = tile % nkb, mb = tile / nkb;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int k = kb * 64 + lane;
+    const int mg = w % MG, sg = w / MG, mb0 = mb * MB;
+    const long long nsteps_total = (nsym + SB - 1) / SB;
+    const long long step0 = chunk * chunk_steps, step1 = min(step0 + chunk_steps, nsteps_total);
+    const long long nseq = (step1 - step0) * N;  // one n per LDS chunk
+    if (nseq <= 0) return;  // whole workgroup
+    // this lane's dword within a half row: element e0 + (lane >> 1) (clamped
+    // to K - 1 past the end: those subcarriers are computed, never stored)
+    const int eh0 = min(kb * 64 + (lane >> 1), K - 1), eh1 = min(kb * 64 + 32 + (lane >> 1), K - 1);
+    const int comp = lane & 1;
+
+    auto issue = [&](long long c) {  // step c (clamped: the tail re-loads the last step)
+        c = min(c, nseq - 1);
+        const int buf = (int)(c % NB);
+        const long long s0 = (step0 + c / N) * SB;
+        const int n = (int)(c % N);
+#pragma unroll
+        for (int i = 0; i < RPW; ++i) {
+            const int row = w + 4 * i;
+            const float2 *src;
+            if (row < MB) {
+                const int m = min(mb0 + row, M - 1);
+                src = Wt + ((long long)m * a_m + (long long)n * a_n) * K;
+            } else {
+                const long long s = min(s0 + (row - MB), nsym - 1);
+                src = in + (s * N + n) * (long long)K;
+            }
+            const unsigned la = (unsigned)(size_t)(lvoid_t *)&sm[buf][row * 64];  // LDS byte address
+            dma_dword(reinterpret_cast<const float *>(src + eh0) + comp, la);
+            dma_dword(reinterpret_cast<const float *>(src + eh1) + comp, la + 256);
+        }
+    };
+
+    float2 acc[MT][ST];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int jj = 0; jj < ST; ++jj) acc[i][jj] = float2{0.f, 0.f};
+#pragma unroll
+    for (int p = 0; p < NB - 1; ++p) issue(p);
+    for (long long c = 0; c < nseq; ++c) {
+        // no __syncthreads(): its fence would wait for every load in flight
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((NB - 2) * LPW) : "memory");
+        issue(c + NB - 1);  // into the buffer of step c - 1, which everyone has finished
+        const float2 *sa = sm[c % NB] + (mg * MT) * 64 + lane;
+        const float2 *sx = sm[c % NB] + (MB + sg * ST) * 64 + lane;
+        float2 a[MT], x[ST];
+#pragma unroll
+        for (int i = 0; i < MT; ++i) a[i] = sa[i * 64];
+#pragma unroll
+        for (int jj = 0; jj < ST; ++jj) x[jj] = sx[jj * 64];
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+            const float ar = a[i].x, ai = CONJ ? -a[i].y : a[i].y;
+#pragma unroll
+            for (int jj = 0; jj < ST; ++jj) {
+                acc[i][jj].x = fmaf(ar, x[jj].x, fmaf(-ai, x[jj].y, acc[i][jj].x));
+                acc[i][jj].y = fmaf(ar, x[jj].y, fmaf(ai, x[jj].x, acc[i][jj].y));
+            }
+        }
+        if (c % N == N - 1) {  // last n of a symbol step: store, reset
+            const long long s0 = (step0 + c / N) * SB + sg * ST;
+            const int m0 = mb0 + mg * MT;
+            if (k < K) {
+#pragma unroll
+                for (int jj = 0; jj < ST; ++jj) {
+                    if (s0 + jj >= nsym) break;
+                    float2 *o = out + ((s0 + jj) * M) * (long long)K + k;
+#pragma unroll
+                    for (int i = 0; i < MT; ++i)
+                        if (m0 + i < M) o[(long long)(m0 + i) * K] = acc[i][jj];
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int jj = 0; jj < ST; ++jj) acc[i][jj] = float2{0.f, 0.f};
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the tail re-loads before exit
 }
 
 }  // namespace zf
@@ -404,10 +535,10 @@ hipError_t gemm_variant(const float2 *Wt, int a_m, int a_n, const float2 *in, in
               : gemm_launch<MT, 8, MG, CONJ, false>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
 }
 
-template <int MG, bool CONJ>
+template <int MG, bool CONJ, bool DMA, int ST = 8>
 hipError_t gemm_lds_launch(const float2 *Wt, int a_m, int a_n, const float2 *in, int N, int M, int K,
                            long long nsym, float2 *out, hipStream_t s) {
-    constexpr int SB = (4 / MG) * 8;
+    constexpr int SB = (4 / MG) * ST;
     const int nkb = (K + 63) / 64, nmb = (M + MG * 8 - 1) / (MG * 8);
     const int ntile = nkb * nmb, tpx = (ntile + 7) / 8;
     const long long nsteps = (nsym + SB - 1) / SB;
@@ -416,8 +547,18 @@ hipError_t gemm_lds_launch(const float2 *Wt, int a_m, int a_n, const float2 *in,
     if (chunk_steps < 4) chunk_steps = 4;
     nchunk = (nsteps + chunk_steps - 1) / chunk_steps;
     const long long blocks = 8LL * tpx * nchunk;
-    hipLaunchKernelGGL((zf::k_zf_gemm_lds<MG, CONJ>), dim3((unsigned)blocks), dim3(256), 0, s, Wt, a_m,
-                       a_n, in, N, M, K, nsym, out, ntile, tpx, nkb, chunk_steps);
+    if (ST == 4)  // 8x4 tiles, one n per LDS chunk, 4 waves/SIMD
+        hipLaunchKernelGGL((zf::k_zf_gemm_lds<MG, CONJ, false, 4, 1>), dim3((unsigned)blocks), dim3(256), 0, s,
+                           Wt, a_m, a_n, in, N, M, K, nsym, out, ntile, tpx, nkb, chunk_steps);
+    else if (DMA)
+        hipLaunchKernelGGL((zf::k_zf_gemm_dma<MG, CONJ>), dim3((unsigned)blocks), dim3(256), 0, s, Wt, a_m,
+                           a_n, in, N, M, K, nsym, out, ntile, tpx, nkb, chunk_steps);
+    else if (env_int("OFDM_ZF_NT", 0))  // nontemporal input stream
+        hipLaunchKernelGGL((zf::k_zf_gemm_lds<MG, CONJ, true>), dim3((unsigned)blocks), dim3(256), 0, s, Wt,
+                           a_m, a_n, in, N, M, K, nsym, out, ntile, tpx, nkb, chunk_steps);
+    else
+        hipLaunchKernelGGL((zf::k_zf_gemm_lds<MG, CONJ>), dim3((unsigned)blocks), dim3(256), 0, s, Wt, a_m,
+                           a_n, in, N, M, K, nsym, out, ntile, tpx, nkb, chunk_steps);
     return hipGetLastError();
 }
 
@@ -427,10 +568,22 @@ hipError_t gemm_dispatch(const float2 *Wt, int a_m, int a_n, const float2 *in, i
     // LDS-shared tiles when both operands are wide enough (measured: at N = 4
     // the per-chunk barriers and stores dominate); OFDM_ZF_LDS=0: the
     // per-wave register-tiled kernel for every shape
-    if (M > 4 && N >= 8 && env_int("OFDM_ZF_LDS", 1)) {
-        if (M <= 8) return gemm_lds_launch<1, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-        if (M <= 16) return gemm_lds_launch<2, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-        return gemm_lds_launch<4, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+    // OFDM_ZF_LDS=2: LDS tiles DMA'd straight from global memory (k_zf_gemm_dma)
+    const int lds = env_int("OFDM_ZF_LDS", 1);
+    if (M > 4 && N >= 8 && lds == 2) {
+        if (M <= 8) return gemm_lds_launch<1, CONJ, true>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+        if (M <= 16) return gemm_lds_launch<2, CONJ, true>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+        return gemm_lds_launch<4, CONJ, true>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+    }
+    if (M > 4 && N >= 8 && lds && env_int("OFDM_ZF_ST", 8) == 4) {
+        if (M <= 8) return gemm_lds_launch<1, CONJ, false, 4>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+        if (M <= 16) return gemm_lds_launch<2, CONJ, false, 4>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+        return gemm_lds_launch<4, CONJ, false, 4>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+    }
+    if (M > 4 && N >= 8 && lds) {
+        if (M <= 8) return gemm_lds_launch<1, CONJ, false>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+        if (M <= 16) return gemm_lds_launch<2, CONJ, false>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+        return gemm_lds_launch<4, CONJ, false>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
     }
     if (M <= 2) return gemm_variant<2, 1, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
     if (M <= 4) return gemm_variant<4, 1, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);

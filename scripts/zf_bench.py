@@ -67,18 +67,21 @@ def main():
         t_pre = timed(lambda: ofdm.zf_precoder(H, W=W, Wt=Wt), a.reps)
         t_tr = timed(lambda: ofdm.zf_transpose(W), a.reps)
         ab = {}
-        if a.ab:  # same-process A/B of the register tile / prefetch knobs
+        if a.ab:  # same-process A/B of the kernel variants (env knobs are read per launch)
+            variants = {"lds": {"OFDM_ZF_LDS": "1"}, "lds_8x4": {"OFDM_ZF_LDS": "1", "OFDM_ZF_ST": "4"},
+                        "lds_nt": {"OFDM_ZF_LDS": "1", "OFDM_ZF_NT": "1"},
+                        "dma": {"OFDM_ZF_LDS": "2"}, "regtile": {"OFDM_ZF_LDS": "0"}}
             for rnd in range(2):
-                for st, pf, lds in (("8", "1", "1"), ("8", "1", "0"), ("4", "1", "0")):
-                        os.environ["OFDM_ZF_ST"], os.environ["OFDM_ZF_PF"] = st, pf
-                        os.environ["OFDM_ZF_LDS"] = lds
-                        key = "lds" if lds == "1" else f"regtile_st{st}"
-                        d = timed(lambda: ofdm.zf_detect(Wt, Y, out=Xo), a.reps)
-                        p = timed(lambda: ofdm.zf_apply(Wt, X, out=Yo), a.reps)
-                        old = ab.get(key, (1e9, 1e9))
-                        ab[key] = (min(old[0], d), min(old[1], p))
-            for v in ("OFDM_ZF_ST", "OFDM_ZF_PF", "OFDM_ZF_LDS"):
-                os.environ.pop(v)
+                for key, env in variants.items():
+                    for v in ("OFDM_ZF_LDS", "OFDM_ZF_NT", "OFDM_ZF_ST"):
+                        os.environ.pop(v, None)
+                    os.environ.update(env)
+                    d = timed(lambda: ofdm.zf_detect(Wt, Y, out=Xo), a.reps)
+                    p = timed(lambda: ofdm.zf_apply(Wt, X, out=Yo), a.reps)
+                    old = ab.get(key, (1e9, 1e9))
+                    ab[key] = (min(old[0], d), min(old[1], p))
+            for v in ("OFDM_ZF_LDS", "OFDM_ZF_NT", "OFDM_ZF_ST"):
+                os.environ.pop(v, None)
         t_det = timed(lambda: ofdm.zf_detect(Wt, Y, out=Xo), a.reps)
         t_app = timed(lambda: ofdm.zf_apply(Wt, X, out=Yo), a.reps)
         byt = n * (U + R) * K * 8.0

@@ -64,6 +64,24 @@ def test_argument_validation_without_device(ofdm):
     assert L.ofdm_frame_demod(fake, 0, 11, 64, 1024, 0, fake, fake, need, fake, None) == 0
 
 
+def test_zf_argument_validation_without_device(ofdm):
+    """ofdm_zf_* reject unsupported geometry and null pointers before any launch."""
+    L = ofdm.lib()
+    P = ctypes.c_void_p
+    fake = P(4096)
+    assert L.ofdm_zf_precoder(fake, 33, 64, 1023, fake, None, None) == -3  # > OFDM_ZF_MAX_USERS
+    assert b"users" in L.ofdm_last_error()
+    assert L.ofdm_zf_precoder(fake, 16, 513, 1023, fake, None, None) == -3  # users*rows > 8192
+    assert L.ofdm_zf_precoder(fake, 0, 64, 1023, fake, None, None) == -3
+    assert L.ofdm_zf_precoder(fake, 4, 0, 1023, fake, None, None) == -1
+    assert L.ofdm_zf_precoder(fake, 4, 8, 1023, None, None, None) == -1  # no output at all
+    assert L.ofdm_zf_precoder(None, 4, 8, 0, None, None, None) == 0  # K = 0: nothing to do
+    assert L.ofdm_zf_transpose(fake, 4, 8, 16, fake, None) == -1  # aliased
+    assert L.ofdm_zf_apply(fake, fake, 4, 8, 16, -1, fake, None) == -1
+    assert L.ofdm_zf_apply(None, None, 4, 8, 16, 0, None, None) == 0  # no symbols
+    assert L.ofdm_zf_detect(fake, None, 4, 8, 16, 3, fake, None) == -1
+
+
 def test_workspace_sizes(ofdm):
     # fused C=1024: Hc [F][R][C] + P [F][C], no staging
     F, S, R, C = 100, 101, 16, 1024

@@ -52,9 +52,11 @@ def test_zf_precoder_single_output(ofdm, dev):
                                      (5, 12, 130, 17), (8, 64, 1023, 40), (12, 40, 200, 16),
                                      (16, 64, 1023, 100), (17, 64, 65, 3), (32, 64, 255, 25),
                                      (16, 100, 1023, 8)])
-@pytest.mark.parametrize("lds", ["1", "0"])  # LDS-shared tiles (default) / per-wave register tiles
-def test_zf_apply_detect_parity(ofdm, oracle, dev, monkeypatch, U, R, K, n, lds):
-    monkeypatch.setenv("OFDM_ZF_LDS", lds)
+@pytest.mark.parametrize("lds", ["1", "0", "2", "1st4"])  # LDS tiles (default) / per-wave registers /
+def test_zf_apply_detect_parity(ofdm, oracle, dev, monkeypatch, U, R, K, n, lds):  # DMA-fed LDS / 8x4 LDS
+    monkeypatch.setenv("OFDM_ZF_LDS", lds[0])
+    if lds.endswith("st4"):
+        monkeypatch.setenv("OFDM_ZF_ST", "4")
     H = channel(U, R, K, seed=n)
     W = oracle.zf_precoder(H)
     X = qpsk(n, U, K, seed=n + 1)
