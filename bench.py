@@ -208,7 +208,7 @@ def main():
            "data_symbols_per_gpu": Q, "global_data_symbols": Q * world,
            "parallelism": f"frame-sharded x{world}, no collective"}
     b_sym = R * C * 8 + K * 8
-    kern = {1024: "k_mrc_td1024_hlds", 2048: "k_mrc_td2048", 4096: "k_mrc_td4096"}.get(C)
+    kern = {1024: "k_mrc_td1024_hlds", 2048: "k_mrc_td2048", 4096: "k_mrc_td4096h"}.get(C)
     mrc_name = f"{kern} (FFT+MRC+normalise+rotate)" if kern else "k_fft_rows + k_mrc_freq (staged)"
     achieved = Q * b_sym / (mrc_ms * 1e-3) / 1e9
     traffic, tsrc = pmc_traffic(args.pmc, cfg)
@@ -389,7 +389,7 @@ def bench_split(args, X, dev, world, rank, barrier):
     mrc_ms = e0.elapsed_time(e1) / reps
     b_sym = R * C * 8 + K * 8
     achieved = Q * b_sym / (mrc_ms * 1e-3) / 1e9
-    kern = {1024: "k_mrc_td1024_hlds", 2048: "k_mrc_td2048", 4096: "k_mrc_td4096x"}.get(C, "k_mrc_freq")
+    kern = {1024: "k_mrc_td1024_hlds", 2048: "k_mrc_td2048", 4096: "k_mrc_td4096h"}.get(C, "k_mrc_freq")
     result = {
         "metric": "OFDM symbols/s (LS+MRC) at 1024 subcarriers x 64 ant; achieved HBM GB/s vs peak",
         "value": Q / (elapsed / args.steps),

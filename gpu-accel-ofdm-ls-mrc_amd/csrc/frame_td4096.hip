@@ -273,15 +273,43 @@ __device__ __forceinline__ pk::v2f dif_tw(pk::v2f base) {  // base * W64^(CM * M
     return pk::cmul_s_v(base, (pk::v2f){w.x, w.y});
 }
 
+typedef __attribute__((address_space(3))) void lvoid_t;
+__device__ __forceinline__ unsigned lds_addr(const void *p) { return (unsigned)(size_t)(lvoid_t *)p; }
+
+// 16 B per lane straight into LDS at byte lds + 16 lane (global_load_lds_dwordx4
+// in inline asm: the builtin makes the compiler wait vmcnt(0) before every LDS
+// read; M0 saved/restored in the same statement, s_nop for the M0 hazard).
+__device__ __forceinline__ void dma16(const void *g, unsigned lds) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(g), "s"(lds)
+                 : "memory");
+}
+// One 32 KiB Hc row (4096 float2) into LDS by a 512-thread workgroup: four
+// wave-instructions of 1 KiB per wave, natural order.
+__device__ __forceinline__ void dma_hc_row(const float2 *g, unsigned lds) {
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const char *src = reinterpret_cast<const char *>(g) + w * 1024 + lane * 16;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dma16(src + j * 8192, lds + j * 8192 + w * 1024);
+}
+
 // One antenna row for wave E of the pair.  On entry a/b hold the row's
 // quarters E and E + 2; with PREF the next row's quarters are loaded into
 // them after the first FFT (behind this row's Hc loads: loads retire in
 // order) and stay in flight through the second FFT and MAC.
-template <int E, bool NT, int PK, bool PREF>
+// HL (k_mrc_td4096h): hr points at this row's Hc in LDS, DMA'd during the
+// previous row; this row's first barrier publishes it (after vmcnt(0)) and
+// the DMA of row r+1 (hnext, into LDS byte address hb_next) is issued right
+// after that barrier, into the buffer every wave finished with in row r-1.
+template <int E, bool NT, int PK, bool PREF, int DBG = 0, bool HL = false>
 __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const float2 *__restrict__ hr,
                                       int t, float2 *T, const float2 *Tp, const float2 *tw1,
                                       const float2 *tw2, pk::v2f wb0, pk::v2f wb1, float2 (&a)[16],
-                                      float2 (&b)[16], float2 (&ae)[16], float2 (&ao)[16]) {
+                                      float2 (&b)[16], float2 (&ae)[16], float2 (&ao)[16],
+                                      const float2 *hnext = nullptr, unsigned hb_next = 0) {
     using namespace pk;
     v2f u[16], v[16];
 #pragma unroll
@@ -290,12 +318,18 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
         v[m] = sub(V(a[m]), V(b[m]));  // d
     }
     float2 h[16], h1[16];
+    if constexpr (!HL) {
 #pragma unroll
-    for (int k = 0; k < 16; ++k) h[k] = hr[k * 64 + t];  // plane 0: bins 4 b + E
+        for (int k = 0; k < 16; ++k)  // plane 0: bins 4 b + E (DBG & 2: diagnostic, no Hc traffic)
+            h[k] = (DBG & 2) ? float2{1.f, (float)k} : hr[k * 64 + t];
+    }
     // wave 0 sends d and keeps s (= a); wave 1 sends s (= c) and keeps d
 #pragma unroll
     for (int m = 0; m < 16; ++m) T[hl::swz(m, t)] = F(E ? u[m] : v[m]);
+    if constexpr (HL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this row's Hc DMA landed
     td1024::lds_barrier();
+    if constexpr (HL)
+        if (hnext) dma_hc_row(hnext, hb_next);
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
         if (E) u[m] = V(Tp[hl::swz(m, t)]);  // b
@@ -348,8 +382,13 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
     hl::row_fft_a<PK>(z, t, T, tw1);
     hl::row_fft_b<PK>(t, T, tw2, x);
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (HL) {
 #pragma unroll
-    for (int k = 0; k < 16; ++k) h1[k] = hr[1024 + k * 64 + t];  // plane 1: bins 4 b + 2 + E
+        for (int k = 0; k < 16; ++k) h[k] = hr[k * 64 + t];  // plane 0 from LDS
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k)  // plane 1: bins 4 b + 2 + E
+        h1[k] = (DBG & 2) ? float2{(float)k, 1.f} : hr[1024 + k * 64 + t];
     mac(ae);
     __builtin_amdgcn_sched_barrier(0);
     // next row in flight during the second FFT and the next row's exchange
@@ -366,7 +405,7 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
     mac(ao);
 }
 
-template <int E, bool NT, int PK>
+template <int E, bool NT, int PK, int DBG = 0>
 __device__ __forceinline__ void x_rows(const float2 *sym, int Cp, int R, const float2 *Hf, int t,
                                        float2 *T, const float2 *Tp, const float2 *tw1,
                                        const float2 *tw2, pk::v2f wb0, pk::v2f wb1,
@@ -375,13 +414,13 @@ __device__ __forceinline__ void x_rows(const float2 *sym, int Cp, int R, const f
     row_load<NT>(sym + 1024 * E, t, a);
     row_load<NT>(sym + 1024 * (E + 2), t, b);
     for (int r = 0; r + 1 < R; ++r)
-        x_row<E, NT, PK, true>(sym + (long long)(r + 1) * Cp, Hf + (long long)r * C, t, T, Tp, tw1,
+        x_row<E, NT, PK, true, DBG>(sym + (long long)(r + 1) * Cp, Hf + (long long)r * C, t, T, Tp, tw1,
                                tw2, wb0, wb1, a, b, ae, ao);
-    x_row<E, NT, PK, false>(sym, Hf + (long long)(R - 1) * C, t, T, Tp, tw1, tw2, wb0, wb1, a, b,
+    x_row<E, NT, PK, false, DBG>(sym, Hf + (long long)(R - 1) * C, t, T, Tp, tw1, tw2, wb0, wb1, a, b,
                             ae, ao);
 }
 
-template <bool NT, int PK, int WPE>
+template <bool NT, int PK, int WPE, int DBG = 0>
 __global__ void __attribute__((amdgpu_flat_work_group_size(128, 128), amdgpu_waves_per_eu(WPE, WPE)))
 k_mrc_td4096x(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
               const float *__restrict__ P, float2 *__restrict__ out, long long nq, long long per_xcd,
@@ -411,9 +450,105 @@ k_mrc_td4096x(const float2 *__restrict__ iq, int S, int R, int prefix, const flo
 #pragma unroll
     for (int k = 0; k < 16; ++k) ae[k] = ao[k] = float2{0.f, 0.f};
     if (e)
-        x_rows<1, NT, PK>(sym, Cp, R, Hf, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
+        x_rows<1, NT, PK, DBG>(sym, Cp, R, Hf, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
     else
-        x_rows<0, NT, PK>(sym, Cp, R, Hf, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
+        x_rows<0, NT, PK, DBG>(sym, Cp, R, Hf, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
+    const int b0 = lane_bin0(t);
+    float2 *o = out + q * K;
+    const float *Pf = P + f * C;
+    if ((mode & 1) == 0) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int be = 4 * (b0 + 16 * k) + e;
+            if (be > 0) {
+                const float pv = Pf[be];
+                o[out_pos(be - 1, K)] = float2{ae[k].x / pv, ae[k].y / pv};
+            }
+            const float pv = Pf[be + 2];
+            o[out_pos(be + 1, K)] = float2{ao[k].x / pv, ao[k].y / pv};
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int be = 4 * (b0 + 16 * k) + e;
+            if (be > 0) o[be - 1] = ae[k];
+            o[be + 1] = ao[k];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// MRC with the channel rows shared through LDS (k_mrc_td4096h): workgroup =
+// 4 wave pairs = 4 consecutive data symbols of ONE frame (frame-aligned block
+// map, bpf = ceil((S-1)/4) blocks per frame; tail pairs repeat the frame's
+// last symbol without storing), so the frame's 32 KiB Hc row is fetched once
+// per workgroup by LDS-DMA into a double buffer instead of by every wave
+// from L2 (k_mrc_td4096x: Hc traffic = IQ traffic; without it the kernel ran
+// 13 % faster, the diagnostic OFDM_MRC4K_DEBUG=2).  The pairs' two exchange
+// barriers per row become workgroup barriers and also publish the Hc row.
+// LDS: tables 8 KiB + 8 transpose images 68 KiB + 2 x 32 KiB = 140 KiB, one
+// workgroup (8 waves, 2 per SIMD as the 242-VGPR x kernel) per CU.
+// ---------------------------------------------------------------------------
+constexpr int H_PAIRS = 4;
+constexpr size_t H_LDS = (size_t)(X_TAB + 2 * H_PAIRS * hl::TS + 2 * C) * sizeof(float2);
+static_assert(H_LDS <= 160 * 1024, "one workgroup per CU");
+
+template <int E, bool NT, int PK>
+__device__ __forceinline__ void h_rows(const float2 *sym, int Cp, int R, const float2 *Hg, float2 *HB, int t,
+                                       float2 *T, const float2 *Tp, const float2 *tw1, const float2 *tw2,
+                                       pk::v2f wb0, pk::v2f wb1, float2 (&ae)[16], float2 (&ao)[16]) {
+    float2 a[16], b[16];
+    row_load<NT>(sym + 1024 * E, t, a);
+    row_load<NT>(sym + 1024 * (E + 2), t, b);
+    const unsigned hb0 = lds_addr(HB), hb1 = lds_addr(HB + C);
+    for (int r = 0; r + 1 < R; ++r)
+        x_row<E, NT, PK, true, 0, true>(sym + (long long)(r + 1) * Cp, HB + (r & 1) * C + E * 2048, t, T, Tp,
+                                        tw1, tw2, wb0, wb1, a, b, ae, ao, Hg + (long long)(r + 1) * C,
+                                        (r & 1) ? hb0 : hb1);
+    x_row<E, NT, PK, false, 0, true>(sym, HB + ((R - 1) & 1) * C + E * 2048, t, T, Tp, tw1, tw2, wb0, wb1, a,
+                                     b, ae, ao, nullptr, 0);
+}
+
+template <bool NT, int PK>
+__global__ void __attribute__((amdgpu_flat_work_group_size(128 * H_PAIRS, 128 * H_PAIRS),
+                               amdgpu_waves_per_eu(2, 2)))
+k_mrc_td4096h(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
+              const float *__restrict__ P, float2 *__restrict__ out, long long nframes, long long nblocks,
+              long long per_xcd, int mode) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), t = threadIdx.x & 63;
+    const int e = w & 1, pair = w >> 1;
+    const float2 *tw1 = lds, *tw2 = lds + hl::TW1S;
+    float2 *T = lds + X_TAB + w * hl::TS;
+    const float2 *Tp = lds + X_TAB + (w ^ 1) * hl::TS;
+    float2 *HB = lds + X_TAB + 2 * H_PAIRS * hl::TS;  // [2][C] Hc rows
+    const long long pb = blockIdx.x;
+    const long long lb = (pb & 7) * per_xcd + (pb >> 3);  // XCD-grouped: a frame's blocks share an L2
+    if (lb >= nblocks) return;  // whole workgroup
+    const int nsym = S - 1;
+    const long long bpf = (nsym + H_PAIRS - 1) / H_PAIRS;
+    const long long f = lb / bpf;
+    const int j = (int)(lb - f * bpf) * H_PAIRS + pair;  // data symbol index within the frame
+    const bool store = j < nsym;
+    const int s = 1 + (store ? j : nsym - 1);
+    const float2 *Hg = Hc + f * (long long)R * C;
+    dma_hc_row(Hg, lds_addr(HB));  // row 0; landed at the first row's barrier
+    hl::fill(lds, lds + hl::TW1S);
+    __syncthreads();
+
+    const int Cp = C + prefix;
+    const float2 *sym = iq + (f * S + s) * (long long)R * Cp + prefix;
+    const pk::v2f wb0 = pk::V(g_tw[(e ? 1 : 2) * t]);
+    const pk::v2f wb1 = pk::V(g_tw[3 * t]);
+    float2 ae[16], ao[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) ae[k] = ao[k] = float2{0.f, 0.f};
+    if (e)
+        h_rows<1, NT, PK>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
+    else
+        h_rows<0, NT, PK>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
+    if (!store) return;
+    const long long q = f * nsym + j;
     const int b0 = lane_bin0(t);
     float2 *o = out + q * K;
     const float *Pf = P + f * C;
@@ -462,6 +597,28 @@ hipError_t launch_mrc_td4096(const float2 *iq, long long nframes, int S, int R, 
     auto knob = [](const char *n, int d) { const char *v = getenv(n); return v ? atoi(v) : d; };
     // OFDM_MRC4K_X=1 (default): k_mrc_td4096x, one row read per pair;
     // OFDM_MRC4K_PK=0/7: scalar / packed-f32 (pk.hpp)
+    // OFDM_MRC4K_H=1 (default): k_mrc_td4096h, Hc rows shared by 4 pairs
+    // through LDS (same-process A/B: 10.92 vs 11.15 ms for the x kernel)
+    if (knob("OFDM_MRC4K_H", 1)) {
+        const long long bpf = ((S - 1) + H_PAIRS - 1) / H_PAIRS, nb = nframes * bpf, pxcd = (nb + 7) / 8;
+        if (pxcd * 8 > 0x7fffffffll) return hipErrorInvalidValue;
+        static bool attr = false;  // > 64 KiB of dynamic LDS: opt in once per kernel
+        if (!attr) {
+            for (const void *k : {reinterpret_cast<const void *>(&k_mrc_td4096h<true, 7>),
+                                  reinterpret_cast<const void *>(&k_mrc_td4096h<true, 0>)}) {
+                hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)H_LDS);
+                if (e != hipSuccess) return e;
+            }
+            attr = true;
+        }
+        if (knob("OFDM_MRC4K_PK", 7) == 0)
+            hipLaunchKernelGGL((k_mrc_td4096h<true, 0>), dim3((unsigned)(pxcd * 8)), dim3(128 * H_PAIRS), H_LDS,
+                               s, iq, S, R, prefix, Hc, P, out, nframes, nb, pxcd, mode);
+        else
+            hipLaunchKernelGGL((k_mrc_td4096h<true, 7>), dim3((unsigned)(pxcd * 8)), dim3(128 * H_PAIRS), H_LDS,
+                               s, iq, S, R, prefix, Hc, P, out, nframes, nb, pxcd, mode);
+        return hipGetLastError();
+    }
     if (knob("OFDM_MRC4K_X", 1)) {
         const long long xg = ((nq + 7) / 8) * 8;
         if (xg > 0x7fffffffll) return hipErrorInvalidValue;
@@ -470,7 +627,10 @@ hipError_t launch_mrc_td4096(const float2 *iq, long long nframes, int S, int R, 
 #define OFDM_X_LAUNCH(NTV, PKV)                                                                 \
     hipLaunchKernelGGL((k_mrc_td4096x<NTV, PKV, 2>), dim3((unsigned)xg), dim3(128), X_LDS, s, iq,   \
                        S, R, prefix, Hc, P, out, nq, xg / 8, mode)
-        if (!nt) OFDM_X_LAUNCH(false, 7);
+        if (knob("OFDM_MRC4K_DEBUG", 0) == 2)  // diagnostic only (wrong results): no Hc traffic
+            hipLaunchKernelGGL((k_mrc_td4096x<true, 7, 2, 2>), dim3((unsigned)xg), dim3(128), X_LDS, s, iq, S,
+                               R, prefix, Hc, P, out, nq, xg / 8, mode);
+        else if (!nt) OFDM_X_LAUNCH(false, 7);
         else if (pkm == 0) OFDM_X_LAUNCH(true, 0);
         else OFDM_X_LAUNCH(true, 7);
 #undef OFDM_X_LAUNCH
