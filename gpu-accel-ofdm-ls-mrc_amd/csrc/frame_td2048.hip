@@ -129,7 +129,7 @@ __global__ void __launch_bounds__(256) k_ls_td2048(const float2 *__restrict__ iq
 // ---------------------------------------------------------------------------
 constexpr int MRC_WAVES = 4;
 
-template <bool NT>
+template <bool NT, int DBG = 0>
 __global__ void __attribute__((amdgpu_flat_work_group_size(256, 256), amdgpu_waves_per_eu(2, 2)))
 k_mrc_td2048(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
              const float *__restrict__ P, float2 *__restrict__ out, long long nq, long long nblocks,
@@ -163,6 +163,100 @@ k_mrc_td2048(const float2 *__restrict__ iq, int S, int R, int prefix, const floa
         // matrixMultThenSum (cpuLS.hpp:203-204), antennas in order
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
+            // DBG & 2: diagnostic only (wrong results), no Hc traffic
+            const float4 h = (DBG & 2) ? float4{1.f, (float)k, (float)k, 1.f} : hr[k * 64 + t];
+            ae[k].x = ae[k].x + (xe[k].x * h.x - xe[k].y * h.y);
+            ae[k].y = ae[k].y + (xe[k].x * h.y + xe[k].y * h.x);
+            ao[k].x = ao[k].x + (xo[k].x * h.z - xo[k].y * h.w);
+            ao[k].y = ao[k].y + (xo[k].x * h.w + xo[k].y * h.z);
+        }
+    }
+    const int b0 = lane_bin0(t);
+    float2 *o = out + q * K;
+    if ((mode & 1) == 0) {
+        const float *Pf = P + f * C;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int be = 2 * (b0 + 16 * k);
+            if (be > 0) {
+                const float pv = Pf[be];
+                o[out_pos(be - 1, K)] = float2{ae[k].x / pv, ae[k].y / pv};
+            }
+            const float pv = Pf[be + 1];
+            o[out_pos(be, K)] = float2{ao[k].x / pv, ao[k].y / pv};
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int be = 2 * (b0 + 16 * k);
+            if (be > 0) o[be - 1] = ae[k];
+            o[be] = ao[k];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// MRC with the channel rows shared through LDS (k_mrc_td2048h): 8 waves = 8
+// consecutive data symbols of ONE frame per workgroup (frame-aligned map,
+// bpf = ceil((S-1)/8); tail waves repeat the frame's last symbol without
+// storing).  The frame's 16 KiB Hc row is LDS-DMA'd once per workgroup into a
+// double buffer instead of loaded by every wave from L2 (k_mrc_td2048 without
+// its Hc loads ran 9.5 % faster: OFDM_MRC2K_DEBUG=2).  One barrier per row:
+// after it, row r's Hc is visible and everyone has finished row r-1, whose
+// buffer then receives row r+1.  LDS 16 KiB tables + 8 transpose images +
+// 2 x 16 KiB = 117.5 KiB: one workgroup (2 waves/SIMD, as k_mrc_td2048) per CU.
+// ---------------------------------------------------------------------------
+constexpr int H_WAVES = 8;
+constexpr size_t H_LDS = (size_t)(TAB + H_WAVES * hl::TS + 2 * C) * sizeof(float2);
+static_assert(H_LDS <= 160 * 1024, "one workgroup per CU");
+
+__device__ __forceinline__ void dma_hc_row(const float2 *g, unsigned lds) {  // 16 KiB, 512 threads
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const char *src = reinterpret_cast<const char *>(g) + w * 1024 + lane * 16;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) td1024::dma16(src + j * 8192, lds + j * 8192 + w * 1024);
+}
+
+template <bool NT>
+__global__ void __attribute__((amdgpu_flat_work_group_size(64 * H_WAVES, 64 * H_WAVES),
+                               amdgpu_waves_per_eu(2, 2)))
+k_mrc_td2048h(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
+              const float *__restrict__ P, float2 *__restrict__ out, long long nblocks, long long per_xcd,
+              int mode) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), t = threadIdx.x & 63;
+    float2 *T = lds + TAB + w * hl::TS;
+    float2 *HB = lds + TAB + H_WAVES * hl::TS;  // [2][C]: Hc rows in the float4 lane order
+    const long long pb = blockIdx.x;
+    const long long lb = (pb & 7) * per_xcd + (pb >> 3);  // XCD-grouped: a frame's blocks share an L2
+    if (lb >= nblocks) return;  // whole workgroup
+    const int nsym = S - 1;
+    const long long bpf = (nsym + H_WAVES - 1) / H_WAVES;
+    const long long f = lb / bpf;
+    const int j = (int)(lb - f * bpf) * H_WAVES + w;  // data symbol index within the frame
+    const bool store = j < nsym;
+    const int s = 1 + (store ? j : nsym - 1);
+    const float2 *Hg = Hc + f * (long long)R * C;
+    const unsigned hb[2] = {td1024::lds_addr(HB), td1024::lds_addr(HB + C)};
+    dma_hc_row(Hg, hb[0]);  // row 0; landed at the first row's barrier
+    fill_tables(lds);
+    __syncthreads();
+
+    const int Cp = C + prefix;
+    const float2 *sym = iq + (f * S + s) * (long long)R * Cp + prefix;
+    float2 ae[16], ao[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) ae[k] = ao[k] = float2{0.f, 0.f};
+    for (int r = 0; r < R; ++r) {
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");  // row r's Hc landed everywhere
+        if (r + 1 < R) dma_hc_row(Hg + (long long)(r + 1) * C, hb[(r + 1) & 1]);
+        float2 xe[16], xo[16];
+        row_fft2048<NT>(sym + (long long)r * Cp, t, T, lds, xe, xo);
+        __builtin_amdgcn_sched_barrier(0);
+        const float4 *hr = reinterpret_cast<const float4 *>(HB + (r & 1) * C);
+        // matrixMultThenSum (cpuLS.hpp:203-204), antennas in order
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
             const float4 h = hr[k * 64 + t];
             ae[k].x = ae[k].x + (xe[k].x * h.x - xe[k].y * h.y);
             ae[k].y = ae[k].y + (xe[k].x * h.y + xe[k].y * h.x);
@@ -170,6 +264,8 @@ k_mrc_td2048(const float2 *__restrict__ iq, int S, int R, int prefix, const floa
             ao[k].y = ao[k].y + (xo[k].x * h.w + xo[k].y * h.z);
         }
     }
+    if (!store) return;
+    const long long q = f * nsym + j;
     const int b0 = lane_bin0(t);
     float2 *o = out + q * K;
     if ((mode & 1) == 0) {
@@ -215,7 +311,26 @@ hipError_t launch_mrc_td2048(const float2 *iq, long long nframes, int S, int R, 
     const long long per_xcd = (nblocks + 7) / 8;
     const long long grid = per_xcd * 8;
     if (grid > 0x7fffffffll) return hipErrorInvalidValue;
-    if (getenv("OFDM_MRC_NTLOAD") && getenv("OFDM_MRC_NTLOAD")[0] == '0')
+    const char *hk = getenv("OFDM_MRC2K_H");  // 1: k_mrc_td2048h, Hc rows shared through LDS
+    if (hk && hk[0] == '1') {
+        const long long bpf = ((S - 1) + H_WAVES - 1) / H_WAVES, nb = nframes * bpf, pxcd = (nb + 7) / 8;
+        if (pxcd * 8 > 0x7fffffffll) return hipErrorInvalidValue;
+        static bool attr = false;  // > 64 KiB of dynamic LDS: opt in once
+        if (!attr) {
+            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mrc_td2048h<true>),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)H_LDS);
+            if (e != hipSuccess) return e;
+            attr = true;
+        }
+        hipLaunchKernelGGL((k_mrc_td2048h<true>), dim3((unsigned)(pxcd * 8)), dim3(64 * H_WAVES), H_LDS, s, iq,
+                           S, R, prefix, Hc, P, out, nb, pxcd, mode);
+        return hipGetLastError();
+    }
+    if (getenv("OFDM_MRC2K_DEBUG") && getenv("OFDM_MRC2K_DEBUG")[0] == '2')
+        hipLaunchKernelGGL((k_mrc_td2048<true, 2>), dim3((unsigned)grid), dim3(64 * MRC_WAVES),
+                           lds_bytes(MRC_WAVES), s, iq, S, R, prefix, Hc, P, out, nq, nblocks, per_xcd,
+                           mode);
+    else if (getenv("OFDM_MRC_NTLOAD") && getenv("OFDM_MRC_NTLOAD")[0] == '0')
         hipLaunchKernelGGL((k_mrc_td2048<false>), dim3((unsigned)grid), dim3(64 * MRC_WAVES),
                            lds_bytes(MRC_WAVES), s, iq, S, R, prefix, Hc, P, out, nq, nblocks, per_xcd,
                            mode);

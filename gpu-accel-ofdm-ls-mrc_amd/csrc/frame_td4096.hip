@@ -273,20 +273,9 @@ __device__ __forceinline__ pk::v2f dif_tw(pk::v2f base) {  // base * W64^(CM * M
     return pk::cmul_s_v(base, (pk::v2f){w.x, w.y});
 }
 
-typedef __attribute__((address_space(3))) void lvoid_t;
-__device__ __forceinline__ unsigned lds_addr(const void *p) { return (unsigned)(size_t)(lvoid_t *)p; }
+using td1024::dma16;
+using td1024::lds_addr;
 
-// 16 B per lane straight into LDS at byte lds + 16 lane (global_load_lds_dwordx4
-// in inline asm: the builtin makes the compiler wait vmcnt(0) before every LDS
-// read; M0 saved/restored in the same statement, s_nop for the M0 hazard).
-__device__ __forceinline__ void dma16(const void *g, unsigned lds) {
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
-                 "s_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(g), "s"(lds)
-                 : "memory");
-}
 // One 32 KiB Hc row (4096 float2) into LDS by a 512-thread workgroup: four
 // wave-instructions of 1 KiB per wave, natural order.
 __device__ __forceinline__ void dma_hc_row(const float2 *g, unsigned lds) {

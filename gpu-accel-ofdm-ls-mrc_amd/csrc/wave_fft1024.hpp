@@ -42,6 +42,21 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+typedef __attribute__((address_space(3))) void lvoid_t;
+__device__ __forceinline__ unsigned lds_addr(const void *p) { return (unsigned)(size_t)(lvoid_t *)p; }
+
+// 16 B per lane straight into LDS at byte lds + 16 lane (global_load_lds_dwordx4
+// in inline asm: the builtin makes the compiler wait vmcnt(0) before every LDS
+// read; M0 saved/restored in the same statement, s_nop for the M0 hazard).
+__device__ __forceinline__ void dma16(const void *g, unsigned lds) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(g), "s"(lds)
+                 : "memory");
+}
+
 // Quad-DFT signs (found by exhaustive search, verified in tests): lane a of a
 // quad pre-scales its B_a by g(a) (folded into TW2) so that both radix-2
 // stages are one fma(dpp(x), S, x) per float with exact results:
