@@ -62,6 +62,53 @@ __device__ __forceinline__ void row_fft2048(const float2 *__restrict__ src, int 
     hl::row_fft_b(t, T, tw2, xo);
 }
 
+// Same FFT with the row already in registers (lo = x[n], hi = x[n + 1024]),
+// the DIF split done in place.  PREF: the next row is loaded into lo (hi) as
+// soon as the first (second) half-FFT has written it to the transpose image,
+// so it is in flight during the rest of this row.
+// Each half is combined as soon as it is transformed (ae += X[2 b] Hc[2 b],
+// ao += X[2 b + 1] Hc[2 b + 1], Hc row hr in LDS, float4 lane order), so only
+// one half's bins are live at a time.
+template <bool NOHC = false>
+__device__ __forceinline__ void mac_half(const float2 *hr, int e, int t, const float2 (&x)[16],
+                                         float2 (&acc)[16]) {
+    // matrixMultThenSum (cpuLS.hpp:203-204), antennas in order
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        // NOHC: diagnostic only (wrong results), no Hc reads
+        const float2 h = NOHC ? float2{1.f, (float)k} : hr[2 * (k * 64 + t) + e];
+        acc[k].x = acc[k].x + (x[k].x * h.x - x[k].y * h.y);
+        acc[k].y = acc[k].y + (x[k].x * h.y + x[k].y * h.x);
+    }
+}
+
+// TWC: no W2048^n table in LDS; W2048^(t + 64 m) = W2048^t W32^m is formed
+// from the lane's W2048^t (wt) and the wave-uniform W32^m (scalar loads).
+template <bool NT, bool PREF, bool NOHC = false, bool TWC = false>
+__device__ __forceinline__ void row_fft2048_pf(const float2 *__restrict__ next, int t, float2 *T,
+                                               const float2 *lds, float2 (&lo)[16], float2 (&hi)[16],
+                                               const float2 *hr, float2 (&ae)[16], float2 (&ao)[16],
+                                               float2 wt = float2{1.f, 0.f}) {
+    float2 x[16];
+    const float2 *tw1 = lds, *tw2 = lds + hl::TW1S, *twv = lds + hl::TW1S + hl::TW2S;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        const float2 d = csub(lo[m], hi[m]);
+        lo[m] = cadd(lo[m], hi[m]);
+        hi[m] = cmul(d, TWC ? cmul(wt, g_tw[64 * m * (OFDM_TW_N / C)]) : twv[m * 64 + t]);
+    }
+    hl::row_fft_a(lo, t, T, tw1);
+    __builtin_amdgcn_sched_barrier(0);
+    if (PREF) row_load<NT>(next, t, lo);
+    hl::row_fft_b(t, T, tw2, x);
+    mac_half<NOHC>(hr, 0, t, x, ae);
+    hl::row_fft_a(hi, t, T, tw1);
+    __builtin_amdgcn_sched_barrier(0);
+    if (PREF) row_load<NT>(next + HALF, t, hi);
+    hl::row_fft_b(t, T, tw2, x);
+    mac_half<NOHC>(hr, 1, t, x, ao);
+}
+
 // ---------------------------------------------------------------------------
 // LS: one workgroup (4 waves) per frame, wave w takes antenna rows w, w+4, ...
 // Pilots (K values) in LDS; partial |H|^2 per wave combined in wave order.
@@ -155,7 +202,17 @@ k_mrc_td2048(const float2 *__restrict__ iq, int S, int R, int prefix, const floa
     float2 ae[16], ao[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) ae[k] = ao[k] = float2{0.f, 0.f};
-    for (int r = 0; r < R; ++r) {
+    if constexpr ((DBG & 4) != 0) {
+        // diagnostic only (wrong results): the row prefetch of k_mrc_td2048h
+        // without any Hc reads -- bounds what a prefetching kernel could gain
+        float2 lo[16], hi[16];
+        row_load<NT>(sym, t, lo);
+        row_load<NT>(sym + HALF, t, hi);
+        for (int r = 0; r < R; ++r)
+            row_fft2048_pf<NT, true, true>(sym + (long long)(r + 1 < R ? r + 1 : r) * Cp, t, T, lds, lo, hi,
+                                           nullptr, ae, ao);
+    }
+    for (int r = 0; r < ((DBG & 4) ? 0 : R); ++r) {
         float2 xe[16], xo[16];
         row_fft2048<NT>(sym + (long long)r * Cp, t, T, lds, xe, xo);
         __builtin_amdgcn_sched_barrier(0);
@@ -206,50 +263,74 @@ k_mrc_td2048(const float2 *__restrict__ iq, int S, int R, int prefix, const floa
 // buffer then receives row r+1.  LDS 16 KiB tables + 8 transpose images +
 // 2 x 16 KiB = 117.5 KiB: one workgroup (2 waves/SIMD, as k_mrc_td2048) per CU.
 // ---------------------------------------------------------------------------
+// HW = 4 (two workgroups per CU, each in its own lockstep) drops the 8 KiB
+// W2048^n table (TWC) so that 2 x (8 + 4 x 8.5 + 32) KiB fit.
+template <int HW>
+struct HLay {
+    static constexpr bool TWC = HW < 8;
+    static constexpr int TABH = TWC ? hl::TW1S + hl::TW2S : TAB;
+    static constexpr size_t LDS = (size_t)(TABH + HW * hl::TS + 2 * C) * sizeof(float2);
+    static_assert(LDS * (8 / HW) <= 160 * 1024, "8 waves per CU");
+};
 constexpr int H_WAVES = 8;
-constexpr size_t H_LDS = (size_t)(TAB + H_WAVES * hl::TS + 2 * C) * sizeof(float2);
-static_assert(H_LDS <= 160 * 1024, "one workgroup per CU");
 
-__device__ __forceinline__ void dma_hc_row(const float2 *g, unsigned lds) {  // 16 KiB, 512 threads
+template <int HW>
+__device__ __forceinline__ void dma_hc_row(const float2 *g, unsigned lds) {  // 16 KiB, 64 HW threads
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const char *src = reinterpret_cast<const char *>(g) + w * 1024 + lane * 16;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) td1024::dma16(src + j * 8192, lds + j * 8192 + w * 1024);
+    for (int j = 0; j < 16 / HW; ++j) td1024::dma16(src + j * HW * 1024, lds + j * HW * 1024 + w * 1024);
 }
 
-template <bool NT>
-__global__ void __attribute__((amdgpu_flat_work_group_size(64 * H_WAVES, 64 * H_WAVES),
-                               amdgpu_waves_per_eu(2, 2)))
+template <bool NT, bool PF, int HW = H_WAVES>
+__global__ void __attribute__((amdgpu_flat_work_group_size(64 * HW, 64 * HW), amdgpu_waves_per_eu(2, 2)))
 k_mrc_td2048h(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
               const float *__restrict__ P, float2 *__restrict__ out, long long nblocks, long long per_xcd,
               int mode) {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), t = threadIdx.x & 63;
-    float2 *T = lds + TAB + w * hl::TS;
-    float2 *HB = lds + TAB + H_WAVES * hl::TS;  // [2][C]: Hc rows in the float4 lane order
+    using L = HLay<HW>;
+    static_assert(PF || !L::TWC, "the table-free twiddles are in the prefetching row loop only");
+    float2 *T = lds + L::TABH + w * hl::TS;
+    float2 *HB = lds + L::TABH + HW * hl::TS;  // [2][C]: Hc rows in the float4 lane order
     const long long pb = blockIdx.x;
     const long long lb = (pb & 7) * per_xcd + (pb >> 3);  // XCD-grouped: a frame's blocks share an L2
     if (lb >= nblocks) return;  // whole workgroup
     const int nsym = S - 1;
-    const long long bpf = (nsym + H_WAVES - 1) / H_WAVES;
+    const long long bpf = (nsym + HW - 1) / HW;
     const long long f = lb / bpf;
-    const int j = (int)(lb - f * bpf) * H_WAVES + w;  // data symbol index within the frame
+    const int j = (int)(lb - f * bpf) * HW + w;  // data symbol index within the frame
     const bool store = j < nsym;
     const int s = 1 + (store ? j : nsym - 1);
     const float2 *Hg = Hc + f * (long long)R * C;
     const unsigned hb[2] = {td1024::lds_addr(HB), td1024::lds_addr(HB + C)};
-    dma_hc_row(Hg, hb[0]);  // row 0; landed at the first row's barrier
-    fill_tables(lds);
+    dma_hc_row<HW>(Hg, hb[0]);  // row 0; landed at the first row's barrier
+    if (L::TWC) hl::fill(lds, lds + hl::TW1S);
+    else fill_tables(lds);
     __syncthreads();
+    const float2 wt = g_tw[t * (OFDM_TW_N / C)];  // TWC: W2048^t
 
     const int Cp = C + prefix;
     const float2 *sym = iq + (f * S + s) * (long long)R * Cp + prefix;
-    float2 ae[16], ao[16];
+    float2 ae[16], ao[16], lo[16], hi[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) ae[k] = ao[k] = float2{0.f, 0.f};
+    if (PF) {
+        row_load<NT>(sym, t, lo);
+        row_load<NT>(sym + HALF, t, hi);
+    }
     for (int r = 0; r < R; ++r) {
-        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");  // row r's Hc landed everywhere
-        if (r + 1 < R) dma_hc_row(Hg + (long long)(r + 1) * C, hb[(r + 1) & 1]);
+        // row r's Hc (and, PF, its IQ) landed everywhere; everyone is done with row r-1's buffer
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        if (r + 1 < R) dma_hc_row<HW>(Hg + (long long)(r + 1) * C, hb[(r + 1) & 1]);
+        if (PF) {
+            const float2 *h2 = HB + (r & 1) * C;
+            // the last row re-loads itself (one row in R) rather than branching:
+            // two copies of the loop body would not fit the register budget
+            row_fft2048_pf<NT, true, false, L::TWC>(sym + (long long)(r + 1 < R ? r + 1 : r) * Cp, t, T, lds,
+                                                    lo, hi, h2, ae, ao, wt);
+            continue;
+        }
         float2 xe[16], xo[16];
         row_fft2048<NT>(sym + (long long)r * Cp, t, T, lds, xe, xo);
         __builtin_amdgcn_sched_barrier(0);
@@ -311,22 +392,40 @@ hipError_t launch_mrc_td2048(const float2 *iq, long long nframes, int S, int R, 
     const long long per_xcd = (nblocks + 7) / 8;
     const long long grid = per_xcd * 8;
     if (grid > 0x7fffffffll) return hipErrorInvalidValue;
-    const char *hk = getenv("OFDM_MRC2K_H");  // 1: k_mrc_td2048h, Hc rows shared through LDS
-    if (hk && hk[0] == '1') {
-        const long long bpf = ((S - 1) + H_WAVES - 1) / H_WAVES, nb = nframes * bpf, pxcd = (nb + 7) / 8;
+    // OFDM_MRC2K_H: k_mrc_td2048h, Hc rows shared through LDS.  1: 8 waves;
+    // 2: 8 waves + the next IQ row prefetched; 4: 2 x 4 waves per CU + prefetch
+    const char *hk = getenv("OFDM_MRC2K_H");
+    const int hv = hk ? hk[0] - '0' : 0;
+    if (hv == 1 || hv == 2 || hv == 4) {
+        const int hw = hv == 4 ? 4 : H_WAVES;
+        const long long bpf = ((S - 1) + hw - 1) / hw, nb = nframes * bpf, pxcd = (nb + 7) / 8;
         if (pxcd * 8 > 0x7fffffffll) return hipErrorInvalidValue;
-        static bool attr = false;  // > 64 KiB of dynamic LDS: opt in once
-        if (!attr) {
-            hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&k_mrc_td2048h<true>),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)H_LDS);
+        const void *kf = hv == 1   ? reinterpret_cast<const void *>(&k_mrc_td2048h<true, false>)
+                         : hv == 2 ? reinterpret_cast<const void *>(&k_mrc_td2048h<true, true>)
+                                   : reinterpret_cast<const void *>(&k_mrc_td2048h<true, true, 4>);
+        const size_t lb = hv == 4 ? HLay<4>::LDS : HLay<H_WAVES>::LDS;
+        static bool attr[5] = {false, false, false, false, false};  // > 64 KiB of dynamic LDS: opt in once
+        if (!attr[hv]) {
+            hipError_t e = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb);
             if (e != hipSuccess) return e;
-            attr = true;
+            attr[hv] = true;
         }
-        hipLaunchKernelGGL((k_mrc_td2048h<true>), dim3((unsigned)(pxcd * 8)), dim3(64 * H_WAVES), H_LDS, s, iq,
-                           S, R, prefix, Hc, P, out, nb, pxcd, mode);
+        if (hv == 1)
+            hipLaunchKernelGGL((k_mrc_td2048h<true, false>), dim3((unsigned)(pxcd * 8)), dim3(64 * hw), lb, s, iq,
+                               S, R, prefix, Hc, P, out, nb, pxcd, mode);
+        else if (hv == 2)
+            hipLaunchKernelGGL((k_mrc_td2048h<true, true>), dim3((unsigned)(pxcd * 8)), dim3(64 * hw), lb, s, iq,
+                               S, R, prefix, Hc, P, out, nb, pxcd, mode);
+        else
+            hipLaunchKernelGGL((k_mrc_td2048h<true, true, 4>), dim3((unsigned)(pxcd * 8)), dim3(64 * hw), lb, s,
+                               iq, S, R, prefix, Hc, P, out, nb, pxcd, mode);
         return hipGetLastError();
     }
-    if (getenv("OFDM_MRC2K_DEBUG") && getenv("OFDM_MRC2K_DEBUG")[0] == '2')
+    if (getenv("OFDM_MRC2K_DEBUG") && getenv("OFDM_MRC2K_DEBUG")[0] == '6')
+        hipLaunchKernelGGL((k_mrc_td2048<true, 6>), dim3((unsigned)grid), dim3(64 * MRC_WAVES),
+                           lds_bytes(MRC_WAVES), s, iq, S, R, prefix, Hc, P, out, nq, nblocks, per_xcd,
+                           mode);
+    else if (getenv("OFDM_MRC2K_DEBUG") && getenv("OFDM_MRC2K_DEBUG")[0] == '2')
         hipLaunchKernelGGL((k_mrc_td2048<true, 2>), dim3((unsigned)grid), dim3(64 * MRC_WAVES),
                            lds_bytes(MRC_WAVES), s, iq, S, R, prefix, Hc, P, out, nq, nblocks, per_xcd,
                            mode);
