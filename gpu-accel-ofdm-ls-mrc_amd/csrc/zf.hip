@@ -21,9 +21,11 @@
 //     and store is one coalesced 512 B wave access); each wave accumulates an
 //     MT x ST (rows x symbols) register tile, so per n it loads MT + ST values
 //     for MT * ST complex MACs.  At U = 16, R = 64 the work is ~13 flop per HBM
-//     byte, under the FP32 ridge (~20): HBM-bound.  MFMA is not used: the f32
-//     matrix peak of gfx950 equals its f32 vector peak (MI355X_MICROARCH.md),
-//     so v_mfma_f32_16x16x4f32 would only add the complex-to-real expansion.
+//     byte, under the FP32 ridge (~20): HBM-bound on paper (at U = 32, 26
+//     flop/B, compute-bound).  The f32 matrix peak of gfx950 equals its f32
+//     vector peak (MI355X_MICROARCH.md); k_zf_mfma / k_zf_mfma_lds below put
+//     the MACs on the matrix cores anyway (16-block 4x4x1 MFMA, one block per
+//     subcarrier) and win only for detect at U >= 32.
 //     The W tile of a (subcarrier block, row block) is re-read for every symbol
 //     step; block ids are mapped so that all workgroups of one XCD share the
 //     same few tiles (dispatch is round-robin over the 8 XCDs), keeping those
@@ -471,6 +473,295 @@ __global__ void __launch_bounds__(256) k_zf_gemm_dma(const float2 *__restrict__ 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the tail re-loads before exit
 }
 
+// The same GEMM on the matrix cores (k_zf_mfma): v_mfma_f32_4x4x1_16b_f32
+// runs 16 INDEPENDENT 4 x 4 x 1 outer products per instruction, one per
+// 4-lane block, at the full f32 matrix rate (64 flop/clk/SIMD, the f32 vector
+// peak, MI355X_MICROARCH.md) -- so each block is one subcarrier and the
+// subcarrier-fastest layouts need no transposition: lane l = 4 b + i works on
+// subcarrier k0 + b.  Complex -> real: the 4 rows of a block are
+// (re m, im m, re m+1, im m+1), its 4 columns 4 symbols; per complex n two
+// MFMAs with the real k-steps Xr and Xi:
+//   A(re step) = (Ar, Ai, Ar', Ai'),  A(im step) = (-Ai, Ar, -Ai', Ar')
+// (Ai -> -Ai for CONJ), B = Xr or Xi of the lane's symbol.  Lane (b, i) loads
+// W(m0 + 2p + i/2, n) and picks its component with one select per step; lane
+// (b, j) loads x[s0 + 4g + j][n][k0 + b].  D(row i, col j) of block b sits in
+// accumulator register i of lane 4 b + j: lane (b, j) stores two float2.
+// Each wave owns MP row pairs x SG symbol quads of 16 subcarriers; the 4 waves
+// of a workgroup take consecutive symbol quads of the same W tile (shared in
+// L1); operands of n+1 are loaded before the MFMAs of n.  f32 MFMA
+// accumulation is an exact f32 fma chain (MI355X_MICROARCH.md).
+typedef float mf4 __attribute__((ext_vector_type(4)));
+
+template <int MP, int SG, bool CONJ>
+__global__ void __launch_bounds__(256) k_zf_mfma(const float2 *__restrict__ Wt, int a_m, int a_n,
+                                                 const float2 *__restrict__ in, int N, int M, int K,
+                                                 long long nsym, float2 *__restrict__ out, int ntile, int tpx,
+                                                 int nkb, long long chunk_steps) {
+    constexpr int SW = 4 * SG, SBLK = 4 * SW;  // symbols per wave / per workgroup step
+    const int bid = blockIdx.x, xcd = bid & 7, jb = bid >> 3;  // XCD-aware mapping as k_zf_gemm
+    const int tile = xcd + 8 * (jb % tpx);
+    if (tile >= ntile) return;
+    const long long chunk = jb / tpx;
+    const int kb = tile % nkb, mb = tile / nkb;
+    const int lane = threadIdx.x & 63, b = lane >> 2, i = lane & 3;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int k = kb * 16 + b, kc = min(k, K - 1);  // lanes past K compute on a valid bin, never store
+    const int m0 = mb * 2 * MP;
+    const long long nsteps_total = (nsym + SBLK - 1) / SBLK;
+    const long long step0 = chunk * chunk_steps, step1 = min(step0 + chunk_steps, nsteps_total);
+    const bool odd = i & 1;
+
+    // W rows of this lane (clamped: rows past M compute, never store)
+    const float2 *wrow[MP];
+#pragma unroll
+    for (int p = 0; p < MP; ++p)
+        wrow[p] = Wt + (long long)min(m0 + 2 * p + (i >> 1), M - 1) * a_m * K + kc;
+    const long long anK = (long long)a_n * K, NK = (long long)N * K;
+
+    for (long long st = step0; st < step1; ++st) {
+        const long long s0 = st * SBLK + w * SW;
+        if (s0 >= nsym) break;  // wave-uniform; no barriers in this kernel
+        const float2 *xrow[SG];
+#pragma unroll
+        for (int g = 0; g < SG; ++g) xrow[g] = in + min(s0 + 4 * g + i, nsym - 1) * NK + kc;
+        mf4 acc[MP][SG];
+#pragma unroll
+        for (int p = 0; p < MP; ++p)
+#pragma unroll
+            for (int g = 0; g < SG; ++g) acc[p][g] = mf4{0.f, 0.f, 0.f, 0.f};
+        float2 wv[MP], xv[SG];
+#pragma unroll
+        for (int p = 0; p < MP; ++p) wv[p] = wrow[p][0];
+#pragma unroll
+        for (int g = 0; g < SG; ++g) xv[g] = xrow[g][0];
+        for (int n = 0; n < N; ++n) {
+            const int nn = min(n + 1, N - 1);  // the last one is a redundant reload
+            float2 wn[MP], xn[SG];
+#pragma unroll
+            for (int p = 0; p < MP; ++p) wn[p] = wrow[p][nn * anK];
+#pragma unroll
+            for (int g = 0; g < SG; ++g) xn[g] = xrow[g][nn * (long long)K];
+            float are[MP], aim[MP];
+#pragma unroll
+            for (int p = 0; p < MP; ++p) {
+                const float wy = CONJ ? -wv[p].y : wv[p].y;
+                are[p] = odd ? wy : wv[p].x;
+                aim[p] = odd ? wv[p].x : -wy;
+            }
+#pragma unroll
+            for (int p = 0; p < MP; ++p)
+#pragma unroll
+                for (int g = 0; g < SG; ++g)
+                    acc[p][g] = __builtin_amdgcn_mfma_f32_4x4x1f32(are[p], xv[g].x, acc[p][g], 0, 0, 0);
+#pragma unroll
+            for (int p = 0; p < MP; ++p)
+#pragma unroll
+                for (int g = 0; g < SG; ++g)
+                    acc[p][g] = __builtin_amdgcn_mfma_f32_4x4x1f32(aim[p], xv[g].y, acc[p][g], 0, 0, 0);
+#pragma unroll
+            for (int p = 0; p < MP; ++p) wv[p] = wn[p];
+#pragma unroll
+            for (int g = 0; g < SG; ++g) xv[g] = xn[g];
+        }
+        if (k < K) {
+#pragma unroll
+            for (int g = 0; g < SG; ++g) {
+                const long long s = s0 + 4 * g + i;  // this lane's column j = i
+                if (s >= nsym) break;
+                float2 *o = out + s * M * (long long)K + k;
+#pragma unroll
+                for (int p = 0; p < MP; ++p) {
+                    const int m = m0 + 2 * p;
+                    if (m < M) o[(long long)m * K] = float2{acc[p][g][0], acc[p][g][1]};
+                    if (m + 1 < M) o[(long long)(m + 1) * K] = float2{acc[p][g][2], acc[p][g][3]};
+                }
+            }
+        }
+    }
+}
+
+// k_zf_mfma fed through LDS (k_zf_mfma_lds): the workgroup DMA's each n-step's
+// operand rows -- MB = 16 rows of A and SB = 4 SG symbols of the input, 64
+// subcarriers (512 B) each, coalesced -- into one of NB LDS buffers
+// (global_load_lds_dword, as k_zf_gemm_dma: three steps in flight, one
+// barrier per step, no VGPR staging), and wave w runs the MFMAs of
+// subcarriers 16 w .. 16 w + 15 of the block, reading its operands from LDS.
+// The 16 dword DMAs of one step of k_zf_mfma_lds<4> (8 rows x 2 halves, row r
+// at LDS byte lds + 2048 r, half h at + 256 h) in one statement: M0 is saved
+// and restored once per step instead of once per load.
+__device__ __forceinline__ void dma_rows8(const float *const (&g)[16], unsigned lds) {
+    const unsigned l0 = lds + 0u;
+    const unsigned l1 = lds + 256u;
+    const unsigned l2 = lds + 2048u;
+    const unsigned l3 = lds + 2304u;
+    const unsigned l4 = lds + 4096u;
+    const unsigned l5 = lds + 4352u;
+    const unsigned l6 = lds + 6144u;
+    const unsigned l7 = lds + 6400u;
+    const unsigned l8 = lds + 8192u;
+    const unsigned l9 = lds + 8448u;
+    const unsigned l10 = lds + 10240u;
+    const unsigned l11 = lds + 10496u;
+    const unsigned l12 = lds + 12288u;
+    const unsigned l13 = lds + 12544u;
+    const unsigned l14 = lds + 14336u;
+    const unsigned l15 = lds + 14592u;
+    unsigned keep;
+    asm volatile("s_mov_b32 %[keep], m0\n\t"
+                 "s_mov_b32 m0, %[l0]\n\ts_nop 0\n\tglobal_load_lds_dword %[a0], off\n\t"
+                 "s_mov_b32 m0, %[l1]\n\ts_nop 0\n\tglobal_load_lds_dword %[a1], off\n\t"
+                 "s_mov_b32 m0, %[l2]\n\ts_nop 0\n\tglobal_load_lds_dword %[a2], off\n\t"
+                 "s_mov_b32 m0, %[l3]\n\ts_nop 0\n\tglobal_load_lds_dword %[a3], off\n\t"
+                 "s_mov_b32 m0, %[l4]\n\ts_nop 0\n\tglobal_load_lds_dword %[a4], off\n\t"
+                 "s_mov_b32 m0, %[l5]\n\ts_nop 0\n\tglobal_load_lds_dword %[a5], off\n\t"
+                 "s_mov_b32 m0, %[l6]\n\ts_nop 0\n\tglobal_load_lds_dword %[a6], off\n\t"
+                 "s_mov_b32 m0, %[l7]\n\ts_nop 0\n\tglobal_load_lds_dword %[a7], off\n\t"
+                 "s_mov_b32 m0, %[l8]\n\ts_nop 0\n\tglobal_load_lds_dword %[a8], off\n\t"
+                 "s_mov_b32 m0, %[l9]\n\ts_nop 0\n\tglobal_load_lds_dword %[a9], off\n\t"
+                 "s_mov_b32 m0, %[l10]\n\ts_nop 0\n\tglobal_load_lds_dword %[a10], off\n\t"
+                 "s_mov_b32 m0, %[l11]\n\ts_nop 0\n\tglobal_load_lds_dword %[a11], off\n\t"
+                 "s_mov_b32 m0, %[l12]\n\ts_nop 0\n\tglobal_load_lds_dword %[a12], off\n\t"
+                 "s_mov_b32 m0, %[l13]\n\ts_nop 0\n\tglobal_load_lds_dword %[a13], off\n\t"
+                 "s_mov_b32 m0, %[l14]\n\ts_nop 0\n\tglobal_load_lds_dword %[a14], off\n\t"
+                 "s_mov_b32 m0, %[l15]\n\ts_nop 0\n\tglobal_load_lds_dword %[a15], off\n\t"
+                 "s_mov_b32 m0, %[keep]"
+                 : [keep] "=&s"(keep)
+                 : [a0] "v"(g[0]), [a1] "v"(g[1]), [a2] "v"(g[2]), [a3] "v"(g[3]), [a4] "v"(g[4]), [a5] "v"(g[5]), [a6] "v"(g[6]), [a7] "v"(g[7]), [a8] "v"(g[8]), [a9] "v"(g[9]), [a10] "v"(g[10]), [a11] "v"(g[11]), [a12] "v"(g[12]), [a13] "v"(g[13]), [a14] "v"(g[14]), [a15] "v"(g[15]),
+                   [l0] "s"(l0), [l1] "s"(l1), [l2] "s"(l2), [l3] "s"(l3), [l4] "s"(l4), [l5] "s"(l5), [l6] "s"(l6), [l7] "s"(l7), [l8] "s"(l8), [l9] "s"(l9), [l10] "s"(l10), [l11] "s"(l11), [l12] "s"(l12), [l13] "s"(l13), [l14] "s"(l14), [l15] "s"(l15)
+                 : "memory");
+}
+
+template <int SG, bool CONJ>
+__global__ void __attribute__((amdgpu_flat_work_group_size(256, 256), amdgpu_waves_per_eu(SG == 4 ? 2 : 1)))
+k_zf_mfma_lds(const float2 *__restrict__ Wt, int a_m, int a_n,
+                                                     const float2 *__restrict__ in, int N, int M, int K,
+                                                     long long nsym, float2 *__restrict__ out, int ntile, int tpx,
+                                                     int nkb, long long chunk_steps) {
+    constexpr int MP = 8, MB = 2 * MP, SB = 4 * SG, NB = 4;
+    constexpr int ROWS = MB + SB, RPW = ROWS / 4, WR = MB / 4, LPW = 2 * RPW;
+    static_assert(ROWS % 4 == 0 && MB % 4 == 0 && (NB - 2) * LPW <= 63, "rows per wave / vmcnt range");
+    extern __shared__ __attribute__((aligned(16))) float2 smd[];  // [NB][ROWS][64]
+    const int bid = blockIdx.x, xcd = bid & 7, jb = bid >> 3;    // XCD-aware mapping as k_zf_gemm
+    const int tile = xcd + 8 * (jb % tpx);
+    if (tile >= ntile) return;  // whole workgroup
+    const long long chunk = jb / tpx;
+    const int kb = tile % nkb, mb = tile / nkb;
+    const int lane = threadIdx.x & 63, b = lane >> 2, i = lane & 3;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int k = kb * 64 + 16 * w + b;
+    const int mb0 = mb * MB;
+    const long long nsteps_total = (nsym + SB - 1) / SB;
+    const long long step0 = chunk * chunk_steps, step1 = min(step0 + chunk_steps, nsteps_total);
+    if (step1 <= step0) return;  // whole workgroup
+    const int nst = (int)(step1 - step0);
+    // this lane's dword of each 256-B half row (clamped past K: computed, never stored)
+    const int off0 = min(kb * 64 + (lane >> 1), K - 1) * 2 + (lane & 1);
+    const int off1 = min(kb * 64 + 32 + (lane >> 1), K - 1) * 2 + (lane & 1);
+    const bool odd = i & 1;
+    const long long anK = (long long)a_n * K, NK = (long long)N * K;
+
+    // DMA issue position (step si, n ni, buffer bi); row bases are wave-uniform
+    int si = 0, ni = 0, bi = 0;
+    const float *wbase[WR];
+#pragma unroll
+    for (int r = 0; r < WR; ++r)
+        wbase[r] = reinterpret_cast<const float *>(Wt + (long long)min(mb0 + w + 4 * r, M - 1) * a_m * K);
+    const unsigned lds0 = (unsigned)(size_t)(lvoid_t *)smd + (unsigned)(w * 512);
+    auto issue = [&]() {
+        const unsigned la = lds0 + (unsigned)(bi * ROWS * 512);
+        const long long s0 = (step0 + si) * SB;
+        const float *ga[2 * RPW];
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) {
+            const float *src;
+            if (r < WR) {
+                src = wbase[r] + 2 * (ni * anK);
+            } else {
+                const long long s = min(s0 + (w + 4 * r - MB), nsym - 1);
+                src = reinterpret_cast<const float *>(in + s * NK + (long long)ni * K);
+            }
+            if constexpr (RPW == 8) {
+                ga[2 * r] = src + off0;
+                ga[2 * r + 1] = src + off1;
+            } else {
+                dma_dword(src + off0, la + r * 2048);
+                dma_dword(src + off1, la + r * 2048 + 256);
+            }
+        }
+        if constexpr (RPW == 8) dma_rows8(ga, la);
+        // advance (the tail re-issues the last step: valid addresses, never read)
+        if (si < nst - 1 || ni < N - 1) {
+            if (++ni == N) {
+                ni = 0;
+                ++si;
+            }
+        }
+        bi = (bi + 1) & (NB - 1);
+    };
+
+    mf4 acc[MP][SG];
+#pragma unroll
+    for (int p = 0; p < MP; ++p)
+#pragma unroll
+        for (int g = 0; g < SG; ++g) acc[p][g] = mf4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int p = 0; p < NB - 1; ++p) issue();
+    int bc = 0;  // buffer of the step being computed
+    for (int st = 0; st < nst; ++st) {
+        for (int n = 0; n < N; ++n) {
+            asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((NB - 2) * LPW) : "memory");
+            if (SG == 4) issue();  // into the buffer of the previous step, which everyone has finished
+            const float2 *sb = smd + bc * ROWS * 64 + 16 * w + b;
+            bc = (bc + 1) & (NB - 1);
+            float are[MP], aim[MP];
+#pragma unroll
+            for (int p = 0; p < MP; ++p) {
+                const float2 wv = sb[(2 * p + (i >> 1)) * 64];
+                const float wy = CONJ ? -wv.y : wv.y;
+                are[p] = odd ? wy : wv.x;
+                aim[p] = odd ? wv.x : -wy;
+            }
+            float2 xv[SG];
+#pragma unroll
+            for (int g = 0; g < SG; ++g) xv[g] = sb[(MB + 4 * g + i) * 64];
+#pragma unroll
+            for (int p = 0; p < MP; ++p)
+#pragma unroll
+                for (int g = 0; g < SG; ++g)
+                    acc[p][g] = __builtin_amdgcn_mfma_f32_4x4x1f32(are[p], xv[g].x, acc[p][g], 0, 0, 0);
+            // SG = 8 (one wave per SIMD): the DMA issue runs in the shadow of
+            // the re-step MFMAs instead of in front of them
+            if (SG == 8) issue();
+#pragma unroll
+            for (int p = 0; p < MP; ++p)
+#pragma unroll
+                for (int g = 0; g < SG; ++g)
+                    acc[p][g] = __builtin_amdgcn_mfma_f32_4x4x1f32(aim[p], xv[g].y, acc[p][g], 0, 0, 0);
+        }
+        // store this step's tile and reset
+        const long long s0 = (step0 + st) * SB;
+        if (k < K) {
+#pragma unroll
+            for (int g = 0; g < SG; ++g) {
+                const long long s = s0 + 4 * g + i;
+                if (s >= nsym) break;
+                float2 *o = out + s * M * (long long)K + k;
+#pragma unroll
+                for (int p = 0; p < MP; ++p) {
+                    const int m = mb0 + 2 * p;
+                    if (m < M) o[(long long)m * K] = float2{acc[p][g][0], acc[p][g][1]};
+                    if (m + 1 < M) o[(long long)(m + 1) * K] = float2{acc[p][g][2], acc[p][g][3]};
+                }
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < MP; ++p)
+#pragma unroll
+            for (int g = 0; g < SG; ++g) acc[p][g] = mf4{0.f, 0.f, 0.f, 0.f};
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the tail re-loads before exit
+}
+
 }  // namespace zf
 
 size_t zf_precoder_lds_bytes(int U, int R) {
@@ -562,9 +853,77 @@ hipError_t gemm_lds_launch(const float2 *Wt, int a_m, int a_n, const float2 *in,
     return hipGetLastError();
 }
 
+template <int MP, int SG, bool CONJ>
+hipError_t mfma_launch(const float2 *Wt, int a_m, int a_n, const float2 *in, int N, int M, int K,
+                       long long nsym, float2 *out, hipStream_t s) {
+    constexpr int SBLK = 16 * SG;
+    const int nkb = (K + 15) / 16, nmb = (M + 2 * MP - 1) / (2 * MP);
+    const int ntile = nkb * nmb, tpx = (ntile + 7) / 8;
+    const long long nsteps = (nsym + SBLK - 1) / SBLK;
+    long long nchunk = (2048 + 8LL * tpx - 1) / (8LL * tpx);
+    long long chunk_steps = (nsteps + nchunk - 1) / nchunk;
+    if (chunk_steps < 2) chunk_steps = 2;
+    nchunk = (nsteps + chunk_steps - 1) / chunk_steps;
+    const long long blocks = 8LL * tpx * nchunk;
+    if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((zf::k_zf_mfma<MP, SG, CONJ>), dim3((unsigned)blocks), dim3(256), 0, s, Wt, a_m, a_n, in,
+                       N, M, K, nsym, out, ntile, tpx, nkb, chunk_steps);
+    return hipGetLastError();
+}
+
+template <bool CONJ>
+hipError_t mfma_dispatch(const float2 *Wt, int a_m, int a_n, const float2 *in, int N, int M, int K,
+                         long long nsym, float2 *out, hipStream_t s) {
+    // OFDM_ZF_SG: symbol quads per wave (2, 4 or 8)
+    const int sg = env_int("OFDM_ZF_SG", 4);
+    if (M <= 4) return mfma_launch<2, 8, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+    if (M <= 8) return mfma_launch<4, 8, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+    if (sg == 8) return mfma_launch<8, 8, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+    if (sg == 2) return mfma_launch<8, 2, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+    return mfma_launch<8, 4, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+}
+
+template <int SG, bool CONJ>
+hipError_t mfma_lds_launch(const float2 *Wt, int a_m, int a_n, const float2 *in, int N, int M, int K,
+                           long long nsym, float2 *out, hipStream_t s) {
+    constexpr int SB = 4 * SG;
+    constexpr size_t lds = (size_t)4 * (16 + SB) * 64 * sizeof(float2);
+    const int nkb = (K + 63) / 64, nmb = (M + 15) / 16;
+    const int ntile = nkb * nmb, tpx = (ntile + 7) / 8;
+    const long long nsteps = (nsym + SB - 1) / SB;
+    long long nchunk = (2048 + 8LL * tpx - 1) / (8LL * tpx);
+    long long chunk_steps = (nsteps + nchunk - 1) / nchunk;
+    if (chunk_steps < 2) chunk_steps = 2;
+    nchunk = (nsteps + chunk_steps - 1) / chunk_steps;
+    const long long blocks = 8LL * tpx * nchunk;
+    if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
+    auto kern = zf::k_zf_mfma_lds<SG, CONJ>;
+    static bool attr = false;  // > 64 KiB of dynamic LDS: opt in once per instantiation
+    if (!attr && lds > 64 * 1024) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), lds, s, Wt, a_m, a_n, in, N, M, K, nsym, out,
+                       ntile, tpx, nkb, chunk_steps);
+    return hipGetLastError();
+}
+
 template <bool CONJ>
 hipError_t gemm_dispatch(const float2 *Wt, int a_m, int a_n, const float2 *in, int N, int M, int K,
                          long long nsym, float2 *out, hipStream_t s) {
+    // OFDM_ZF_LDS=3: matrix cores, operands from L1 (k_zf_mfma); =4: matrix
+    // cores, operands DMA'd through LDS (k_zf_mfma_lds; OFDM_ZF_SG = 4 or 8)
+    // Default: the LDS-fed MFMA kernel for detect at M = U >= 32 (same-process
+    // A/B: 3.79-3.97 vs 4.07-4.08 ms at U = 32, R = 64; equal at U = 16,
+    // slower for apply and for U <= 8), the LDS VALU kernel otherwise.
+    const int mode = env_int("OFDM_ZF_LDS", (CONJ && M >= 32 && N >= 8) ? 4 : 1);
+    if (mode == 3) return mfma_dispatch<CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+    if (mode == 4) {
+        if (env_int("OFDM_ZF_SG", 4) == 8) return mfma_lds_launch<8, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+        return mfma_lds_launch<4, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+    }
     // LDS-shared tiles when both operands are wide enough (measured: at N = 4
     // the per-chunk barriers and stores dominate); OFDM_ZF_LDS=0: the
     // per-wave register-tiled kernel for every shape

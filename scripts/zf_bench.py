@@ -70,17 +70,22 @@ def main():
         if a.ab:  # same-process A/B of the kernel variants (env knobs are read per launch)
             variants = {"lds": {"OFDM_ZF_LDS": "1"}, "lds_8x4": {"OFDM_ZF_LDS": "1", "OFDM_ZF_ST": "4"},
                         "lds_nt": {"OFDM_ZF_LDS": "1", "OFDM_ZF_NT": "1"},
-                        "dma": {"OFDM_ZF_LDS": "2"}, "regtile": {"OFDM_ZF_LDS": "0"}}
+                        "dma": {"OFDM_ZF_LDS": "2"}, "regtile": {"OFDM_ZF_LDS": "0"},
+                        "mfma_sg2": {"OFDM_ZF_LDS": "3", "OFDM_ZF_SG": "2"},
+                        "mfma_sg4": {"OFDM_ZF_LDS": "3", "OFDM_ZF_SG": "4"},
+                        "mfma_sg8": {"OFDM_ZF_LDS": "3", "OFDM_ZF_SG": "8"},
+                        "mfma_lds_sg4": {"OFDM_ZF_LDS": "4", "OFDM_ZF_SG": "4"},
+                        "mfma_lds_sg8": {"OFDM_ZF_LDS": "4", "OFDM_ZF_SG": "8"}}
             for rnd in range(2):
                 for key, env in variants.items():
-                    for v in ("OFDM_ZF_LDS", "OFDM_ZF_NT", "OFDM_ZF_ST"):
+                    for v in ("OFDM_ZF_LDS", "OFDM_ZF_NT", "OFDM_ZF_ST", "OFDM_ZF_SG"):
                         os.environ.pop(v, None)
                     os.environ.update(env)
                     d = timed(lambda: ofdm.zf_detect(Wt, Y, out=Xo), a.reps)
                     p = timed(lambda: ofdm.zf_apply(Wt, X, out=Yo), a.reps)
                     old = ab.get(key, (1e9, 1e9))
                     ab[key] = (min(old[0], d), min(old[1], p))
-            for v in ("OFDM_ZF_LDS", "OFDM_ZF_NT", "OFDM_ZF_ST"):
+            for v in ("OFDM_ZF_LDS", "OFDM_ZF_NT", "OFDM_ZF_ST", "OFDM_ZF_SG"):
                 os.environ.pop(v, None)
         t_det = timed(lambda: ofdm.zf_detect(Wt, Y, out=Xo), a.reps)
         t_app = timed(lambda: ofdm.zf_apply(Wt, X, out=Yo), a.reps)
