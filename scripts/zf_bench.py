@@ -75,7 +75,8 @@ def main():
                         "mfma_sg4": {"OFDM_ZF_LDS": "3", "OFDM_ZF_SG": "4"},
                         "mfma_sg8": {"OFDM_ZF_LDS": "3", "OFDM_ZF_SG": "8"},
                         "mfma_lds_sg4": {"OFDM_ZF_LDS": "4", "OFDM_ZF_SG": "4"},
-                        "mfma_lds_sg8": {"OFDM_ZF_LDS": "4", "OFDM_ZF_SG": "8"}}
+                        "mfma_lds_sg8": {"OFDM_ZF_LDS": "4", "OFDM_ZF_SG": "8"},
+                        "mfma_lds8": {"OFDM_ZF_LDS": "5"}}
             for rnd in range(2):
                 for key, env in variants.items():
                     for v in ("OFDM_ZF_LDS", "OFDM_ZF_NT", "OFDM_ZF_ST", "OFDM_ZF_SG"):
