@@ -101,10 +101,23 @@ def cpu_baseline(args, X, ofdm, torch, dev):
     o.frames_demod(iq, Xh, args.prefix, nthreads=threads)
     dt = time.perf_counter() - t0
     syms = nf * (args.S - 1)
+    # BASELINE configs[0] / SURVEY.md 8(d)(a): the cpuLS.hpp shape (R=4, C=1024,
+    # one frame of 100 symbols = 1 pilot + 99 data) on ONE host thread
+    c1 = ofdm.synth_frames(1, 100, 4, 1024, X, prefix=0, seed=args.seed + 11, noise_std=args.noise)
+    torch.cuda.synchronize()
+    c1 = c1.cpu().numpy()
+    reps, t0 = 0, time.perf_counter()
+    while reps < 5 or time.perf_counter() - t0 < 1.0:
+        o.frames_demod(c1, Xh, 0, nthreads=1)
+        reps += 1
+    d1 = time.perf_counter() - t0
     return {"value": syms / dt, "unit": "symbols/s", "cores": threads, "kind": "port",
             "sample": f"{nf} frames x {args.S} symbols (R={args.R}, C={args.C}, prefix="
                       f"{args.prefix}), FFT+LS+MRC+rotate, OpenMP over frames, "
-                      f"{dt:.1f} s wall", "seconds": dt}
+                      f"{dt:.1f} s wall", "seconds": dt,
+            "configs0_single_thread": {"value": reps * 99 / d1, "unit": "symbols/s", "cores": 1,
+                                       "sample": f"R=4, C=1024, 1 frame x 100 symbols, {reps} repetitions, "
+                                                 f"{d1:.2f} s wall"}}
 
 
 def pmc_traffic(path, cfg):

@@ -631,7 +631,9 @@ __device__ __forceinline__ void dma_rows8(const float *const (&g)[16], unsigned 
                  : "memory");
 }
 
-template <int SG, bool CONJ>
+// DBG = 1: diagnostic only (wrong results) -- the data movement (DMA, LDS
+// reads, stores) without the MFMAs, bounding what the MAC side costs.
+template <int SG, bool CONJ, int DBG = 0>
 __global__ void __attribute__((amdgpu_flat_work_group_size(256, 256), amdgpu_waves_per_eu(SG == 4 ? 2 : 1)))
 k_zf_mfma_lds(const float2 *__restrict__ Wt, int a_m, int a_n,
                                                      const float2 *__restrict__ in, int N, int M, int K,
@@ -724,6 +726,12 @@ k_zf_mfma_lds(const float2 *__restrict__ Wt, int a_m, int a_n,
             float2 xv[SG];
 #pragma unroll
             for (int g = 0; g < SG; ++g) xv[g] = sb[(MB + 4 * g + i) * 64];
+            if constexpr (DBG == 1) {
+#pragma unroll
+                for (int p = 0; p < MP; ++p)
+#pragma unroll
+                    for (int g = 0; g < SG; ++g) acc[p][g][g & 3] += are[p] * xv[g].x + aim[p] * xv[g].y;
+            } else {
 #pragma unroll
             for (int p = 0; p < MP; ++p)
 #pragma unroll
@@ -737,6 +745,7 @@ k_zf_mfma_lds(const float2 *__restrict__ Wt, int a_m, int a_n,
 #pragma unroll
                 for (int g = 0; g < SG; ++g)
                     acc[p][g] = __builtin_amdgcn_mfma_f32_4x4x1f32(aim[p], xv[g].y, acc[p][g], 0, 0, 0);
+            }
         }
         // store this step's tile and reset
         const long long s0 = (step0 + st) * SB;
@@ -1058,8 +1067,8 @@ hipError_t mfma_lds_launch(const float2 *Wt, int a_m, int a_n, const float2 *in,
     nchunk = (nsteps + chunk_steps - 1) / chunk_steps;
     const long long blocks = 8LL * tpx * nchunk;
     if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
-    auto kern = zf::k_zf_mfma_lds<SG, CONJ>;
-    static bool attr = false;  // > 64 KiB of dynamic LDS: opt in once per instantiation
+    auto kern = env_int("OFDM_ZF_DEBUG", 0) == 1 ? zf::k_zf_mfma_lds<SG, CONJ, 1> : zf::k_zf_mfma_lds<SG, CONJ>;
+    static bool attr = false;  // > 64 KiB of dynamic LDS: opt in (debug variant: only SG = 4, 64 KiB)
     if (!attr && lds > 64 * 1024) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
