@@ -807,18 +807,20 @@ __device__ __forceinline__ void dma_rows6(const float *const (&g)[12], unsigned 
                  : "memory");
 }
 
-// k_zf_mfma_lds with 8 waves (512 threads) per workgroup and 32 symbols per
-// step: the 16-row W tile is staged once per 32 symbols instead of 16 (the
-// W re-reads from L2 halve) while every wave keeps 128 accumulators (4 row
-// pairs x 8 symbol quads), so two waves share each SIMD: wave w computes
-// subcarriers 16 (w & 3) + b of the block for row pairs 4 (w >> 2) .. + 3,
-// and stages rows w + 8 r (r < 2: W rows, else symbols) of every step.
-template <bool CONJ>
+// k_zf_mfma_lds with 8 waves (512 threads) per workgroup: MB = 4 MPW rows of
+// A and SB = 4 SG symbols per step, every wave keeping MPW x SG x 4 = 128
+// accumulators so that two waves share each SIMD.  Wave w computes
+// subcarriers 16 (w & 3) + b of the block for row pairs MPW (w >> 2) .. + MPW-1
+// and stages rows w + 8 r of every step (the first MB / 8 of them A rows).
+// <4, 8>: the 16-row A tile is staged once per 32 symbols (half the re-reads
+// of k_zf_mfma_lds); <8, 4>: 32-row tiles, so at M = 32 every input row is
+// staged once instead of once per 16-row block.
+template <int MPW, int SG, bool CONJ>
 __global__ void __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(2, 2)))
 k_zf_mfma_lds8(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__restrict__ in, int N, int M,
                int K, long long nsym, float2 *__restrict__ out, int ntile, int tpx, int nkb,
                long long chunk_steps) {
-    constexpr int MP = 4, SG = 8, MB = 16, SB = 4 * SG, NB = 4;
+    constexpr int MP = MPW, MB = 4 * MPW, SB = 4 * SG, NB = 4;
     constexpr int ROWS = MB + SB, RPW = ROWS / 8, WR = MB / 8, LPW = 2 * RPW;
     static_assert(ROWS % 8 == 0 && RPW == 6 && (NB - 2) * LPW <= 63, "rows per wave / vmcnt range");
     extern __shared__ __attribute__((aligned(16))) float2 smd[];  // [NB][ROWS][64]
@@ -1080,12 +1082,12 @@ hipError_t mfma_lds_launch(const float2 *Wt, int a_m, int a_n, const float2 *in,
     return hipGetLastError();
 }
 
-template <bool CONJ>
+template <int MPW, int SG, bool CONJ>
 hipError_t mfma_lds8_launch(const float2 *Wt, int a_m, int a_n, const float2 *in, int N, int M, int K,
                             long long nsym, float2 *out, hipStream_t s) {
-    constexpr int SB = 32;
-    constexpr size_t lds = (size_t)4 * (16 + SB) * 64 * sizeof(float2);  // 96 KiB
-    const int nkb = (K + 63) / 64, nmb = (M + 15) / 16;
+    constexpr int SB = 4 * SG, MB = 4 * MPW;
+    constexpr size_t lds = (size_t)4 * (MB + SB) * 64 * sizeof(float2);  // 96 KiB
+    const int nkb = (K + 63) / 64, nmb = (M + MB - 1) / MB;
     const int ntile = nkb * nmb, tpx = (ntile + 7) / 8;
     const long long nsteps = (nsym + SB - 1) / SB;
     long long nchunk = (1024 + 8LL * tpx - 1) / (8LL * tpx);
@@ -1094,7 +1096,7 @@ hipError_t mfma_lds8_launch(const float2 *Wt, int a_m, int a_n, const float2 *in
     nchunk = (nsteps + chunk_steps - 1) / chunk_steps;
     const long long blocks = 8LL * tpx * nchunk;
     if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
-    auto kern = zf::k_zf_mfma_lds8<CONJ>;
+    auto kern = zf::k_zf_mfma_lds8<MPW, SG, CONJ>;
     static bool attr = false;
     if (!attr) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
@@ -1112,12 +1114,15 @@ hipError_t gemm_dispatch(const float2 *Wt, int a_m, int a_n, const float2 *in, i
                          long long nsym, float2 *out, hipStream_t s) {
     // OFDM_ZF_LDS=3: matrix cores, operands from L1 (k_zf_mfma); =4: matrix
     // cores, operands DMA'd through LDS (k_zf_mfma_lds; OFDM_ZF_SG = 4 or 8)
-    // Default: the LDS-fed MFMA kernel for detect at M = U >= 32 (same-process
-    // A/B: 3.79-3.97 vs 4.07-4.08 ms at U = 32, R = 64; equal at U = 16,
-    // slower for apply and for U <= 8), the LDS VALU kernel otherwise.
-    const int mode = env_int("OFDM_ZF_LDS", (CONJ && M >= 32 && N >= 8) ? 4 : 1);
+    // Default: the 8-wave LDS-fed MFMA kernel with 32-row tiles for detect at
+    // M = U >= 32 (same-process A/B at U = 32, R = 64: 3.66 ms vs 3.80 for
+    // k_zf_mfma_lds and 4.09 for the VALU kernel; the MFMA kernels are equal
+    // at U = 16 and slower for apply and U <= 8), the LDS VALU kernel otherwise.
+    const int mode = env_int("OFDM_ZF_LDS", (CONJ && M >= 32 && N >= 8) ? 6 : 1);
     if (mode == 3) return mfma_dispatch<CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-    if (mode == 5) return mfma_lds8_launch<CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+    // =5: 8-wave workgroups, 16 rows x 32 symbols per step; =6: 32 rows x 16 symbols
+    if (mode == 5) return mfma_lds8_launch<4, 8, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+    if (mode == 6) return mfma_lds8_launch<8, 4, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
     if (mode == 4) {
         if (env_int("OFDM_ZF_SG", 4) == 8) return mfma_lds_launch<8, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
         return mfma_lds_launch<4, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
