@@ -934,6 +934,175 @@ k_zf_mfma_lds8(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the tail re-loads before exit
 }
 
+// The 16 dword DMAs of one wave's step in k_zf_mfma_w128 (4 rows x 4
+// quarters of a 1 KiB row; row r at LDS byte lds + 8192 r, quarter q at
+// + 256 q), M0 saved once.
+__device__ __forceinline__ void dma_rows4x4(const float *const (&g)[16], unsigned lds) {
+    const unsigned l0 = lds + 0u;
+    const unsigned l1 = lds + 256u;
+    const unsigned l2 = lds + 512u;
+    const unsigned l3 = lds + 768u;
+    const unsigned l4 = lds + 8192u;
+    const unsigned l5 = lds + 8448u;
+    const unsigned l6 = lds + 8704u;
+    const unsigned l7 = lds + 8960u;
+    const unsigned l8 = lds + 16384u;
+    const unsigned l9 = lds + 16640u;
+    const unsigned l10 = lds + 16896u;
+    const unsigned l11 = lds + 17152u;
+    const unsigned l12 = lds + 24576u;
+    const unsigned l13 = lds + 24832u;
+    const unsigned l14 = lds + 25088u;
+    const unsigned l15 = lds + 25344u;
+    unsigned keep;
+    asm volatile("s_mov_b32 %[keep], m0\n\t"
+                 "s_mov_b32 m0, %[l0]\n\ts_nop 0\n\tglobal_load_lds_dword %[a0], off\n\t"
+                 "s_mov_b32 m0, %[l1]\n\ts_nop 0\n\tglobal_load_lds_dword %[a1], off\n\t"
+                 "s_mov_b32 m0, %[l2]\n\ts_nop 0\n\tglobal_load_lds_dword %[a2], off\n\t"
+                 "s_mov_b32 m0, %[l3]\n\ts_nop 0\n\tglobal_load_lds_dword %[a3], off\n\t"
+                 "s_mov_b32 m0, %[l4]\n\ts_nop 0\n\tglobal_load_lds_dword %[a4], off\n\t"
+                 "s_mov_b32 m0, %[l5]\n\ts_nop 0\n\tglobal_load_lds_dword %[a5], off\n\t"
+                 "s_mov_b32 m0, %[l6]\n\ts_nop 0\n\tglobal_load_lds_dword %[a6], off\n\t"
+                 "s_mov_b32 m0, %[l7]\n\ts_nop 0\n\tglobal_load_lds_dword %[a7], off\n\t"
+                 "s_mov_b32 m0, %[l8]\n\ts_nop 0\n\tglobal_load_lds_dword %[a8], off\n\t"
+                 "s_mov_b32 m0, %[l9]\n\ts_nop 0\n\tglobal_load_lds_dword %[a9], off\n\t"
+                 "s_mov_b32 m0, %[l10]\n\ts_nop 0\n\tglobal_load_lds_dword %[a10], off\n\t"
+                 "s_mov_b32 m0, %[l11]\n\ts_nop 0\n\tglobal_load_lds_dword %[a11], off\n\t"
+                 "s_mov_b32 m0, %[l12]\n\ts_nop 0\n\tglobal_load_lds_dword %[a12], off\n\t"
+                 "s_mov_b32 m0, %[l13]\n\ts_nop 0\n\tglobal_load_lds_dword %[a13], off\n\t"
+                 "s_mov_b32 m0, %[l14]\n\ts_nop 0\n\tglobal_load_lds_dword %[a14], off\n\t"
+                 "s_mov_b32 m0, %[l15]\n\ts_nop 0\n\tglobal_load_lds_dword %[a15], off\n\t"
+                 "s_mov_b32 m0, %[keep]"
+                 : [keep] "=&s"(keep)
+                 : [a0] "v"(g[0]), [a1] "v"(g[1]), [a2] "v"(g[2]), [a3] "v"(g[3]), [a4] "v"(g[4]), [a5] "v"(g[5]), [a6] "v"(g[6]), [a7] "v"(g[7]), [a8] "v"(g[8]), [a9] "v"(g[9]), [a10] "v"(g[10]), [a11] "v"(g[11]), [a12] "v"(g[12]), [a13] "v"(g[13]), [a14] "v"(g[14]), [a15] "v"(g[15]),
+                   [l0] "s"(l0), [l1] "s"(l1), [l2] "s"(l2), [l3] "s"(l3), [l4] "s"(l4), [l5] "s"(l5), [l6] "s"(l6), [l7] "s"(l7), [l8] "s"(l8), [l9] "s"(l9), [l10] "s"(l10), [l11] "s"(l11), [l12] "s"(l12), [l13] "s"(l13), [l14] "s"(l14), [l15] "s"(l15)
+                 : "memory");
+}
+
+// k_zf_mfma_lds with 128-subcarrier blocks (k_zf_mfma_w128): 8 waves, wave w
+// computes subcarriers 16 w + b of the block (16 rows x 16 symbols, 128
+// accumulators, 2 waves/SIMD), so every staged row piece is 1 KiB of a row
+// instead of 512 B (the no-MAC diagnostic showed the staging, not the MACs,
+// sets the time).  LDS 4 x 32 rows x 1 KiB = 128 KiB: one workgroup per CU.
+template <bool CONJ>
+__global__ void __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(2, 2)))
+k_zf_mfma_w128(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__restrict__ in, int N, int M,
+               int K, long long nsym, float2 *__restrict__ out, int ntile, int tpx, int nkb,
+               long long chunk_steps) {
+    constexpr int MP = 8, SG = 4, MB = 16, SB = 16, NB = 4, BW = 128;
+    constexpr int ROWS = MB + SB, RPW = ROWS / 8, WR = MB / 8, LPW = 4 * RPW;
+    static_assert(RPW == 4 && (NB - 2) * LPW <= 63, "rows per wave / vmcnt range");
+    extern __shared__ __attribute__((aligned(16))) float2 smd[];  // [NB][ROWS][BW]
+    const int bid = blockIdx.x, xcd = bid & 7, jb = bid >> 3;    // XCD-aware mapping as k_zf_gemm
+    const int tile = xcd + 8 * (jb % tpx);
+    if (tile >= ntile) return;  // whole workgroup
+    const long long chunk = jb / tpx;
+    const int kb = tile % nkb, mb = tile / nkb;
+    const int lane = threadIdx.x & 63, b = lane >> 2, i = lane & 3;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int k = kb * BW + 16 * w + b;
+    const int mb0 = mb * MB;
+    const long long nsteps_total = (nsym + SB - 1) / SB;
+    const long long step0 = chunk * chunk_steps, step1 = min(step0 + chunk_steps, nsteps_total);
+    if (step1 <= step0) return;  // whole workgroup
+    const int nst = (int)(step1 - step0);
+    int offq[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) offq[q] = min(kb * BW + 32 * q + (lane >> 1), K - 1) * 2 + (lane & 1);
+    const bool odd = i & 1;
+    const long long anK = (long long)a_n * K, NK = (long long)N * K;
+
+    int si = 0, ni = 0, bi = 0;
+    const float *wbase[WR];
+#pragma unroll
+    for (int r = 0; r < WR; ++r)
+        wbase[r] = reinterpret_cast<const float *>(Wt + (long long)min(mb0 + w + 8 * r, M - 1) * a_m * K);
+    const unsigned lds0 = (unsigned)(size_t)(lvoid_t *)smd + (unsigned)(w * BW * 8);
+    auto issue = [&]() {
+        const unsigned la = lds0 + (unsigned)(bi * ROWS * BW * 8);
+        const long long s0 = (step0 + si) * SB;
+        const float *ga[4 * RPW];
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) {
+            const float *src;
+            if (r < WR) {
+                src = wbase[r] + 2 * (ni * anK);
+            } else {
+                const long long s = min(s0 + (w + 8 * r - MB), nsym - 1);
+                src = reinterpret_cast<const float *>(in + s * NK + (long long)ni * K);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) ga[4 * r + q] = src + offq[q];
+        }
+        dma_rows4x4(ga, la);
+        if (si < nst - 1 || ni < N - 1) {  // advance (the tail re-issues the last step)
+            if (++ni == N) {
+                ni = 0;
+                ++si;
+            }
+        }
+        bi = (bi + 1) & (NB - 1);
+    };
+
+    mf4 acc[MP][SG];
+#pragma unroll
+    for (int p = 0; p < MP; ++p)
+#pragma unroll
+        for (int g = 0; g < SG; ++g) acc[p][g] = mf4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int p = 0; p < NB - 1; ++p) issue();
+    int bc = 0;
+    for (int st = 0; st < nst; ++st) {
+        for (int n = 0; n < N; ++n) {
+            asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((NB - 2) * LPW) : "memory");
+            issue();  // into the buffer of the previous step, which everyone has finished
+            const float2 *sb = smd + bc * ROWS * BW + 16 * w + b;
+            bc = (bc + 1) & (NB - 1);
+            float are[MP], aim[MP];
+#pragma unroll
+            for (int p = 0; p < MP; ++p) {
+                const float2 wv = sb[(2 * p + (i >> 1)) * BW];
+                const float wy = CONJ ? -wv.y : wv.y;
+                are[p] = odd ? wy : wv.x;
+                aim[p] = odd ? wv.x : -wy;
+            }
+            float2 xv[SG];
+#pragma unroll
+            for (int g = 0; g < SG; ++g) xv[g] = sb[(MB + 4 * g + i) * BW];
+#pragma unroll
+            for (int p = 0; p < MP; ++p)
+#pragma unroll
+                for (int g = 0; g < SG; ++g)
+                    acc[p][g] = __builtin_amdgcn_mfma_f32_4x4x1f32(are[p], xv[g].x, acc[p][g], 0, 0, 0);
+#pragma unroll
+            for (int p = 0; p < MP; ++p)
+#pragma unroll
+                for (int g = 0; g < SG; ++g)
+                    acc[p][g] = __builtin_amdgcn_mfma_f32_4x4x1f32(aim[p], xv[g].y, acc[p][g], 0, 0, 0);
+        }
+        const long long s0 = (step0 + st) * SB;
+        if (k < K) {
+#pragma unroll
+            for (int g = 0; g < SG; ++g) {
+                const long long s = s0 + 4 * g + i;
+                if (s >= nsym) break;
+                float2 *o = out + s * M * (long long)K + k;
+#pragma unroll
+                for (int p = 0; p < MP; ++p) {
+                    const int m = mb0 + 2 * p;
+                    if (m < M) o[(long long)m * K] = float2{acc[p][g][0], acc[p][g][1]};
+                    if (m + 1 < M) o[(long long)(m + 1) * K] = float2{acc[p][g][2], acc[p][g][3]};
+                }
+            }
+        }
+#pragma unroll
+        for (int p = 0; p < MP; ++p)
+#pragma unroll
+            for (int g = 0; g < SG; ++g) acc[p][g] = mf4{0.f, 0.f, 0.f, 0.f};
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the tail re-loads before exit
+}
+
 }  // namespace zf
 
 size_t zf_precoder_lds_bytes(int U, int R) {
@@ -1110,6 +1279,33 @@ hipError_t mfma_lds8_launch(const float2 *Wt, int a_m, int a_n, const float2 *in
 }
 
 template <bool CONJ>
+hipError_t mfma_w128_launch(const float2 *Wt, int a_m, int a_n, const float2 *in, int N, int M, int K,
+                            long long nsym, float2 *out, hipStream_t s) {
+    constexpr int SB = 16, MB = 16;
+    constexpr size_t lds = (size_t)4 * (MB + SB) * 128 * sizeof(float2);  // 128 KiB
+    const int nkb = (K + 127) / 128, nmb = (M + MB - 1) / MB;
+    const int ntile = nkb * nmb, tpx = (ntile + 7) / 8;
+    const long long nsteps = (nsym + SB - 1) / SB;
+    long long nchunk = (1024 + 8LL * tpx - 1) / (8LL * tpx);
+    long long chunk_steps = (nsteps + nchunk - 1) / nchunk;
+    if (chunk_steps < 2) chunk_steps = 2;
+    nchunk = (nsteps + chunk_steps - 1) / chunk_steps;
+    const long long blocks = 8LL * tpx * nchunk;
+    if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
+    auto kern = zf::k_zf_mfma_w128<CONJ>;
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(512), lds, s, Wt, a_m, a_n, in, N, M, K, nsym, out,
+                       ntile, tpx, nkb, chunk_steps);
+    return hipGetLastError();
+}
+
+template <bool CONJ>
 hipError_t gemm_dispatch(const float2 *Wt, int a_m, int a_n, const float2 *in, int N, int M, int K,
                          long long nsym, float2 *out, hipStream_t s) {
     // OFDM_ZF_LDS=3: matrix cores, operands from L1 (k_zf_mfma); =4: matrix
@@ -1118,11 +1314,14 @@ hipError_t gemm_dispatch(const float2 *Wt, int a_m, int a_n, const float2 *in, i
     // M = U >= 32 (same-process A/B at U = 32, R = 64: 3.66 ms vs 3.80 for
     // k_zf_mfma_lds and 4.09 for the VALU kernel; the MFMA kernels are equal
     // at U = 16 and slower for apply and U <= 8), the LDS VALU kernel otherwise.
-    const int mode = env_int("OFDM_ZF_LDS", (CONJ && M >= 32 && N >= 8) ? 6 : 1);
+    // At 8 < M <= 16 (one 16-row block) the 128-subcarrier MFMA kernel: 1.98 vs
+    // 2.06 ms at U = 16.
+    const int mode = env_int("OFDM_ZF_LDS", !(CONJ && N >= 8) ? 1 : M > 16 ? 6 : M > 8 ? 7 : 1);
     if (mode == 3) return mfma_dispatch<CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
     // =5: 8-wave workgroups, 16 rows x 32 symbols per step; =6: 32 rows x 16 symbols
     if (mode == 5) return mfma_lds8_launch<4, 8, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
     if (mode == 6) return mfma_lds8_launch<8, 4, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+    if (mode == 7) return mfma_w128_launch<CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);  // 128-sc blocks
     if (mode == 4) {
         if (env_int("OFDM_ZF_SG", 4) == 8) return mfma_lds_launch<8, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
         return mfma_lds_launch<4, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
