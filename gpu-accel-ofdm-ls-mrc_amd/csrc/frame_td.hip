@@ -495,6 +495,83 @@ k_mrc_td1024_hlds(const float2 *__restrict__ iq, int S, int R, int prefix,
     }
 }
 
+// Small batches (k_mrc_td1024_rsplit): the 8 waves of a workgroup are 4
+// symbols x 2 antenna halves -- wave w takes symbol w & 3 and rows
+// [h R0, h R0 + R_h), h = w >> 2, R0 = ceil(R / 2), with its own Hc rows
+// from L2 (the per-wave path of hlds_rows) -- and the two partial sums meet
+// in LDS: Z = sum_{r < R0} + sum_{r >= R0} (not the strictly sequential
+// antenna order of matrixMultThenSum; the difference is f32 rounding, far
+// inside the 1e-5 tolerance).  Twice the waves per symbol, half the rows
+// each: a batch of Q symbols is 2Q half-length wave tasks, so the last
+// round of workgroups is much fuller when Q is only a few times the ~4 096
+// resident waves (configs[1]: 10 000 symbols = 2.44 rounds of the 8-symbol
+// workgroups, the third 44 % full).
+template <bool NT>
+__global__ void __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 4)))
+k_mrc_td1024_rsplit(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
+                    const float *__restrict__ P, float2 *__restrict__ out, long long nq, long long nblocks,
+                    long long per_xcd, int mode) {
+    using namespace hlds;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    float2 *tw1 = lds, *tw2 = lds + TW1S;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), t = threadIdx.x & 63;
+    float2 *T0 = lds + TW1S + TW2S;
+    float2 *T = T0 + w * TS;
+    const long long pb = blockIdx.x;
+    const long long lb = (pb & 7) * per_xcd + (pb >> 3);  // XCD-grouped logical block
+    if (lb >= nblocks) return;                            // whole workgroup
+    fill(tw1, tw2);
+    __syncthreads();
+    const int h = w >> 2, R0 = (R + 1) >> 1, rows = h ? R - R0 : R0;
+    const long long qw = lb * 4 + (w & 3);
+    const bool store = qw < nq;
+    const long long q = store ? qw : nq - 1;  // tail waves compute a valid symbol, never store
+    const int nsym = S - 1;
+    const long long f = q / nsym;
+    const int s = 1 + (int)(q % nsym);
+    const int Cp = C + prefix;
+    const float2 *sym = iq + ((f * S + s) * (long long)R + (long long)h * R0) * Cp + prefix;
+    const float4 *Hf = reinterpret_cast<const float4 *>(Hc + (f * (long long)R + (long long)h * R0) * C);
+    float2 acc[16];
+    hlds_rows<NT, false, false, 0, 8>(sym, Cp, rows, Hf, t, T, tw1, tw2, T0, nullptr, acc);
+    // second half -> its transpose image -> first half (same lane, same bins)
+    if (h) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) T[k * hlds::TP + t] = acc[k];
+    }
+    __syncthreads();
+    if (h || !store) return;
+    const float2 *Tp = T0 + (w + 4) * TS;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const float2 v = Tp[k * hlds::TP + t];
+        acc[k] = float2{acc[k].x + v.x, acc[k].y + v.y};
+    }
+    // outputs staged in this wave's image, then 16 contiguous 512-B stores
+    const int b0 = lane_bin0(t);
+    float2 *o = out + q * K;
+    const float *Pf = P + f * C + b0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int b = b0 + 16 * k;
+        if (b == 0) continue;
+        float2 v = acc[k];
+        int j = b - 1;
+        if ((mode & 1) == 0) {
+            const float pv = Pf[16 * k];
+            v = float2{acc[k].x / pv, acc[k].y / pv};
+            j = out_pos(b - 1, K);
+        }
+        T[(j >> 6) * hlds::TP + (j & 63)] = v;
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        const int j = t + 64 * m;
+        if (j < K) o[j] = T[m * hlds::TP + t];
+    }
+}
+
 #define OFDM_MRC_ARGS                                                                            \
     const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,     \
         const float *__restrict__ P, float2 *__restrict__ out, long long nq, long long nblocks, \
@@ -557,6 +634,14 @@ hipError_t launch_mrc_td1024(const float2 *iq, long long nframes, int S, int R, 
         grid = pg < grid ? pg : grid;
     }
     if (grid > 0x7fffffffll) return hipErrorInvalidValue;
+    // OFDM_MRC_RSPLIT=1: antenna-split workgroups (k_mrc_td1024_rsplit)
+    if (W == 8 && hlds_on && !persist && !sync && !dbg && nt && knob("OFDM_MRC_RSPLIT", 0) == 1) {
+        const long long nb = (nq + 3) / 4, pxcd = (nb + 7) / 8;
+        if (pxcd * 8 > 0x7fffffffll) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((k_mrc_td1024_rsplit<true>), dim3((unsigned)(pxcd * 8)), dim3(512), hlds::LDS_BYTES, s,
+                           iq, S, R, prefix, Hc, P, out, nq, nb, pxcd, mode);
+        return hipGetLastError();
+    }
     if (W == 8 && hlds_on && !persist && !sync && !dbg) {
         const int pf = knob("OFDM_MRC_PF", 1);  // next-row prefetch into the dead a[]
         // packed-f32 FFT halves / MAC (pk.hpp): bit 0 first FFT half, bit 1

@@ -160,6 +160,35 @@ def test_empty_batch_is_noop(ofdm, dev):
     assert out.shape == (0, 2, 1023)
 
 
+@pytest.mark.parametrize("F,S,R,C,prefix", [c for c in CONFIGS if c[3] == 1024] + [(2, 9, 2, 1024, 3),
+                                                                                    (100, 101, 16, 1024, 0)])
+def test_frame_demod_rsplit_vs_oracle(ofdm, oracle, dev, monkeypatch, F, S, R, C, prefix):
+    """k_mrc_td1024_rsplit (OFDM_MRC_RSPLIT=1: two waves per symbol, antenna
+    halves summed in LDS), normalised outputs and partial numerators."""
+    import torch
+    monkeypatch.setenv("OFDM_MRC_RSPLIT", "1")
+    X = to_dev(qpsk_pilots(C - 1), dev)
+    big = F * (S - 1) > 2000
+    seed = 7 + R if big else 99 + C  # small cases: the realisations of test_frame_demod_synth_vs_oracle
+    iq = ofdm.synth_frames(F, S, R, C, X, prefix=prefix, seed=seed, noise_std=0.01 if big else 0.05)
+    out = ofdm.frame_demod(iq, X, prefix)
+    if big:  # the configs[1] batch: size-independent check + oracle on two frames
+        assert int(ofdm.count_symbol_errors(out, S, seed=seed).item()) == 0
+        sel = [0, F - 1]
+        parity(host(out)[sel], oracle.frames_demod(host(iq)[sel], host(X), prefix, nthreads=8))
+        return
+    parity(host(out), oracle.frames_demod(host(iq), host(X), prefix, nthreads=8))
+    monkeypatch.setenv("OFDM_MRC_RSPLIT", "0")
+    parity(host(out), host(ofdm.frame_demod(iq, X, prefix)))  # vs the sequential-order kernel
+    monkeypatch.setenv("OFDM_MRC_RSPLIT", "1")
+    Pp, ws = ofdm.frame_ls_partial(iq, X, prefix)
+    num = ofdm.frame_mrc_partial(iq, ws, prefix)
+    monkeypatch.setenv("OFDM_MRC_RSPLIT", "0")
+    num_ref = ofdm.frame_mrc_partial(iq, ws, prefix)
+    torch.cuda.synchronize()
+    parity(host(num), host(num_ref))
+
+
 # ------------------------------------------ antenna split (partial MRC path)
 
 @pytest.mark.parametrize("C,prefix", [(1024, 0), (1024, 16), (2048, 0), (2048, 12), (4096, 0), (4096, 3), (256, 0)])
