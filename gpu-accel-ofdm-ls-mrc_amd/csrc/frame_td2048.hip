@@ -252,6 +252,66 @@ k_mrc_td2048(const float2 *__restrict__ iq, int S, int R, int prefix, const floa
     }
 }
 
+// k_mrc_td2048 with fewer live registers (k_mrc_td2048_lr, OFDM_MRC2K_LR=1):
+// each FFT half is combined right after it is transformed, with that half's
+// Hc words read from L2 just then (row_fft2048_pf without its prefetch), so
+// only one half's bins and Hc are live -- WPE = 3 waves per SIMD instead of 2
+// (12 per CU, LDS 51 KiB per 4-wave workgroup), more waves to cover the L2
+// latency of the per-symbol Hc row.
+template <bool NT, int WPE>
+__global__ void __attribute__((amdgpu_flat_work_group_size(256, 256), amdgpu_waves_per_eu(WPE, WPE)))
+k_mrc_td2048_lr(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
+                const float *__restrict__ P, float2 *__restrict__ out, long long nq, long long nblocks,
+                long long per_xcd, int mode) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int w = threadIdx.x >> 6, t = threadIdx.x & 63;
+    float2 *T = lds + TAB + w * hl::TS;
+    const long long pb = blockIdx.x;
+    const long long lb = (pb & 7) * per_xcd + (pb >> 3);
+    if (lb >= nblocks) return;
+    fill_tables(lds);
+    __syncthreads();
+    const long long q = lb * MRC_WAVES + w;
+    if (q >= nq) return;  // no block-level sync follows
+    const int nsym = S - 1;
+    const long long f = q / nsym;
+    const int s = 1 + (int)(q % nsym);
+    const int Cp = C + prefix;
+    const float2 *sym = iq + (f * S + s) * (long long)R * Cp + prefix;
+    const float2 *Hf = Hc + f * (long long)R * C;  // float4 lane order read as float2 pairs
+    float2 ae[16], ao[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) ae[k] = ao[k] = float2{0.f, 0.f};
+    for (int r = 0; r < R; ++r) {
+        float2 lo[16], hi[16];
+        row_load<NT>(sym + (long long)r * Cp, t, lo);
+        row_load<NT>(sym + (long long)r * Cp + HALF, t, hi);
+        row_fft2048_pf<NT, false>(nullptr, t, T, lds, lo, hi, Hf + (long long)r * C, ae, ao);
+    }
+    const int b0 = lane_bin0(t);
+    float2 *o = out + q * K;
+    if ((mode & 1) == 0) {
+        const float *Pf = P + f * C;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int be = 2 * (b0 + 16 * k);
+            if (be > 0) {
+                const float pv = Pf[be];
+                o[out_pos(be - 1, K)] = float2{ae[k].x / pv, ae[k].y / pv};
+            }
+            const float pv = Pf[be + 1];
+            o[out_pos(be, K)] = float2{ao[k].x / pv, ao[k].y / pv};
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const int be = 2 * (b0 + 16 * k);
+            if (be > 0) o[be - 1] = ae[k];
+            o[be] = ao[k];
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // MRC with the channel rows shared through LDS (k_mrc_td2048h): 8 waves = 8
 // consecutive data symbols of ONE frame per workgroup (frame-aligned map,
@@ -419,6 +479,16 @@ hipError_t launch_mrc_td2048(const float2 *iq, long long nframes, int S, int R, 
         else
             hipLaunchKernelGGL((k_mrc_td2048h<true, true, 4>), dim3((unsigned)(pxcd * 8)), dim3(64 * hw), lb, s,
                                iq, S, R, prefix, Hc, P, out, nb, pxcd, mode);
+        return hipGetLastError();
+    }
+    const char *lr = getenv("OFDM_MRC2K_LR");  // 1: k_mrc_td2048_lr, 3 waves/SIMD; 2: same code, 2 waves/SIMD
+    if (lr && (lr[0] == '1' || lr[0] == '2')) {
+        if (lr[0] == '1')
+            hipLaunchKernelGGL((k_mrc_td2048_lr<true, 3>), dim3((unsigned)grid), dim3(64 * MRC_WAVES),
+                               lds_bytes(MRC_WAVES), s, iq, S, R, prefix, Hc, P, out, nq, nblocks, per_xcd, mode);
+        else
+            hipLaunchKernelGGL((k_mrc_td2048_lr<true, 2>), dim3((unsigned)grid), dim3(64 * MRC_WAVES),
+                               lds_bytes(MRC_WAVES), s, iq, S, R, prefix, Hc, P, out, nq, nblocks, per_xcd, mode);
         return hipGetLastError();
     }
     if (getenv("OFDM_MRC2K_DEBUG") && getenv("OFDM_MRC2K_DEBUG")[0] == '6')
