@@ -1103,6 +1103,113 @@ k_zf_mfma_w128(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the tail re-loads before exit
 }
 
+// W-stationary MFMA GEMM for M <= 16 (k_zf_wstat; detect at U <= 16): the
+// no-MAC diagnostic showed the re-staging of W tiles next to the input stream
+// costs most of the time, so here a workgroup owns 16 subcarriers and ONE
+// contiguous range of symbols, loads its whole A tile (all M <= 16 rows x N
+// <= 72 columns x 16 subcarriers, <= 144 KiB) into LDS once, and its 8 waves
+// then stream the input straight from HBM -- each wave its own 16 symbols
+// per step, so no input is shared and nothing but the input and output
+// crosses the memory system per symbol.  Lane (b, i) = block b = subcarrier
+// k0 + b, as k_zf_mfma; A operands from LDS ([n][16 rows][16 subcarriers],
+// rows >= M zero), input operands from global memory, prefetched PD n-steps
+// ahead in registers.
+// XMAP: block b runs on XCD b % 8 (round-robin dispatch; speed only): the
+// chunk is b % 8 + 8 (b / (8 nkb)) and the subcarrier block (b / 8) % nkb, so
+// one XCD reads all subcarrier pieces of the same symbol rows.
+template <bool CONJ, bool XMAP = false>
+__global__ void __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(2, 2)))
+k_zf_wstat(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__restrict__ in, int N, int M, int K,
+           long long nsym, float2 *__restrict__ out, int nkb, int nmb, long long chunk_syms) {
+    constexpr int MP = 8, SG = 4, SW = 4 * SG, PD = 3;
+    extern __shared__ __attribute__((aligned(16))) float2 smd[];  // [N][16][16]
+    // tile = (subcarrier block, 16-row block); the row blocks of one subcarrier
+    // block are adjacent in dispatch order, so they read the same input rows
+    // at about the same time (the second read hits L2)
+    const long long ntl = (long long)nkb * nmb;
+    const int tl = XMAP ? (int)((blockIdx.x >> 3) % ntl) : (int)(blockIdx.x % ntl);
+    const int kb = tl / nmb, mb = tl % nmb, mr0 = 16 * mb;
+    const long long chunk = XMAP ? (long long)(blockIdx.x & 7) + 8LL * (blockIdx.x / (8LL * ntl))
+                                 : (long long)(blockIdx.x / ntl);
+    const int lane = threadIdx.x & 63, b = lane >> 2, i = lane & 3;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int k0 = kb * 16, k = k0 + b, kc = min(k, K - 1);
+    const long long sbeg = chunk * chunk_syms, send = min(sbeg + chunk_syms, nsym);
+    if (sbeg >= send) return;  // whole workgroup
+    // A tile -> LDS: element (n, m, bb) = A_k0+bb(m, n), rows m >= M zero
+    for (int e = threadIdx.x; e < N * 256; e += 512) {
+        const int bb = e & 15, m = mr0 + ((e >> 4) & 15), n = e >> 8;
+        const int kk = min(k0 + bb, K - 1);
+        smd[e] = m < M ? Wt[((long long)m * a_m + (long long)n * a_n) * K + kk] : float2{0.f, 0.f};
+    }
+    __syncthreads();
+    const bool odd = i & 1;
+    const long long NK = (long long)N * K;
+    const float2 *wl = smd + (i >> 1) * 16 + b;  // + n * 256 + 2 p * 16
+
+    for (long long s0 = sbeg + (long long)w * SW; s0 < send; s0 += 8LL * SW) {
+        const float2 *xrow[SG];
+#pragma unroll
+        for (int g = 0; g < SG; ++g) xrow[g] = in + min(s0 + 4 * g + i, send - 1) * NK + kc;
+        mf4 acc[MP][SG];
+#pragma unroll
+        for (int p = 0; p < MP; ++p)
+#pragma unroll
+            for (int g = 0; g < SG; ++g) acc[p][g] = mf4{0.f, 0.f, 0.f, 0.f};
+        float2 xq[PD][SG];
+#pragma unroll
+        for (int d = 0; d < PD; ++d)
+#pragma unroll
+            for (int g = 0; g < SG; ++g) xq[d][g] = xrow[g][(long long)min(d, N - 1) * K];
+        for (int n0 = 0; n0 < N; n0 += PD) {
+#pragma unroll
+            for (int d = 0; d < PD; ++d) {
+                const int n = n0 + d;
+                if (n < N) {  // wave-uniform
+                    float are[MP], aim[MP];
+#pragma unroll
+                    for (int p = 0; p < MP; ++p) {
+                        const float2 wv = wl[n * 256 + 2 * p * 16];
+                        const float wy = CONJ ? -wv.y : wv.y;
+                        are[p] = odd ? wy : wv.x;
+                        aim[p] = odd ? wv.x : -wy;
+                    }
+                    float2 xv[SG];
+#pragma unroll
+                    for (int g = 0; g < SG; ++g) xv[g] = xq[d][g];
+                    const int nn = min(n + PD, N - 1);  // refill this slot PD steps ahead
+#pragma unroll
+                    for (int g = 0; g < SG; ++g) xq[d][g] = xrow[g][(long long)nn * K];
+#pragma unroll
+                    for (int p = 0; p < MP; ++p)
+#pragma unroll
+                        for (int g = 0; g < SG; ++g)
+                            acc[p][g] = __builtin_amdgcn_mfma_f32_4x4x1f32(are[p], xv[g].x, acc[p][g], 0, 0, 0);
+#pragma unroll
+                    for (int p = 0; p < MP; ++p)
+#pragma unroll
+                        for (int g = 0; g < SG; ++g)
+                            acc[p][g] = __builtin_amdgcn_mfma_f32_4x4x1f32(aim[p], xv[g].y, acc[p][g], 0, 0, 0);
+                }
+            }
+        }
+        if (k < K) {
+#pragma unroll
+            for (int g = 0; g < SG; ++g) {
+                const long long s = s0 + 4 * g + i;
+                if (s >= send) break;
+                float2 *o = out + s * M * (long long)K + k;
+#pragma unroll
+                for (int p = 0; p < MP; ++p) {
+                    const int m = mr0 + 2 * p;
+                    if (m < M) o[(long long)m * K] = float2{acc[p][g][0], acc[p][g][1]};
+                    if (m + 1 < M) o[(long long)(m + 1) * K] = float2{acc[p][g][2], acc[p][g][3]};
+                }
+            }
+        }
+    }
+}
+
 }  // namespace zf
 
 size_t zf_precoder_lds_bytes(int U, int R) {
@@ -1305,6 +1412,33 @@ hipError_t mfma_w128_launch(const float2 *Wt, int a_m, int a_n, const float2 *in
     return hipGetLastError();
 }
 
+template <bool CONJ, bool XMAP>
+hipError_t wstat_launch(const float2 *Wt, int a_m, int a_n, const float2 *in, int N, int M, int K,
+                        long long nsym, float2 *out, hipStream_t s) {
+    const size_t lds = (size_t)N * 256 * sizeof(float2);  // N <= 72: <= 144 KiB
+    const int nkb = (K + 15) / 16, nmb = (M + 15) / 16;
+    // ~1 workgroup per CU over all (tile, symbol chunk) pairs;
+    // XMAP: a multiple of 8 chunks (one per XCD)
+    long long nchunk = XMAP ? 8 : (256 + nkb * nmb - 1) / (nkb * nmb);
+    long long chunk_syms = (nsym + nchunk - 1) / nchunk;
+    if (chunk_syms < 128) chunk_syms = 128;
+    nchunk = (nsym + chunk_syms - 1) / chunk_syms;
+    if (XMAP) nchunk = (nchunk + 7) / 8 * 8;  // empty chunks return at once
+    const long long blocks = (long long)nkb * nmb * nchunk;
+    if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
+    auto kern = zf::k_zf_wstat<CONJ, XMAP>;
+    static bool attr = false;
+    if (!attr) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 72 * 256 * (int)sizeof(float2));
+        if (e != hipSuccess) return e;
+        attr = true;
+    }
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(512), lds, s, Wt, a_m, a_n, in, N, M, K, nsym, out, nkb,
+                       nmb, chunk_syms);
+    return hipGetLastError();
+}
+
 template <bool CONJ>
 hipError_t gemm_dispatch(const float2 *Wt, int a_m, int a_n, const float2 *in, int N, int M, int K,
                          long long nsym, float2 *out, hipStream_t s) {
@@ -1314,14 +1448,23 @@ hipError_t gemm_dispatch(const float2 *Wt, int a_m, int a_n, const float2 *in, i
     // M = U >= 32 (same-process A/B at U = 32, R = 64: 3.66 ms vs 3.80 for
     // k_zf_mfma_lds and 4.09 for the VALU kernel; the MFMA kernels are equal
     // at U = 16 and slower for apply and U <= 8), the LDS VALU kernel otherwise.
-    // At 8 < M <= 16 (one 16-row block) the 128-subcarrier MFMA kernel: 1.98 vs
-    // 2.06 ms at U = 16.
-    const int mode = env_int("OFDM_ZF_LDS", !(CONJ && N >= 8) ? 1 : M > 16 ? 6 : M > 8 ? 7 : 1);
+    // Measured defaults (same-process A/B, R = 64, 10 000 symbols):
+    //   detect, M = U > 8, N = R <= 72: W-stationary MFMA with one symbol chunk
+    //     per XCD (k_zf_wstat<., true>): 1.87 vs 2.05 ms (VALU) at U = 16,
+    //     3.34 vs 3.67 (k_zf_mfma_lds8<8,4>) / 4.09 (VALU) at U = 32;
+    //   detect with N > 72: k_zf_mfma_lds8<8,4> (M > 16) / k_zf_mfma_w128;
+    //   apply at N = U >= 32: k_zf_wstat<., true> (4.08 vs 4.28 ms);
+    //   everything else (U <= 8, apply at U < 32): the LDS VALU kernel.
+    const int wdef = CONJ ? (N < 8 || M <= 8 ? 1 : N <= 72 ? 9 : M > 16 ? 6 : 7) : (N >= 32 && N <= 72 ? 9 : 1);
+    const int mode = env_int("OFDM_ZF_LDS", wdef);
     if (mode == 3) return mfma_dispatch<CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
     // =5: 8-wave workgroups, 16 rows x 32 symbols per step; =6: 32 rows x 16 symbols
     if (mode == 5) return mfma_lds8_launch<4, 8, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
     if (mode == 6) return mfma_lds8_launch<8, 4, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
     if (mode == 7) return mfma_w128_launch<CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);  // 128-sc blocks
+    // =8 / 9: W-stationary MFMA (N <= 72; 16-row blocks), 9 with one symbol chunk per XCD
+    if (mode == 8 && N <= 72) return wstat_launch<CONJ, false>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+    if (mode == 9 && N <= 72) return wstat_launch<CONJ, true>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
     if (mode == 4) {
         if (env_int("OFDM_ZF_SG", 4) == 8) return mfma_lds_launch<8, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
         return mfma_lds_launch<4, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
