@@ -243,7 +243,9 @@ __global__ void __launch_bounds__(256) k_zf_gemm(const float2 *__restrict__ Wt, 
 // conflict free: 64 lanes x 8 B contiguous).  The loads of chunk c+1 are in
 // flight while chunk c is computed; two LDS buffers, one barrier per chunk.
 // ST = 4, NC = 1 (OFDM_ZF_ST=4): 8x4 tiles, 64 accumulator VGPRs, 4 waves/SIMD.
-template <int MG, bool CONJ, bool NTIN = false, int ST = 8, int NC = 2>
+// XMAP (OFDM_ZF_XMAP=1): XCD x takes symbol chunks x, x + 8, ... with all
+// tiles (the k_zf_wstat map) instead of tiles x, x + 8, ... with all chunks.
+template <int MG, bool CONJ, bool NTIN = false, int ST = 8, int NC = 2, bool XMAP = false>
 __global__ void __attribute__((amdgpu_flat_work_group_size(256, 256), amdgpu_waves_per_eu(ST == 4 ? 4 : 1)))
 k_zf_gemm_lds(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__restrict__ in, int N, int M,
               int K, long long nsym, float2 *__restrict__ out, int ntile, int tpx, int nkb,
@@ -253,9 +255,9 @@ k_zf_gemm_lds(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__r
     static_assert(AROWS % 4 == 0 && ROWS % 4 == 0, "rows split evenly over the 4 waves");
     __shared__ float2 sm[2][ROWS * 64];
     const int b = blockIdx.x, xcd = b & 7, j = b >> 3;  // XCD-aware mapping as k_zf_gemm
-    const int tile = xcd + 8 * (j % tpx);
+    const int tile = XMAP ? j % ntile : xcd + 8 * (j % tpx);
     if (tile >= ntile) return;  // whole workgroup
-    const long long chunk = j / tpx;
+    const long long chunk = XMAP ? xcd + 8LL * (j / ntile) : j / tpx;
     const int kb = tile % nkb, mb = tile / nkb;
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1286,6 +1288,12 @@ hipError_t gemm_lds_launch(const float2 *Wt, int a_m, int a_n, const float2 *in,
     if (chunk_steps < 4) chunk_steps = 4;
     nchunk = (nsteps + chunk_steps - 1) / chunk_steps;
     const long long blocks = 8LL * tpx * nchunk;
+    if (env_int("OFDM_ZF_XMAP", 0) && ST == 8 && !DMA) {
+        const long long nc8 = (nchunk + 7) / 8 * 8;  // one chunk per XCD per round; empty chunks return
+        hipLaunchKernelGGL((zf::k_zf_gemm_lds<MG, CONJ, false, 8, 2, true>), dim3((unsigned)(ntile * nc8)), dim3(256),
+                           0, s, Wt, a_m, a_n, in, N, M, K, nsym, out, ntile, tpx, nkb, chunk_steps);
+        return hipGetLastError();
+    }
     if (ST == 4)  // 8x4 tiles, one n per LDS chunk, 4 waves/SIMD
         hipLaunchKernelGGL((zf::k_zf_gemm_lds<MG, CONJ, false, 4, 1>), dim3((unsigned)blocks), dim3(256), 0, s,
                            Wt, a_m, a_n, in, N, M, K, nsym, out, ntile, tpx, nkb, chunk_steps);
@@ -1454,8 +1462,10 @@ hipError_t gemm_dispatch(const float2 *Wt, int a_m, int a_n, const float2 *in, i
     //     3.34 vs 3.67 (k_zf_mfma_lds8<8,4>) / 4.09 (VALU) at U = 32;
     //   detect with N > 72: k_zf_mfma_lds8<8,4> (M > 16) / k_zf_mfma_w128;
     //   apply at N = U >= 32: k_zf_wstat<., true> (4.08 vs 4.28 ms);
-    //   everything else (U <= 8, apply at U < 32): the LDS VALU kernel.
-    const int wdef = CONJ ? (N < 8 || M <= 8 ? 1 : N <= 72 ? 9 : M > 16 ? 6 : 7) : (N >= 32 && N <= 72 ? 9 : 1);
+    //   detect at U <= 8: the per-wave register-tiled VALU kernel (1.26-1.37 vs
+    //     1.35-1.39 ms at U = 8);
+    //   apply at U < 32: the LDS VALU kernel.
+    const int wdef = CONJ ? (N < 8 ? 1 : M <= 8 ? 0 : N <= 72 ? 9 : M > 16 ? 6 : 7) : (N >= 32 && N <= 72 ? 9 : 1);
     const int mode = env_int("OFDM_ZF_LDS", wdef);
     if (mode == 3) return mfma_dispatch<CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
     // =5: 8-wave workgroups, 16 rows x 32 symbols per step; =6: 32 rows x 16 symbols

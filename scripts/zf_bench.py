@@ -76,18 +76,18 @@ def main():
                         "mfma_sg8": {"OFDM_ZF_LDS": "3", "OFDM_ZF_SG": "8"},
                         "mfma_lds_sg4": {"OFDM_ZF_LDS": "4", "OFDM_ZF_SG": "4"},
                         "mfma_lds_sg8": {"OFDM_ZF_LDS": "4", "OFDM_ZF_SG": "8"},
-                        "mfma_lds8": {"OFDM_ZF_LDS": "5"}, "mfma_lds8_m32": {"OFDM_ZF_LDS": "6"}, "mfma_w128": {"OFDM_ZF_LDS": "7"}, "mfma_wstat": {"OFDM_ZF_LDS": "8"}, "mfma_wstat_xmap": {"OFDM_ZF_LDS": "9"},
+                        "mfma_lds8": {"OFDM_ZF_LDS": "5"}, "mfma_lds8_m32": {"OFDM_ZF_LDS": "6"}, "mfma_w128": {"OFDM_ZF_LDS": "7"}, "mfma_wstat": {"OFDM_ZF_LDS": "8"}, "mfma_wstat_xmap": {"OFDM_ZF_LDS": "9"}, "lds_xmap": {"OFDM_ZF_LDS": "1", "OFDM_ZF_XMAP": "1"},
                         "diag_nomac_lds_sg4": {"OFDM_ZF_LDS": "4", "OFDM_ZF_SG": "4", "OFDM_ZF_DEBUG": "1"}}
             for rnd in range(2):
                 for key, env in variants.items():
-                    for v in ("OFDM_ZF_LDS", "OFDM_ZF_NT", "OFDM_ZF_ST", "OFDM_ZF_SG", "OFDM_ZF_DEBUG"):
+                    for v in ("OFDM_ZF_LDS", "OFDM_ZF_NT", "OFDM_ZF_ST", "OFDM_ZF_SG", "OFDM_ZF_DEBUG", "OFDM_ZF_XMAP"):
                         os.environ.pop(v, None)
                     os.environ.update(env)
                     d = timed(lambda: ofdm.zf_detect(Wt, Y, out=Xo), a.reps)
                     p = timed(lambda: ofdm.zf_apply(Wt, X, out=Yo), a.reps)
                     old = ab.get(key, (1e9, 1e9))
                     ab[key] = (min(old[0], d), min(old[1], p))
-            for v in ("OFDM_ZF_LDS", "OFDM_ZF_NT", "OFDM_ZF_ST", "OFDM_ZF_SG", "OFDM_ZF_DEBUG"):
+            for v in ("OFDM_ZF_LDS", "OFDM_ZF_NT", "OFDM_ZF_ST", "OFDM_ZF_SG", "OFDM_ZF_DEBUG", "OFDM_ZF_XMAP"):
                 os.environ.pop(v, None)
         t_det = timed(lambda: ofdm.zf_detect(Wt, Y, out=Xo), a.reps)
         t_app = timed(lambda: ofdm.zf_apply(Wt, X, out=Yo), a.reps)
