@@ -206,7 +206,9 @@ def main():
     barrier()
 
     ls_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
-    mrc_ms = sum(e[1].elapsed_time(e[2]) for e in events) / args.steps
+    mrc_all = sorted(e[1].elapsed_time(e[2]) for e in events)
+    mrc_ms = sum(mrc_all) / args.steps
+    mrc_median = mrc_all[len(mrc_all) // 2]
     stats = torch.tensor([elapsed, float(errs)], dtype=torch.float64, device=dev)
     if world > 1:
         mx = stats.clone()
@@ -244,7 +246,8 @@ def main():
                      "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                      "traffic_source": tsrc,
-                     "bytes_per_launch": Q * b_sym, "avg_launch_ms": mrc_ms},
+                     "bytes_per_launch": Q * b_sym, "avg_launch_ms": mrc_ms,
+                     "median_launch_ms": mrc_median},
         "stages_ms": {"estimate_ls": ls_ms, "combine_mrc": mrc_ms},
         "step_algorithmic_GBps": step_bytes / (elapsed / args.steps) / 1e9,
         "check": {"qpsk_symbol_errors": errs},
@@ -425,7 +428,8 @@ def bench_split(args, X, dev, world, rank, barrier):
         "roofline": {"kernel": f"{kern} partial numerators (FFT+MRC)", "bound": "hbm",
                      "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
-                     "bytes_per_launch": Q * b_sym, "avg_launch_ms": mrc_ms},
+                     "bytes_per_launch": Q * b_sym, "avg_launch_ms": mrc_ms,
+                     "median_launch_ms": mrc_median},
         "check": {"qpsk_symbol_errors": errs},
         "cpu_baseline": None,
     }
