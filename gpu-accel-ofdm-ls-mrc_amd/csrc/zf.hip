@@ -1119,18 +1119,22 @@ k_zf_mfma_w128(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__
 // XMAP: block b runs on XCD b % 8 (round-robin dispatch; speed only): the
 // chunk is b % 8 + 8 (b / (8 nkb)) and the subcarrier block (b / 8) % nkb, so
 // one XCD reads all subcarrier pieces of the same symbol rows.
-template <bool CONJ, bool XMAP = false>
-__global__ void __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(2, 2)))
+template <bool CONJ, bool XMAP = false, int MR = 16>
+__global__ void __attribute__((amdgpu_flat_work_group_size(MR == 64 ? 256 : 512, MR == 64 ? 256 : 512),
+                               amdgpu_waves_per_eu(MR == 64 ? 1 : 2, MR == 64 ? 1 : 2)))
 k_zf_wstat(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__restrict__ in, int N, int M, int K,
            long long nsym, float2 *__restrict__ out, int nkb, int nmb, long long chunk_syms) {
-    constexpr int MP = 8, SG = 4, SW = 4 * SG, PD = 3;
-    extern __shared__ __attribute__((aligned(16))) float2 smd[];  // [N][16][16]
+    // MR rows per tile: 16 (MP = 8 row pairs x SG = 4 symbol quads per wave) or
+    // 64 (apply at U = 16: all R = 64 output rows, MP = 32 x SG = 1)
+    // MR = 64: 4-wave workgroups, one wave per SIMD (512 registers for 128 accumulators + 32 A pairs)
+    constexpr int MP = MR / 2, SG = MR == 16 ? 4 : 1, SW = 4 * SG, PD = 3, TR = MR * 16, NW = MR == 64 ? 4 : 8;
+    extern __shared__ __attribute__((aligned(16))) float2 smd[];  // [N][MR][16]
     // tile = (subcarrier block, 16-row block); the row blocks of one subcarrier
     // block are adjacent in dispatch order, so they read the same input rows
     // at about the same time (the second read hits L2)
     const long long ntl = (long long)nkb * nmb;
     const int tl = XMAP ? (int)((blockIdx.x >> 3) % ntl) : (int)(blockIdx.x % ntl);
-    const int kb = tl / nmb, mb = tl % nmb, mr0 = 16 * mb;
+    const int kb = tl / nmb, mb = tl % nmb, mr0 = MR * mb;
     const long long chunk = XMAP ? (long long)(blockIdx.x & 7) + 8LL * (blockIdx.x / (8LL * ntl))
                                  : (long long)(blockIdx.x / ntl);
     const int lane = threadIdx.x & 63, b = lane >> 2, i = lane & 3;
@@ -1139,17 +1143,17 @@ k_zf_wstat(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__rest
     const long long sbeg = chunk * chunk_syms, send = min(sbeg + chunk_syms, nsym);
     if (sbeg >= send) return;  // whole workgroup
     // A tile -> LDS: element (n, m, bb) = A_k0+bb(m, n), rows m >= M zero
-    for (int e = threadIdx.x; e < N * 256; e += 512) {
-        const int bb = e & 15, m = mr0 + ((e >> 4) & 15), n = e >> 8;
+    for (int e = threadIdx.x; e < N * TR; e += 64 * NW) {
+        const int bb = e & 15, m = mr0 + ((e >> 4) % MR), n = e / TR;
         const int kk = min(k0 + bb, K - 1);
         smd[e] = m < M ? Wt[((long long)m * a_m + (long long)n * a_n) * K + kk] : float2{0.f, 0.f};
     }
     __syncthreads();
     const bool odd = i & 1;
     const long long NK = (long long)N * K;
-    const float2 *wl = smd + (i >> 1) * 16 + b;  // + n * 256 + 2 p * 16
+    const float2 *wl = smd + (i >> 1) * 16 + b;  // + n * TR + 2 p * 16
 
-    for (long long s0 = sbeg + (long long)w * SW; s0 < send; s0 += 8LL * SW) {
+    for (long long s0 = sbeg + (long long)w * SW; s0 < send; s0 += (long long)NW * SW) {
         const float2 *xrow[SG];
 #pragma unroll
         for (int g = 0; g < SG; ++g) xrow[g] = in + min(s0 + 4 * g + i, send - 1) * NK + kc;
@@ -1168,30 +1172,36 @@ k_zf_wstat(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__rest
             for (int d = 0; d < PD; ++d) {
                 const int n = n0 + d;
                 if (n < N) {  // wave-uniform
-                    float are[MP], aim[MP];
-#pragma unroll
-                    for (int p = 0; p < MP; ++p) {
-                        const float2 wv = wl[n * 256 + 2 * p * 16];
-                        const float wy = CONJ ? -wv.y : wv.y;
-                        are[p] = odd ? wy : wv.x;
-                        aim[p] = odd ? wv.x : -wy;
-                    }
                     float2 xv[SG];
 #pragma unroll
                     for (int g = 0; g < SG; ++g) xv[g] = xq[d][g];
                     const int nn = min(n + PD, N - 1);  // refill this slot PD steps ahead
 #pragma unroll
                     for (int g = 0; g < SG; ++g) xq[d][g] = xrow[g][(long long)nn * K];
+                    // row pairs in groups of 4: only one group's A operands live
 #pragma unroll
-                    for (int p = 0; p < MP; ++p)
+                    for (int p0 = 0; p0 < MP; p0 += 4) {
+                        float are[4], aim[4];
 #pragma unroll
-                        for (int g = 0; g < SG; ++g)
-                            acc[p][g] = __builtin_amdgcn_mfma_f32_4x4x1f32(are[p], xv[g].x, acc[p][g], 0, 0, 0);
+                        for (int p = 0; p < 4; ++p) {
+                            const float2 wv = wl[n * TR + 2 * (p0 + p) * 16];
+                            const float wy = CONJ ? -wv.y : wv.y;
+                            are[p] = odd ? wy : wv.x;
+                            aim[p] = odd ? wv.x : -wy;
+                        }
 #pragma unroll
-                    for (int p = 0; p < MP; ++p)
+                        for (int p = 0; p < 4; ++p)
 #pragma unroll
-                        for (int g = 0; g < SG; ++g)
-                            acc[p][g] = __builtin_amdgcn_mfma_f32_4x4x1f32(aim[p], xv[g].y, acc[p][g], 0, 0, 0);
+                            for (int g = 0; g < SG; ++g)
+                                acc[p0 + p][g] =
+                                    __builtin_amdgcn_mfma_f32_4x4x1f32(are[p], xv[g].x, acc[p0 + p][g], 0, 0, 0);
+#pragma unroll
+                        for (int p = 0; p < 4; ++p)
+#pragma unroll
+                            for (int g = 0; g < SG; ++g)
+                                acc[p0 + p][g] =
+                                    __builtin_amdgcn_mfma_f32_4x4x1f32(aim[p], xv[g].y, acc[p0 + p][g], 0, 0, 0);
+                    }
                 }
             }
         }
@@ -1420,11 +1430,11 @@ hipError_t mfma_w128_launch(const float2 *Wt, int a_m, int a_n, const float2 *in
     return hipGetLastError();
 }
 
-template <bool CONJ, bool XMAP>
+template <bool CONJ, bool XMAP, int MR = 16>
 hipError_t wstat_launch(const float2 *Wt, int a_m, int a_n, const float2 *in, int N, int M, int K,
                         long long nsym, float2 *out, hipStream_t s) {
-    const size_t lds = (size_t)N * 256 * sizeof(float2);  // N <= 72: <= 144 KiB
-    const int nkb = (K + 15) / 16, nmb = (M + 15) / 16;
+    const size_t lds = (size_t)N * MR * 16 * sizeof(float2);  // N * MR <= 1152: <= 144 KiB
+    const int nkb = (K + 15) / 16, nmb = (M + MR - 1) / MR;
     // ~1 workgroup per CU over all (tile, symbol chunk) pairs;
     // XMAP: a multiple of 8 chunks (one per XCD)
     long long nchunk = XMAP ? 8 : (256 + nkb * nmb - 1) / (nkb * nmb);
@@ -1434,7 +1444,7 @@ hipError_t wstat_launch(const float2 *Wt, int a_m, int a_n, const float2 *in, in
     if (XMAP) nchunk = (nchunk + 7) / 8 * 8;  // empty chunks return at once
     const long long blocks = (long long)nkb * nmb * nchunk;
     if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
-    auto kern = zf::k_zf_wstat<CONJ, XMAP>;
+    auto kern = zf::k_zf_wstat<CONJ, XMAP, MR>;
     static bool attr = false;
     if (!attr) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
@@ -1442,8 +1452,8 @@ hipError_t wstat_launch(const float2 *Wt, int a_m, int a_n, const float2 *in, in
         if (e != hipSuccess) return e;
         attr = true;
     }
-    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(512), lds, s, Wt, a_m, a_n, in, N, M, K, nsym, out, nkb,
-                       nmb, chunk_syms);
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(MR == 64 ? 256 : 512), lds, s, Wt, a_m, a_n, in, N, M, K,
+                       nsym, out, nkb, nmb, chunk_syms);
     return hipGetLastError();
 }
 
@@ -1475,6 +1485,8 @@ hipError_t gemm_dispatch(const float2 *Wt, int a_m, int a_n, const float2 *in, i
     // =8 / 9: W-stationary MFMA (N <= 72; 16-row blocks), 9 with one symbol chunk per XCD
     if (mode == 8 && N <= 72) return wstat_launch<CONJ, false>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
     if (mode == 9 && N <= 72) return wstat_launch<CONJ, true>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+    // =10: W-stationary with 64-row tiles (N <= 18), one symbol chunk per XCD
+    if (mode == 10 && N <= 18) return wstat_launch<CONJ, true, 64>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
     if (mode == 4) {
         if (env_int("OFDM_ZF_SG", 4) == 8) return mfma_lds_launch<8, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
         return mfma_lds_launch<4, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);

@@ -76,7 +76,7 @@ def main():
                         "mfma_sg8": {"OFDM_ZF_LDS": "3", "OFDM_ZF_SG": "8"},
                         "mfma_lds_sg4": {"OFDM_ZF_LDS": "4", "OFDM_ZF_SG": "4"},
                         "mfma_lds_sg8": {"OFDM_ZF_LDS": "4", "OFDM_ZF_SG": "8"},
-                        "mfma_lds8": {"OFDM_ZF_LDS": "5"}, "mfma_lds8_m32": {"OFDM_ZF_LDS": "6"}, "mfma_w128": {"OFDM_ZF_LDS": "7"}, "mfma_wstat": {"OFDM_ZF_LDS": "8"}, "mfma_wstat_xmap": {"OFDM_ZF_LDS": "9"}, "lds_xmap": {"OFDM_ZF_LDS": "1", "OFDM_ZF_XMAP": "1"},
+                        "mfma_lds8": {"OFDM_ZF_LDS": "5"}, "mfma_lds8_m32": {"OFDM_ZF_LDS": "6"}, "mfma_w128": {"OFDM_ZF_LDS": "7"}, "mfma_wstat": {"OFDM_ZF_LDS": "8"}, "mfma_wstat_xmap": {"OFDM_ZF_LDS": "9"}, "mfma_wstat64": {"OFDM_ZF_LDS": "10"}, "lds_xmap": {"OFDM_ZF_LDS": "1", "OFDM_ZF_XMAP": "1"},
                         "diag_nomac_lds_sg4": {"OFDM_ZF_LDS": "4", "OFDM_ZF_SG": "4", "OFDM_ZF_DEBUG": "1"}}
             for rnd in range(2):
                 for key, env in variants.items():

@@ -53,7 +53,7 @@ def test_zf_precoder_single_output(ofdm, dev):
                                      (16, 64, 1023, 100), (17, 64, 65, 3), (32, 64, 255, 25),
                                      (16, 100, 1023, 8)])
 # LDS tiles (default) / per-wave registers / DMA-fed LDS / 8x4 LDS / matrix cores from L1 (3 symbol-quad counts) / through LDS (2 + two 8-wave + 128-subcarrier / W-stationary)
-@pytest.mark.parametrize("lds", ["1", "0", "2", "1st4", "3", "3sg2", "3sg8", "4", "4sg8", "5", "6", "7", "8", "9", "1xmap"])
+@pytest.mark.parametrize("lds", ["1", "0", "2", "1st4", "3", "3sg2", "3sg8", "4", "4sg8", "5", "6", "7", "8", "9", "10", "1xmap"])
 def test_zf_apply_detect_parity(ofdm, oracle, dev, monkeypatch, U, R, K, n, lds):
     monkeypatch.setenv("OFDM_ZF_LDS", lds[0])
     if lds.endswith("st4"):
