@@ -53,9 +53,13 @@ def test_zf_precoder_single_output(ofdm, dev):
                                      (16, 64, 1023, 100), (17, 64, 65, 3), (32, 64, 255, 25),
                                      (16, 100, 1023, 8)])
 # LDS tiles (default) / per-wave registers / DMA-fed LDS / 8x4 LDS / matrix cores from L1 (3 symbol-quad counts) / through LDS (2 + two 8-wave + 128-subcarrier / W-stationary)
-@pytest.mark.parametrize("lds", ["1", "0", "2", "1st4", "3", "3sg2", "3sg8", "4", "4sg8", "5", "6", "7", "8", "9", "10", "1xmap"])
+@pytest.mark.parametrize("lds", ["1", "0", "2", "1st4", "3", "3sg2", "3sg8", "4", "4sg8", "5", "6", "7", "8", "9", "10", "1xmap", "default"])
 def test_zf_apply_detect_parity(ofdm, oracle, dev, monkeypatch, U, R, K, n, lds):
-    monkeypatch.setenv("OFDM_ZF_LDS", lds[0])
+    if lds == "default":  # the shape-based dispatch with no knob set
+        for v in ("OFDM_ZF_LDS", "OFDM_ZF_ST", "OFDM_ZF_SG", "OFDM_ZF_XMAP", "OFDM_ZF_DEBUG"):
+            monkeypatch.delenv(v, raising=False)
+    else:
+        monkeypatch.setenv("OFDM_ZF_LDS", lds[:2] if lds[:2].isdigit() else lds[0])
     if lds.endswith("st4"):
         monkeypatch.setenv("OFDM_ZF_ST", "4")
     if "sg" in lds:
