@@ -404,6 +404,9 @@ k_mrc_td1024_hlds(const float2 *__restrict__ iq, int S, int R, int prefix,
     const long long pb = blockIdx.x;
     const long long lb = (pb & 7) * per_xcd + (pb >> 3);  // XCD-grouped logical block
     if (lb >= nblocks) return;
+    // mode bit 3 (OFDM_MRC_PRIO=1, A/B): the second-dispatched half of the
+    // workgroup at priority 1 (MI355X_MICROARCH.md, two waves per SIMD, item 4)
+    if ((mode & 8) && w >= HW / 2) __builtin_amdgcn_s_setprio(1);
     fill(tw1, tw2);
     __syncthreads();
 
@@ -623,6 +626,7 @@ hipError_t launch_mrc_td1024(const float2 *iq, long long nframes, int S, int R, 
     const int sync = knob("OFDM_MRC_SYNC", 0), hlds_on = knob("OFDM_MRC_HLDS", 1);
     if (knob("OFDM_MRC_NTSTORE", 0)) mode |= 2;  // bit 1: nontemporal output stores
     if (!knob("OFDM_MRC_OSTAGE", 1)) mode |= 4;  // bit 2: HLDS stores outputs without LDS staging
+    if (knob("OFDM_MRC_PRIO", 0)) mode |= 8;     // bit 3: HLDS younger half at s_setprio 1
     const long long nblocks = (nq + W - 1) / W;
     const long long per_xcd = (nblocks + 7) / 8;
     long long grid = per_xcd * 8;
