@@ -660,15 +660,10 @@ hipError_t launch_mrc_td1024(const float2 *iq, long long nframes, int S, int R, 
         const long long pxcd = (nb + 7) / 8;
         if (pxcd * 8 > 0x7fffffffll) return hipErrorInvalidValue;
         if (hw == 16) {
-            static bool attr = false;  // > 64 KiB of dynamic LDS must be opted into once
-            if (!attr) {
-                for (const void *k : {reinterpret_cast<const void *>(&k_mrc_td1024_hlds<true, true, 0, 16, false>),
-                                      reinterpret_cast<const void *>(&k_mrc_td1024_hlds<true, true, 0, 16, true>)}) {
-                    hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                       (int)hlds_lds_bytes<16>());
-                    if (e != hipSuccess) return e;
-                }
-                attr = true;
+            for (const void *k : {reinterpret_cast<const void *>(&k_mrc_td1024_hlds<true, true, 0, 16, false>),
+                                  reinterpret_cast<const void *>(&k_mrc_td1024_hlds<true, true, 0, 16, true>)}) {
+                hipError_t e = opt_in_lds(k, (int)hlds_lds_bytes<16>());
+                if (e != hipSuccess) return e;
             }
             if (align)
                 hipLaunchKernelGGL((k_mrc_td1024_hlds<true, true, 0, 16, true>), dim3((unsigned)(pxcd * 8)),

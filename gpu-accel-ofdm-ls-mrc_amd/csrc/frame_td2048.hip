@@ -464,12 +464,7 @@ hipError_t launch_mrc_td2048(const float2 *iq, long long nframes, int S, int R, 
                          : hv == 2 ? reinterpret_cast<const void *>(&k_mrc_td2048h<true, true>)
                                    : reinterpret_cast<const void *>(&k_mrc_td2048h<true, true, 4>);
         const size_t lb = hv == 4 ? HLay<4>::LDS : HLay<H_WAVES>::LDS;
-        static bool attr[5] = {false, false, false, false, false};  // > 64 KiB of dynamic LDS: opt in once
-        if (!attr[hv]) {
-            hipError_t e = hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lb);
-            if (e != hipSuccess) return e;
-            attr[hv] = true;
-        }
+        if (hipError_t e = opt_in_lds(kf, (int)lb); e != hipSuccess) return e;  // > 64 KiB of dynamic LDS
         if (hv == 1)
             hipLaunchKernelGGL((k_mrc_td2048h<true, false>), dim3((unsigned)(pxcd * 8)), dim3(64 * hw), lb, s, iq,
                                S, R, prefix, Hc, P, out, nb, pxcd, mode);

@@ -591,14 +591,10 @@ hipError_t launch_mrc_td4096(const float2 *iq, long long nframes, int S, int R, 
     if (knob("OFDM_MRC4K_H", 1)) {
         const long long bpf = ((S - 1) + H_PAIRS - 1) / H_PAIRS, nb = nframes * bpf, pxcd = (nb + 7) / 8;
         if (pxcd * 8 > 0x7fffffffll) return hipErrorInvalidValue;
-        static bool attr = false;  // > 64 KiB of dynamic LDS: opt in once per kernel
-        if (!attr) {
-            for (const void *k : {reinterpret_cast<const void *>(&k_mrc_td4096h<true, 7>),
-                                  reinterpret_cast<const void *>(&k_mrc_td4096h<true, 0>)}) {
-                hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)H_LDS);
-                if (e != hipSuccess) return e;
-            }
-            attr = true;
+        for (const void *k : {reinterpret_cast<const void *>(&k_mrc_td4096h<true, 7>),
+                              reinterpret_cast<const void *>(&k_mrc_td4096h<true, 0>)}) {
+            hipError_t e = opt_in_lds(k, (int)H_LDS);  // > 64 KiB of dynamic LDS
+            if (e != hipSuccess) return e;
         }
         if (knob("OFDM_MRC4K_PK", 7) == 0)
             hipLaunchKernelGGL((k_mrc_td4096h<true, 0>), dim3((unsigned)(pxcd * 8)), dim3(128 * H_PAIRS), H_LDS,

@@ -6,7 +6,28 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <mutex>
+#include <set>
+#include <tuple>
+
 namespace ofdm {
+
+// Opts `kernel` into `bytes` of dynamic LDS (launches above 64 KiB need it)
+// once per (kernel, device, size) in this process; thread-safe, so a process
+// driving several GPUs or launching from several host threads is covered.
+inline hipError_t opt_in_lds(const void *kernel, int bytes) {
+    static std::mutex mu;
+    static std::set<std::tuple<const void *, int, int>> done;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lock(mu);
+    const auto key = std::make_tuple(kernel, dev, bytes);
+    if (done.count(key)) return hipSuccess;
+    e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e == hipSuccess) done.insert(key);
+    return e;
+}
 
 // Sets ofdm_last_error() for the calling thread and returns `code`.
 int set_error(int code, const char *msg);

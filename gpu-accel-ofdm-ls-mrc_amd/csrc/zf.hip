@@ -1232,11 +1232,9 @@ hipError_t launch_zf_precoder(const float2 *Hin, int U, int R, int K, float2 *W,
                               hipStream_t s) {
     if (K == 0) return hipSuccess;
     const size_t lds = zf_precoder_lds_bytes(U, R);
-    if (lds > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&zf::k_zf_precoder),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-    }
+    if (lds > 64 * 1024)
+        if (hipError_t e = opt_in_lds(reinterpret_cast<const void *>(&zf::k_zf_precoder), (int)lds); e != hipSuccess)
+            return e;
     hipLaunchKernelGGL(zf::k_zf_precoder, dim3(K), dim3(256), lds, s, Hin, U, R, K, W, Wt);
     return hipGetLastError();
 }
@@ -1364,13 +1362,8 @@ hipError_t mfma_lds_launch(const float2 *Wt, int a_m, int a_n, const float2 *in,
     const long long blocks = 8LL * tpx * nchunk;
     if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
     auto kern = env_int("OFDM_ZF_DEBUG", 0) == 1 ? zf::k_zf_mfma_lds<SG, CONJ, 1> : zf::k_zf_mfma_lds<SG, CONJ>;
-    static bool attr = false;  // > 64 KiB of dynamic LDS: opt in (debug variant: only SG = 4, 64 KiB)
-    if (!attr && lds > 64 * 1024) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
+    if (lds > 64 * 1024)
+        if (hipError_t e = opt_in_lds(reinterpret_cast<const void *>(kern), (int)lds); e != hipSuccess) return e;
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), lds, s, Wt, a_m, a_n, in, N, M, K, nsym, out,
                        ntile, tpx, nkb, chunk_steps);
     return hipGetLastError();
@@ -1391,13 +1384,7 @@ hipError_t mfma_lds8_launch(const float2 *Wt, int a_m, int a_n, const float2 *in
     const long long blocks = 8LL * tpx * nchunk;
     if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
     auto kern = zf::k_zf_mfma_lds8<MPW, SG, CONJ>;
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
+    if (hipError_t e = opt_in_lds(reinterpret_cast<const void *>(kern), (int)lds); e != hipSuccess) return e;
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(512), lds, s, Wt, a_m, a_n, in, N, M, K, nsym, out,
                        ntile, tpx, nkb, chunk_steps);
     return hipGetLastError();
@@ -1418,13 +1405,7 @@ hipError_t mfma_w128_launch(const float2 *Wt, int a_m, int a_n, const float2 *in
     const long long blocks = 8LL * tpx * nchunk;
     if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
     auto kern = zf::k_zf_mfma_w128<CONJ>;
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
+    if (hipError_t e = opt_in_lds(reinterpret_cast<const void *>(kern), (int)lds); e != hipSuccess) return e;
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(512), lds, s, Wt, a_m, a_n, in, N, M, K, nsym, out,
                        ntile, tpx, nkb, chunk_steps);
     return hipGetLastError();
@@ -1445,13 +1426,9 @@ hipError_t wstat_launch(const float2 *Wt, int a_m, int a_n, const float2 *in, in
     const long long blocks = (long long)nkb * nmb * nchunk;
     if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
     auto kern = zf::k_zf_wstat<CONJ, XMAP, MR>;
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 72 * 256 * (int)sizeof(float2));
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
+    if (hipError_t e = opt_in_lds(reinterpret_cast<const void *>(kern), 72 * 256 * (int)sizeof(float2));
+        e != hipSuccess)
+        return e;
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(MR == 64 ? 256 : 512), lds, s, Wt, a_m, a_n, in, N, M, K,
                        nsym, out, nkb, nmb, chunk_syms);
     return hipGetLastError();

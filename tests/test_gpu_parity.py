@@ -269,3 +269,35 @@ def test_stagewise_ops_vs_oracle(ofdm, oracle, dev, R, C):
     parity(np.stack([oracle.shift_one_row(u) for u in unrot]), ref)
     sh = host(ofdm.shift_rows(to_dev(unrot, dev)))
     parity(sh, ref)
+
+
+def test_concurrent_host_threads_large_lds_kernels(ofdm, dev):
+    """Kernels launched with > 64 KiB of dynamic LDS (the C = 4096 receiver,
+    the ZF matrix-core detect) opt in through a per-(kernel, device) cache
+    (launch.hpp opt_in_lds); several host threads launching them at once must
+    all succeed and agree (ctypes releases the GIL around the C calls)."""
+    import threading
+    import torch
+    X = to_dev(qpsk_pilots(4095), dev)
+    iq = ofdm.synth_frames(2, 3, 8, 4096, X, seed=11, noise_std=0.02)
+    ref = host(ofdm.frame_demod(iq, X))
+    outs, errs = [None] * 4, []
+
+    def work(i):
+        try:
+            st = torch.cuda.Stream(device=dev)
+            with torch.cuda.stream(st):
+                o = ofdm.frame_demod(iq, X, stream=st)
+            st.synchronize()
+            outs[i] = o.cpu().numpy()
+        except Exception as e:  # surfaced below
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    for o in outs:
+        assert np.array_equal(o, ref)
