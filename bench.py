@@ -142,6 +142,13 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    # rehearsal of the N > 1 path on fewer GPUs (tests only, never the
+    # measurement): OFDM_BENCH_SHARE_GPU=1 maps ranks onto the visible GPUs
+    # round-robin, OFDM_BENCH_BACKEND=gloo replaces RCCL (which refuses two
+    # ranks on one GPU)
+    if os.environ.get("OFDM_BENCH_SHARE_GPU") == "1":
+        local = local % max(1, torch.cuda.device_count())
+    backend = os.environ.get("OFDM_BENCH_BACKEND", "nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1 or args.mode == "split":
@@ -150,7 +157,10 @@ def main():
             os.environ.setdefault("MASTER_PORT", "29517")
             os.environ.setdefault("RANK", "0")
             os.environ.setdefault("WORLD_SIZE", "1")
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     def barrier():
         if world > 1:
