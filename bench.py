@@ -405,14 +405,16 @@ def bench_split(args, X, dev, world, rank, barrier):
     _, ws = ofdm.frame_ls_partial(iq, X, prefix)
     num = ofdm.c64((F, S - 1, K), dev)
     reps = 5
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(reps + 1)]
     ofdm.frame_mrc_partial(iq, ws, prefix, num=num)
-    e0.record(stream)
-    for _ in range(reps):
+    evs[0].record(stream)
+    for i in range(reps):
         ofdm.frame_mrc_partial(iq, ws, prefix, num=num)
-    e1.record(stream)
+        evs[i + 1].record(stream)
     torch.cuda.synchronize()
-    mrc_ms = e0.elapsed_time(e1) / reps
+    mrc_all = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(reps))
+    mrc_ms = sum(mrc_all) / reps
+    mrc_median = mrc_all[reps // 2]
     b_sym = R * C * 8 + K * 8
     achieved = Q * b_sym / (mrc_ms * 1e-3) / 1e9
     kern = {1024: "k_mrc_td1024_hlds", 2048: "k_mrc_td2048", 4096: "k_mrc_td4096h"}.get(C, "k_mrc_freq")
