@@ -119,7 +119,19 @@ class SplitPipeline:
         self.mine = [torch.empty(self.per, dtype=torch.complex64, device=device) for _ in range(2)]
 
     def run(self, shard, X, out, stream=None):
-        """shard: (F, S, R_local, C + prefix) on this rank; out: (F, S-1, K)."""
+        """shard: (F, S, R_local, C + prefix) on this rank; out: (F, S-1, K).
+        stream: a torch.cuda.Stream to run on (default: the current stream).
+        The whole step -- kernels, collectives and their waits -- is issued
+        with `stream` as torch's current stream, because the async
+        collectives and work.wait() order themselves against the current
+        stream: kernels on any other stream could race them."""
+        if stream is not None and self.ops is HipOps:
+            import torch
+            with torch.cuda.stream(stream):
+                return self._run(shard, X, out)
+        return self._run(shard, X, out)
+
+    def _run(self, shard, X, out, stream=None):
         import torch.distributed as dist
         F, S, K = self.F, self.S, self.K
         pending = []

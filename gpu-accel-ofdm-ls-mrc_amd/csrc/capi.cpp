@@ -5,6 +5,8 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 
 #include "../../include/ofdm_lsmrc.h"
@@ -92,6 +94,43 @@ int carve(void *d_ws, size_t bytes, long long F, int S, int R, int C, bool need_
     return OFDM_OK;
 }
 
+// What each frame workspace holds (host-side registry, per process): the
+// geometry of the estimate last stored in it, whether its Hc rows are in a
+// fused kernel's lane order and whether P is an antenna-split partial.  The
+// consumers (combine, mrc_partial, export) refuse a workspace whose estimate
+// was made for another geometry instead of dividing by the wrong |H|^2.
+struct WsTag {
+    long long F;
+    int S, R, C;
+    bool lane_order, partial;
+};
+std::mutex g_ws_mu;
+std::map<const void *, WsTag> g_ws;
+
+void ws_record(const void *ws, long long F, int S, int R, int C, bool lane_order, bool partial) {
+    std::lock_guard<std::mutex> lock(g_ws_mu);
+    g_ws[ws] = WsTag{F, S, R, C, lane_order, partial};
+}
+
+// need_full: the consumer divides by P, so a partial (antenna-split) P is refused
+int ws_check(const void *ws, long long F, int S, int R, int C, bool need_full, const char *fn,
+             WsTag *out = nullptr) {
+    std::lock_guard<std::mutex> lock(g_ws_mu);
+    auto it = g_ws.find(ws);
+    if (it == g_ws.end())
+        return fail(OFDM_E_ARG, "%s: the workspace holds no estimate (run ofdm_frame_estimate, "
+                                "ofdm_frame_demod or ofdm_frame_ls_partial on it first)", fn);
+    const WsTag &t = it->second;
+    if (t.F != F || t.S != S || t.R != R || t.C != C)
+        return fail(OFDM_E_ARG, "%s: the workspace estimate is for nframes=%lld S=%d R=%d C=%d, "
+                                "called with nframes=%lld S=%d R=%d C=%d", fn, t.F, t.S, t.R, t.C, F, S, R, C);
+    if (need_full && t.partial)
+        return fail(OFDM_E_ARG, "%s: the workspace holds a partial (antenna-split) |H|^2; "
+                                "finalise with ofdm_mrc_finalize instead", fn);
+    if (out) *out = t;
+    return OFDM_OK;
+}
+
 int check_frame_args(const void *in, long long F, int S, int R, int C, int prefix,
                      const void *out, const char *fn) {
     if (F < 0) return fail(OFDM_E_ARG, "%s: nframes < 0", fn);
@@ -152,6 +191,17 @@ int set_error(int code, const char *msg) {
     g_err = msg;
     return code;
 }
+#ifdef OFDM_AB_KNOBS
+int ab_knob(const char *name, int def) {  // OFDM_AB_<name>, read once
+    static std::mutex mu;
+    static std::map<std::string, int> cache;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = cache.find(name);
+    if (it != cache.end()) return it->second;
+    const char *v = getenv((std::string("OFDM_AB_") + name).c_str());
+    return cache[name] = (v && *v) ? atoi(v) : def;
+}
+#endif
 }  // namespace ofdm
 
 extern "C" {
@@ -294,9 +344,11 @@ int ofdm_frame_estimate(const ofdm_cf32 *d_iq, long long nframes, int S, int R, 
     if ((rc = carve(d_ws, ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
     hipStream_t s = hs(stream);
     if (fused_c(C))
-        return hip_check(ls_fused(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w.Hc, w.P, 0, s),
-                         "ls_fused");
-    return td_staged(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w, nullptr, 2, s);
+        rc = hip_check(ls_fused(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w.Hc, w.P, 0, s), "ls_fused");
+    else
+        rc = td_staged(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w, nullptr, 2, s);
+    if (rc == OFDM_OK) ws_record(d_ws, nframes, S, R, C, fused_c(C), false);
+    return rc;
 }
 
 int ofdm_frame_combine(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, int prefix,
@@ -304,6 +356,7 @@ int ofdm_frame_combine(const ofdm_cf32 *d_iq, long long nframes, int S, int R, i
     int rc = check_frame_args(d_iq, nframes, S, R, C, prefix, d_out, "ofdm_frame_combine");
     if (rc) return rc;
     if (nframes == 0) return OFDM_OK;
+    if ((rc = ws_check(d_ws, nframes, S, R, C, true, "ofdm_frame_combine"))) return rc;
     Workspace w;
     if ((rc = carve(d_ws, ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
     hipStream_t s = hs(stream);
@@ -325,6 +378,7 @@ int ofdm_frame_demod(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int
     Workspace w;
     if ((rc = carve(d_ws, ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
     hipStream_t s = hs(stream);
+    ws_record(d_ws, nframes, S, R, C, fused_c(C), false);
     if (fused_c(C)) {
         rc = hip_check(ls_fused(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w.Hc, w.P, 0, s),
                        "ls_fused");
@@ -347,6 +401,7 @@ int ofdm_frame_demod_freq(const ofdm_cf32 *d_Y, long long nframes, int S, int R,
     if ((rc = carve(d_ws, ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
     hipStream_t s = hs(stream);
     const long long fst = (long long)S * R * C;
+    ws_record(d_ws, nframes, S, R, C, false, false);
     rc = hip_check(ofdm::launch_ls_freq(F2(d_Y), fst, nframes, R, C, F2(d_X), w.Hc, (long long)R * C, C,
                                         1, w.P, C, 1, s),
                    "ls_freq");
@@ -355,6 +410,28 @@ int ofdm_frame_demod_freq(const ofdm_cf32 *d_Y, long long nframes, int S, int R,
                                            S - 1, R, C, w.Hc, (long long)R * C, C, 0, w.P, C, 1,
                                            F2(d_out), 0, s),
                      "mrc_freq");
+}
+
+int ofdm_frame_demod_freq_mfma(const ofdm_cf32 *d_Y, long long nframes, int S, int R, int C,
+                               const ofdm_cf32 *d_X, void *d_ws, size_t ws_bytes_, ofdm_cf32 *d_out,
+                               ofdm_stream_t stream) {
+    int rc = check_frame_args(d_Y, nframes, S, R, C, 0, d_out, "ofdm_frame_demod_freq_mfma");
+    if (rc) return rc;
+    if (C < 64) return fail(OFDM_E_UNSUPPORTED, "ofdm_frame_demod_freq_mfma: C=%d < 64", C);
+    if (!d_X) return fail(OFDM_E_ARG, "ofdm_frame_demod_freq_mfma: null pilots");
+    if (nframes == 0) return OFDM_OK;
+    Workspace w;
+    if ((rc = carve(d_ws, ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
+    hipStream_t s = hs(stream);
+    const long long fst = (long long)S * R * C;
+    ws_record(d_ws, nframes, S, R, C, false, false);
+    rc = hip_check(ofdm::launch_ls_freq(F2(d_Y), fst, nframes, R, C, F2(d_X), w.Hc, (long long)R * C, C,
+                                        1, w.P, C, 1, s),
+                   "ls_freq");
+    if (rc) return rc;
+    return hip_check(ofdm::launch_mrc_freq_mfma(F2(d_Y) + (long long)R * C, fst, (long long)R * C, nframes,
+                                                S - 1, R, C, w.Hc, (long long)R * C, w.P, C, F2(d_out), 0, s),
+                     "mrc_freq_mfma");
 }
 
 int ofdm_frame_ls_partial(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, int prefix,
@@ -373,6 +450,7 @@ int ofdm_frame_ls_partial(const ofdm_cf32 *d_iq, long long nframes, int S, int R
     else
         rc = td_staged(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w, nullptr, 2, s);
     if (rc) return rc;
+    ws_record(d_ws, nframes, S, R, C, fused_c(C), true);
     // bins 1..C-1 of the bin-layout P -> [F][K]
     const int K = C - 1;
     return hip_check(hipMemcpy2DAsync(d_P, K * sizeof(float), w.P + 1, C * sizeof(float),
@@ -386,6 +464,7 @@ int ofdm_frame_mrc_partial(const ofdm_cf32 *d_iq, long long nframes, int S, int 
     int rc = check_frame_args(d_iq, nframes, S, R, C, prefix, d_num, "ofdm_frame_mrc_partial");
     if (rc) return rc;
     if (nframes == 0) return OFDM_OK;
+    if ((rc = ws_check(d_ws, nframes, S, R, C, false, "ofdm_frame_mrc_partial"))) return rc;
     Workspace w;
     if ((rc = carve(d_ws, ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
     hipStream_t s = hs(stream);
@@ -394,6 +473,22 @@ int ofdm_frame_mrc_partial(const ofdm_cf32 *d_iq, long long nframes, int S, int 
                                                  F2(d_num), 1, s),
                          "mrc_fused");
     return td_staged(F2(d_iq), nframes, S, R, C, prefix, nullptr, w, F2(d_num), 1, s);
+}
+
+int ofdm_frame_export_estimate(const void *d_ws, size_t ws_bytes_, long long nframes, int S, int R, int C,
+                               long long frame, ofdm_cf32 *d_Hconj, float *d_Hsqrd, ofdm_stream_t stream) {
+    if (!d_Hconj) return fail(OFDM_E_ARG, "ofdm_frame_export_estimate: null d_Hconj");
+    if (nframes < 1 || frame < 0 || frame >= nframes)
+        return fail(OFDM_E_ARG, "ofdm_frame_export_estimate: frame %lld outside [0, %lld)", frame, nframes);
+    if (S < 2 || R < 1 || !pow2_c(C)) return fail(OFDM_E_ARG, "ofdm_frame_export_estimate: bad geometry");
+    WsTag tag;
+    int rc = ws_check(d_ws, nframes, S, R, C, false, "ofdm_frame_export_estimate", &tag);
+    if (rc) return rc;
+    Workspace w;
+    if ((rc = carve(const_cast<void *>(d_ws), ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
+    return hip_check(ofdm::launch_export_estimate(w.Hc + frame * R * C, w.P + frame * C, R, C, tag.lane_order,
+                                                  F2(d_Hconj), d_Hsqrd, hs(stream)),
+                     "ofdm_frame_export_estimate");
 }
 
 int ofdm_synth_frames(ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, int prefix,

@@ -15,9 +15,10 @@
 // Hc "lane order" for C = 4096: per (frame, antenna) 4096 float2 in planes
 // [e][h][k][t]: float2 e*2048 + h*1024 + k*64 + t = Hc[4 b + 2 h + e] with
 // b = b0(t) + 16 k -- each plane one coalesced 512-B wave load per k.
-// P bin-indexed [F][C].
+// P bin-indexed [F][C].  The LS kernel (one read per frame) uses the direct
+// form above, each wave reading the whole row.
 //
-// k_mrc_td4096x (default) instead reads every row ONCE per pair: radix-4
+// The MRC kernel (k_mrc_td4096h) reads every row ONCE per pair: radix-4
 // decimation in frequency, n = n0 + 1024 n1, z_c[n0] = sum_n1 x[n0 + 1024 n1]
 // (-i)^(c n1) W4096^(c n0), X[4 k + c] = FFT1024(z_c)[k].  Wave e loads
 // quarters e and e + 2 and forms s = x_e + x_(e+2), d = x_e - x_(e+2); the
@@ -27,8 +28,6 @@
 // z3 = (b + i d) W^(3 n0).  Same bin ownership as above.
 #include "launch.hpp"
 #include "wave_fft1024.hpp"
-
-#include <stdlib.h>
 
 namespace ofdm {
 namespace td4096 {
@@ -165,106 +164,13 @@ __global__ void __launch_bounds__(256) k_ls_td4096(const float2 *__restrict__ iq
 }
 
 // ---------------------------------------------------------------------------
-// MRC: a wave pair per data symbol, 2 symbols per 4-wave workgroup,
-// XCD-grouped block order.  mode 0: out[q][out_pos(j)] = acc / P;
-// mode 1: out[q][j] = acc (numerator).
-// ---------------------------------------------------------------------------
-constexpr int MRC_WAVES = 4;
-constexpr int MRC_SYMS = MRC_WAVES / 2;
-
-template <int E, bool NT, bool SYNC>
-__device__ __forceinline__ void mrc_symbol(const float2 *sym, int Cp, int R, const float2 *Hf,
-                                           const float *Pf, float2 *o, int mode, int t, float2 *T,
-                                           const float2 *lds, bool store) {
-    float2 ae[16], ao[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) ae[k] = ao[k] = float2{0.f, 0.f};
-    for (int r = 0; r < R; ++r) {
-        float2 xe[16], xo[16];
-        // SYNC: both waves of a pair request the row's lines together, so the
-        // second request hits L2 instead of going to the fabric again
-        if (SYNC) __syncthreads();
-        row_fft4096<E, NT>(sym + (long long)r * Cp, t, T, lds, xe, xo);
-        __builtin_amdgcn_sched_barrier(0);
-        const float2 *hr = Hf + (long long)r * C + E * 2048;
-        // matrixMultThenSum (cpuLS.hpp:203-204), antennas in order
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const float2 h0 = hr[k * 64 + t], h1 = hr[1024 + k * 64 + t];
-            const float4 h = float4{h0.x, h0.y, h1.x, h1.y};
-            ae[k].x = ae[k].x + (xe[k].x * h.x - xe[k].y * h.y);
-            ae[k].y = ae[k].y + (xe[k].x * h.y + xe[k].y * h.x);
-            ao[k].x = ao[k].x + (xo[k].x * h.z - xo[k].y * h.w);
-            ao[k].y = ao[k].y + (xo[k].x * h.w + xo[k].y * h.z);
-        }
-    }
-    if (!store) return;
-    const int b0 = lane_bin0(t);
-    if ((mode & 1) == 0) {
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const int be = 4 * (b0 + 16 * k) + E;
-            if (be > 0) {
-                const float pv = Pf[be];
-                o[out_pos(be - 1, K)] = float2{ae[k].x / pv, ae[k].y / pv};
-            }
-            const float pv = Pf[be + 2];
-            o[out_pos(be + 1, K)] = float2{ao[k].x / pv, ao[k].y / pv};
-        }
-    } else {
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const int be = 4 * (b0 + 16 * k) + E;
-            if (be > 0) o[be - 1] = ae[k];
-            o[be + 1] = ao[k];
-        }
-    }
-}
-
-template <bool NT, bool SYNC>
-__global__ void __attribute__((amdgpu_flat_work_group_size(256, 256), amdgpu_waves_per_eu(2, 2)))
-k_mrc_td4096(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
-             const float *__restrict__ P, float2 *__restrict__ out, long long nq, long long nblocks,
-             long long per_xcd, int mode) {
-    extern __shared__ __attribute__((aligned(16))) float2 lds[];
-    const int w = threadIdx.x >> 6, t = threadIdx.x & 63;
-    float2 *T = lds + TAB + w * hl::TS;
-    const long long pb = blockIdx.x;
-    const long long lb = (pb & 7) * per_xcd + (pb >> 3);
-    if (lb >= nblocks) return;
-    fill_tables(lds);
-    __syncthreads();
-    const long long qw = lb * MRC_SYMS + (w >> 1);
-    const bool store = qw < nq;
-    if (!SYNC && !store) return;  // no block-level sync follows
-    // SYNC: tail pairs repeat the last symbol (without storing) so that every
-    // wave takes part in the per-row barriers
-    const long long q = store ? qw : nq - 1;
-
-    const int nsym = S - 1;
-    const long long f = q / nsym;
-    const int s = 1 + (int)(q % nsym);
-    const int Cp = C + prefix;
-    const float2 *sym = iq + (f * S + s) * (long long)R * Cp + prefix;
-    const float2 *Hf = Hc + f * (long long)R * C;
-    const float *Pf = P + f * C;
-    float2 *o = out + q * K;
-    if (w & 1)
-        mrc_symbol<1, NT, SYNC>(sym, Cp, R, Hf, Pf, o, mode, t, T, lds, store);
-    else
-        mrc_symbol<0, NT, SYNC>(sym, Cp, R, Hf, Pf, o, mode, t, T, lds, store);
-}
-
-// ---------------------------------------------------------------------------
-// MRC, one read per row (k_mrc_td4096x): a workgroup is ONE wave pair = one
-// data symbol, so the two LDS barriers per row involve just the pair.  LDS:
-// the radix-16 twiddle tables + two transpose images (25.6 KiB: 6 groups per
-// CU); the DIF twiddles W4096^(c n0), n0 = t + 64 m, are the lane's
+// MRC, one read per row: a wave PAIR per data symbol (see the header: radix-4
+// DIF, wave e loads quarters e and e + 2, the pair swaps one half through
+// LDS).  The DIF twiddles W4096^(c n0), n0 = t + 64 m, are the lane's
 // W4096^(c t) times the compile-time W64^(c m).  PK: packed-f32 arithmetic
 // (pk.hpp) in the split and both FFT halves.
 // ---------------------------------------------------------------------------
 constexpr int X_TAB = hl::TW1S + hl::TW2S;
-constexpr size_t X_LDS = (size_t)(X_TAB + 2 * hl::TS) * sizeof(float2);
 
 template <int CM, int M>
 __device__ __forceinline__ pk::v2f dif_tw(pk::v2f base) {  // base * W64^(CM * M)
@@ -287,18 +193,17 @@ __device__ __forceinline__ void dma_hc_row(const float2 *g, unsigned lds) {
 
 // One antenna row for wave E of the pair.  On entry a/b hold the row's
 // quarters E and E + 2; with PREF the next row's quarters are loaded into
-// them after the first FFT (behind this row's Hc loads: loads retire in
-// order) and stay in flight through the second FFT and MAC.
-// HL (k_mrc_td4096h): hr points at this row's Hc in LDS, DMA'd during the
-// previous row; this row's first barrier publishes it (after vmcnt(0)) and
-// the DMA of row r+1 (hnext, into LDS byte address hb_next) is issued right
-// after that barrier, into the buffer every wave finished with in row r-1.
-template <int E, bool NT, int PK, bool PREF, int DBG = 0, bool HL = false>
+// them after the first FFT and stay in flight through the second FFT and
+// MAC.  hr points at this row's Hc in LDS, DMA'd during the previous row;
+// this row's first barrier publishes it (after vmcnt(0)) and the DMA of row
+// r+1 (hnext, into LDS byte address hb_next) is issued right after that
+// barrier, into the buffer every wave finished with in row r-1.
+template <int E, int PK, bool PREF>
 __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const float2 *__restrict__ hr,
                                       int t, float2 *T, const float2 *Tp, const float2 *tw1,
                                       const float2 *tw2, pk::v2f wb0, pk::v2f wb1, float2 (&a)[16],
                                       float2 (&b)[16], float2 (&ae)[16], float2 (&ao)[16],
-                                      const float2 *hnext = nullptr, unsigned hb_next = 0) {
+                                      const float2 *hnext, unsigned hb_next) {
     using namespace pk;
     v2f u[16], v[16];
 #pragma unroll
@@ -307,18 +212,12 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
         v[m] = sub(V(a[m]), V(b[m]));  // d
     }
     float2 h[16], h1[16];
-    if constexpr (!HL) {
-#pragma unroll
-        for (int k = 0; k < 16; ++k)  // plane 0: bins 4 b + E (DBG & 2: diagnostic, no Hc traffic)
-            h[k] = (DBG & 2) ? float2{1.f, (float)k} : hr[k * 64 + t];
-    }
     // wave 0 sends d and keeps s (= a); wave 1 sends s (= c) and keeps d
 #pragma unroll
     for (int m = 0; m < 16; ++m) T[hl::swz(m, t)] = F(E ? u[m] : v[m]);
-    if constexpr (HL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this row's Hc DMA landed
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this row's Hc DMA landed
     td1024::lds_barrier();
-    if constexpr (HL)
-        if (hnext) dma_hc_row(hnext, hb_next);
+    if (hnext) dma_hc_row(hnext, hb_next);
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
         if (E) u[m] = V(Tp[hl::swz(m, t)]);  // b
@@ -371,19 +270,16 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
     hl::row_fft_a<PK>(z, t, T, tw1);
     hl::row_fft_b<PK>(t, T, tw2, x);
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (HL) {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) h[k] = hr[k * 64 + t];  // plane 0 from LDS
-    }
+    for (int k = 0; k < 16; ++k) h[k] = hr[k * 64 + t];  // plane 0: bins 4 b + E, from LDS
 #pragma unroll
-    for (int k = 0; k < 16; ++k)  // plane 1: bins 4 b + 2 + E
-        h1[k] = (DBG & 2) ? float2{(float)k, 1.f} : hr[1024 + k * 64 + t];
+    for (int k = 0; k < 16; ++k) h1[k] = hr[1024 + k * 64 + t];  // plane 1: bins 4 b + 2 + E
     mac(ae);
     __builtin_amdgcn_sched_barrier(0);
     // next row in flight during the second FFT and the next row's exchange
     if (PREF) {
-        row_load<NT>(next + 1024 * E, t, a);
-        row_load<NT>(next + 1024 * (E + 2), t, b);
+        row_load<true>(next + 1024 * E, t, a);
+        row_load<true>(next + 1024 * (E + 2), t, b);
     }
 #pragma unroll
     for (int k = 0; k < 16; ++k) h[k] = h1[k];
@@ -394,86 +290,14 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
     mac(ao);
 }
 
-template <int E, bool NT, int PK, int DBG = 0>
-__device__ __forceinline__ void x_rows(const float2 *sym, int Cp, int R, const float2 *Hf, int t,
-                                       float2 *T, const float2 *Tp, const float2 *tw1,
-                                       const float2 *tw2, pk::v2f wb0, pk::v2f wb1,
-                                       float2 (&ae)[16], float2 (&ao)[16]) {
-    float2 a[16], b[16];
-    row_load<NT>(sym + 1024 * E, t, a);
-    row_load<NT>(sym + 1024 * (E + 2), t, b);
-    for (int r = 0; r + 1 < R; ++r)
-        x_row<E, NT, PK, true, DBG>(sym + (long long)(r + 1) * Cp, Hf + (long long)r * C, t, T, Tp, tw1,
-                               tw2, wb0, wb1, a, b, ae, ao);
-    x_row<E, NT, PK, false, DBG>(sym, Hf + (long long)(R - 1) * C, t, T, Tp, tw1, tw2, wb0, wb1, a, b,
-                            ae, ao);
-}
-
-template <bool NT, int PK, int WPE, int DBG = 0>
-__global__ void __attribute__((amdgpu_flat_work_group_size(128, 128), amdgpu_waves_per_eu(WPE, WPE)))
-k_mrc_td4096x(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
-              const float *__restrict__ P, float2 *__restrict__ out, long long nq, long long per_xcd,
-              int mode) {
-    extern __shared__ __attribute__((aligned(16))) float2 lds[];
-    const int e = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), t = threadIdx.x & 63;
-    const float2 *tw1 = lds, *tw2 = lds + hl::TW1S;
-    float2 *T = lds + X_TAB + e * hl::TS;
-    const float2 *Tp = lds + X_TAB + (e ^ 1) * hl::TS;
-    const long long pb = blockIdx.x;
-    const long long q = (pb & 7) * per_xcd + (pb >> 3);  // XCD-grouped symbol order
-    if (q >= nq) return;  // both waves of the pair leave together
-    hl::fill(lds, lds + hl::TW1S);
-    __syncthreads();
-
-    const int nsym = S - 1;
-    const long long f = q / nsym;
-    const int s = 1 + (int)(q % nsym);
-    const int Cp = C + prefix;
-    const float2 *sym = iq + (f * S + s) * (long long)R * Cp + prefix;
-    const float2 *Hf = Hc + f * (long long)R * C + e * 2048;
-    // lane bases of the DIF twiddles: wave 0 W4096^(2t); wave 1 W4096^t, W4096^(3t)
-    const pk::v2f wb0 = pk::V(g_tw[(e ? 1 : 2) * t]);
-    const pk::v2f wb1 = pk::V(g_tw[3 * t]);
-
-    float2 ae[16], ao[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) ae[k] = ao[k] = float2{0.f, 0.f};
-    if (e)
-        x_rows<1, NT, PK, DBG>(sym, Cp, R, Hf, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
-    else
-        x_rows<0, NT, PK, DBG>(sym, Cp, R, Hf, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
-    const int b0 = lane_bin0(t);
-    float2 *o = out + q * K;
-    const float *Pf = P + f * C;
-    if ((mode & 1) == 0) {
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const int be = 4 * (b0 + 16 * k) + e;
-            if (be > 0) {
-                const float pv = Pf[be];
-                o[out_pos(be - 1, K)] = float2{ae[k].x / pv, ae[k].y / pv};
-            }
-            const float pv = Pf[be + 2];
-            o[out_pos(be + 1, K)] = float2{ao[k].x / pv, ao[k].y / pv};
-        }
-    } else {
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const int be = 4 * (b0 + 16 * k) + e;
-            if (be > 0) o[be - 1] = ae[k];
-            o[be + 1] = ao[k];
-        }
-    }
-}
-
 // ---------------------------------------------------------------------------
 // MRC with the channel rows shared through LDS (k_mrc_td4096h): workgroup =
 // 4 wave pairs = 4 consecutive data symbols of ONE frame (frame-aligned block
 // map, bpf = ceil((S-1)/4) blocks per frame; tail pairs repeat the frame's
 // last symbol without storing), so the frame's 32 KiB Hc row is fetched once
 // per workgroup by LDS-DMA into a double buffer instead of by every wave
-// from L2 (k_mrc_td4096x: Hc traffic = IQ traffic; without it the kernel ran
-// 13 % faster, the diagnostic OFDM_MRC4K_DEBUG=2).  The pairs' two exchange
+// from L2 (round 1's one-pair-per-workgroup kernel: Hc traffic = IQ
+// traffic; a diagnostic without Hc loads ran 13 % faster).  The pairs' two exchange
 // barriers per row become workgroup barriers and also publish the Hc row.
 // LDS: tables 8 KiB + 8 transpose images 68 KiB + 2 x 32 KiB = 140 KiB, one
 // workgroup (8 waves, 2 per SIMD as the 242-VGPR x kernel) per CU.
@@ -482,23 +306,24 @@ constexpr int H_PAIRS = 4;
 constexpr size_t H_LDS = (size_t)(X_TAB + 2 * H_PAIRS * hl::TS + 2 * C) * sizeof(float2);
 static_assert(H_LDS <= 160 * 1024, "one workgroup per CU");
 
-template <int E, bool NT, int PK>
+template <int E, int PK>
 __device__ __forceinline__ void h_rows(const float2 *sym, int Cp, int R, const float2 *Hg, float2 *HB, int t,
                                        float2 *T, const float2 *Tp, const float2 *tw1, const float2 *tw2,
                                        pk::v2f wb0, pk::v2f wb1, float2 (&ae)[16], float2 (&ao)[16]) {
     float2 a[16], b[16];
-    row_load<NT>(sym + 1024 * E, t, a);
-    row_load<NT>(sym + 1024 * (E + 2), t, b);
+    row_load<true>(sym + 1024 * E, t, a);
+    row_load<true>(sym + 1024 * (E + 2), t, b);
     const unsigned hb0 = lds_addr(HB), hb1 = lds_addr(HB + C);
     for (int r = 0; r + 1 < R; ++r)
-        x_row<E, NT, PK, true, 0, true>(sym + (long long)(r + 1) * Cp, HB + (r & 1) * C + E * 2048, t, T, Tp,
+        x_row<E, PK, true>(sym + (long long)(r + 1) * Cp, HB + (r & 1) * C + E * 2048, t, T, Tp,
                                         tw1, tw2, wb0, wb1, a, b, ae, ao, Hg + (long long)(r + 1) * C,
                                         (r & 1) ? hb0 : hb1);
-    x_row<E, NT, PK, false, 0, true>(sym, HB + ((R - 1) & 1) * C + E * 2048, t, T, Tp, tw1, tw2, wb0, wb1, a,
+    x_row<E, PK, false>(sym, HB + ((R - 1) & 1) * C + E * 2048, t, T, Tp, tw1, tw2, wb0, wb1, a,
                                      b, ae, ao, nullptr, 0);
 }
 
-template <bool NT, int PK>
+constexpr int H_PK = 7;  // packed-f32 split, FFT halves and MAC (pk.hpp)
+
 __global__ void __attribute__((amdgpu_flat_work_group_size(128 * H_PAIRS, 128 * H_PAIRS),
                                amdgpu_waves_per_eu(2, 2)))
 k_mrc_td4096h(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
@@ -533,9 +358,9 @@ k_mrc_td4096h(const float2 *__restrict__ iq, int S, int R, int prefix, const flo
 #pragma unroll
     for (int k = 0; k < 16; ++k) ae[k] = ao[k] = float2{0.f, 0.f};
     if (e)
-        h_rows<1, NT, PK>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
+        h_rows<1, H_PK>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
     else
-        h_rows<0, NT, PK>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
+        h_rows<0, H_PK>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
     if (!store) return;
     const long long q = f * nsym + j;
     const int b0 = lane_bin0(t);
@@ -579,59 +404,12 @@ hipError_t launch_mrc_td4096(const float2 *iq, long long nframes, int S, int R, 
     using namespace td4096;
     const long long nq = nframes * (S - 1);
     if (nq <= 0) return hipSuccess;
-    const long long nblocks = (nq + MRC_SYMS - 1) / MRC_SYMS;
-    const long long per_xcd = (nblocks + 7) / 8;
-    const long long grid = per_xcd * 8;
-    if (grid > 0x7fffffffll) return hipErrorInvalidValue;
-    auto knob = [](const char *n, int d) { const char *v = getenv(n); return v ? atoi(v) : d; };
-    // OFDM_MRC4K_X=1 (default): k_mrc_td4096x, one row read per pair;
-    // OFDM_MRC4K_PK=0/7: scalar / packed-f32 (pk.hpp)
-    // OFDM_MRC4K_H=1 (default): k_mrc_td4096h, Hc rows shared by 4 pairs
-    // through LDS (same-process A/B: 10.92 vs 11.15 ms for the x kernel)
-    if (knob("OFDM_MRC4K_H", 1)) {
-        const long long bpf = ((S - 1) + H_PAIRS - 1) / H_PAIRS, nb = nframes * bpf, pxcd = (nb + 7) / 8;
-        if (pxcd * 8 > 0x7fffffffll) return hipErrorInvalidValue;
-        for (const void *k : {reinterpret_cast<const void *>(&k_mrc_td4096h<true, 7>),
-                              reinterpret_cast<const void *>(&k_mrc_td4096h<true, 0>)}) {
-            hipError_t e = opt_in_lds(k, (int)H_LDS);  // > 64 KiB of dynamic LDS
-            if (e != hipSuccess) return e;
-        }
-        if (knob("OFDM_MRC4K_PK", 7) == 0)
-            hipLaunchKernelGGL((k_mrc_td4096h<true, 0>), dim3((unsigned)(pxcd * 8)), dim3(128 * H_PAIRS), H_LDS,
-                               s, iq, S, R, prefix, Hc, P, out, nframes, nb, pxcd, mode);
-        else
-            hipLaunchKernelGGL((k_mrc_td4096h<true, 7>), dim3((unsigned)(pxcd * 8)), dim3(128 * H_PAIRS), H_LDS,
-                               s, iq, S, R, prefix, Hc, P, out, nframes, nb, pxcd, mode);
-        return hipGetLastError();
-    }
-    if (knob("OFDM_MRC4K_X", 1)) {
-        const long long xg = ((nq + 7) / 8) * 8;
-        if (xg > 0x7fffffffll) return hipErrorInvalidValue;
-        const int pkm = knob("OFDM_MRC4K_PK", 7);
-        const bool nt = knob("OFDM_MRC4K_NT", 1);
-#define OFDM_X_LAUNCH(NTV, PKV)                                                                 \
-    hipLaunchKernelGGL((k_mrc_td4096x<NTV, PKV, 2>), dim3((unsigned)xg), dim3(128), X_LDS, s, iq,   \
-                       S, R, prefix, Hc, P, out, nq, xg / 8, mode)
-        if (knob("OFDM_MRC4K_DEBUG", 0) == 2)  // diagnostic only (wrong results): no Hc traffic
-            hipLaunchKernelGGL((k_mrc_td4096x<true, 7, 2, 2>), dim3((unsigned)xg), dim3(128), X_LDS, s, iq, S,
-                               R, prefix, Hc, P, out, nq, xg / 8, mode);
-        else if (!nt) OFDM_X_LAUNCH(false, 7);
-        else if (pkm == 0) OFDM_X_LAUNCH(true, 0);
-        else OFDM_X_LAUNCH(true, 7);
-#undef OFDM_X_LAUNCH
-        return hipGetLastError();
-    }
-    // nontemporal row loads would evict the row before the partner wave reads
-    // it.  OFDM_MRC4K_SYNC=0/1 (default 1): per-row workgroup barrier.
-    const char *e = getenv("OFDM_MRC4K_SYNC");
-    if (e && e[0] == '0')
-        hipLaunchKernelGGL((k_mrc_td4096<false, false>), dim3((unsigned)grid), dim3(64 * MRC_WAVES),
-                           lds_bytes(MRC_WAVES), s, iq, S, R, prefix, Hc, P, out, nq, nblocks, per_xcd,
-                           mode);
-    else
-        hipLaunchKernelGGL((k_mrc_td4096<false, true>), dim3((unsigned)grid), dim3(64 * MRC_WAVES),
-                           lds_bytes(MRC_WAVES), s, iq, S, R, prefix, Hc, P, out, nq, nblocks, per_xcd,
-                           mode);
+    const long long bpf = ((S - 1) + H_PAIRS - 1) / H_PAIRS, nb = nframes * bpf, pxcd = (nb + 7) / 8;
+    if (pxcd * 8 > 0x7fffffffll) return hipErrorInvalidValue;
+    if (hipError_t e = opt_in_lds(reinterpret_cast<const void *>(&k_mrc_td4096h), (int)H_LDS); e != hipSuccess)
+        return e;  // > 64 KiB of dynamic LDS
+    hipLaunchKernelGGL(k_mrc_td4096h, dim3((unsigned)(pxcd * 8)), dim3(128 * H_PAIRS), H_LDS, s, iq, S, R, prefix,
+                       Hc, P, out, nframes, nb, pxcd, mode);
     return hipGetLastError();
 }
 

@@ -29,6 +29,17 @@ inline hipError_t opt_in_lds(const void *kernel, int bytes) {
     return e;
 }
 
+// Experiment switches.  The product library (make) has none: ab_knob() is the
+// compile-time default and no environment variable changes what a kernel
+// computes or which kernel runs.  The A/B build (make ab ->
+// lib/libofdm_lsmrc_ab.so, -DOFDM_AB_KNOBS) reads OFDM_AB_<name> once per
+// process, for same-process comparisons of candidate kernels in scripts/.
+#ifdef OFDM_AB_KNOBS
+int ab_knob(const char *name, int def);
+#else
+constexpr int ab_knob(const char *, int def) { return def; }
+#endif
+
 // Sets ofdm_last_error() for the calling thread and returns `code`.
 int set_error(int code, const char *msg);
 
@@ -99,6 +110,11 @@ hipError_t launch_combine(const float2 *prod, long long nsyms, int R, int K, con
                           int rotate, float2 *out, hipStream_t s);
 hipError_t launch_shift_rows(const float2 *in, long long nrows, int K, float2 *out, hipStream_t s);
 hipError_t launch_dist_sqrd(const float2 *H, int R, int K, float *P, hipStream_t s);
+// One frame's workspace estimate (Hc rows of C float2: lane_order = the
+// fused LS kernel for C wrote them, else bin layout; P bin-indexed) ->
+// Hconj [R][K], Hsqrd [K] (may be null).
+hipError_t launch_export_estimate(const float2 *Hc, const float *P, int R, int C, bool lane_order,
+                                  float2 *Hconj, float *Hsqrd, hipStream_t s);
 
 // Synthetic frames: time-domain (freq_domain=0, rows of C+prefix with a
 // cyclic prefix) or frequency-domain (freq_domain=1, rows of C) IQ.

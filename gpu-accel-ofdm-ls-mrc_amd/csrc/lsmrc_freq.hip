@@ -127,12 +127,6 @@ hipError_t launch_mrc_freq(const float2 *Y, long long frame_stride, long long sy
     if (blocks > 0x7fffffffll) return hipErrorInvalidValue;
     const bool bin = (hc_jofs == 0 && hc_ld == C && (hc_fstride % 2) == 0 &&
                       ((uintptr_t)Hc % 16) == 0);
-    // OFDM_MRC_FREQ_MFMA=1: the combine on the matrix cores (mrc_mfma.hip),
-    // kept for the configs[4] MFMA-vs-elementwise comparison
-    const char *mf = getenv("OFDM_MRC_FREQ_MFMA");
-    if (bin && p_jofs == 1 && mf && mf[0] == '1' && C >= 64)
-        return launch_mrc_freq_mfma(Y, frame_stride, sym_stride, nframes, nsym, R, C, Hc,
-                                    hc_fstride, P, p_fstride, out, mode, s);
     if (bin)
         hipLaunchKernelGGL(k_mrc_freq<true>, dim3((unsigned)blocks), dim3(threads), 0, s, Y,
                            frame_stride, sym_stride, nq, nsym, R, C, Hc, hc_fstride, hc_ld, hc_jofs,

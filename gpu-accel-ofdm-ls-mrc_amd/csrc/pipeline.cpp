@@ -64,9 +64,24 @@ int herr(hipError_t e, const char *fn, const char *what) {
         if (rc_) return rc_;                             \
     } while (0)
 
+// Makes the pipeline's device current for the scope of a call and restores
+// the caller's current device on every return path (a host thread driving
+// pipelines on several GPUs keeps its own device selection).
+struct DeviceGuard {
+    int prev = -1;
+    hipError_t e = hipSuccess;
+    explicit DeviceGuard(int dev) {
+        e = hipGetDevice(&prev);
+        if (e == hipSuccess && prev != dev) e = hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
 void release(ofdm_pipeline *p) {
     if (!p) return;
-    (void)hipSetDevice(p->device);
+    DeviceGuard dg(p->device);
     for (auto &s : p->slots) {
         if (s.iq) (void)hipFree(s.iq);
         if (s.out) (void)hipFree(s.out);
@@ -141,7 +156,8 @@ int ofdm_pipeline_acquire(ofdm_pipeline *p, ofdm_cf32 **d_iq, ofdm_stream_t *cop
     if (!p || !d_iq) return err(OFDM_E_ARG, fn, "null pointer");
     auto &s = p->slots[p->next];
     if (s.acquired) return err(OFDM_E_ARG, fn, "slot already acquired: submit it first");
-    PL_TRY(hipSetDevice(p->device), fn, "hipSetDevice");
+    DeviceGuard dg(p->device);
+    PL_TRY(dg.e, fn, "hipSetDevice");
     // the copy into this slot must not overwrite IQ its previous compute still reads
     if (s.used) PL_TRY(hipStreamWaitEvent(p->s_in, s.comp_done, 0), fn, "hipStreamWaitEvent");
     s.acquired = true;
@@ -156,7 +172,17 @@ int ofdm_pipeline_submit(ofdm_pipeline *p, long long nframes, ofdm_cf32 *out) {
     auto &s = p->slots[p->next];
     if (!s.acquired) return err(OFDM_E_ARG, fn, "no acquired slot");
     if (nframes < 0 || nframes > p->chunk) return err(OFDM_E_ARG, fn, "nframes out of [0, chunk_frames]");
-    PL_TRY(hipSetDevice(p->device), fn, "hipSetDevice");
+    DeviceGuard dg(p->device);
+    // any failure below releases the slot (its frames are not demodulated) so
+    // the pipeline stays usable: the next acquire hands out the same slot
+    struct Release {
+        ofdm_pipeline::Slot &s;
+        bool ok = false;
+        ~Release() {
+            if (!ok) s.acquired = false;
+        }
+    } rel{s};
+    PL_TRY(dg.e, fn, "hipSetDevice");
     PL_TRY(hipEventRecord(s.in_done, p->s_in), fn, "hipEventRecord");
     PL_TRY(hipStreamWaitEvent(p->s_comp, s.in_done, 0), fn, "hipStreamWaitEvent");
     if (s.used) PL_TRY(hipStreamWaitEvent(p->s_comp, s.out_done, 0), fn, "hipStreamWaitEvent");
@@ -172,6 +198,7 @@ int ofdm_pipeline_submit(ofdm_pipeline *p, long long nframes, ofdm_cf32 *out) {
                               hipMemcpyDefault, p->s_out),
                fn, "copy-out");
     PL_TRY(hipEventRecord(s.out_done, p->s_out), fn, "hipEventRecord");
+    rel.ok = true;
     s.used = true;
     s.acquired = false;
     p->next = (p->next + 1) % (int)p->slots.size();
@@ -200,7 +227,8 @@ int ofdm_pipeline_demod(ofdm_pipeline *p, const ofdm_cf32 *iq, long long nframes
 int ofdm_pipeline_sync(ofdm_pipeline *p) {
     static const char *fn = "ofdm_pipeline_sync";
     if (!p) return err(OFDM_E_ARG, fn, "null pipeline");
-    PL_TRY(hipSetDevice(p->device), fn, "hipSetDevice");
+    DeviceGuard dg(p->device);
+    PL_TRY(dg.e, fn, "hipSetDevice");
     PL_TRY(hipStreamSynchronize(p->s_in), fn, "sync copy-in");
     PL_TRY(hipStreamSynchronize(p->s_comp), fn, "sync compute");
     PL_TRY(hipStreamSynchronize(p->s_out), fn, "sync copy-out");

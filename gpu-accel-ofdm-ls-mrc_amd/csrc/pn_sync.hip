@@ -184,9 +184,9 @@ hipError_t launch_pn_correlate(const float2 *buf, int R, long long N, const floa
     const long long nblk = (nl + pn::TILE - 1) / pn::TILE;
     if (nblk * R > 0x7fffffffll) return hipErrorInvalidValue;
     auto *best = reinterpret_cast<unsigned long long *>(pos);
-    // packed exact MAC (A/B knob; both forms are bit-identical)
-    const char *kn = getenv("OFDM_PN_PK");
-    const bool pk = kn ? atoi(kn) != 0 : true;
+    // packed exact MAC (the scalar form, bit-identical and 5 % slower, is
+    // kept for the A/B build: OFDM_AB_PN_PK=0)
+    const bool pk = ab_knob("PN_PK", 1) != 0;
 #define OFDM_PN_LAUNCH(ST, PKV)                                                                  \
     hipLaunchKernelGGL((pn::k_pn_correlate<ST, PKV>), dim3((unsigned)(nblk * R)), dim3(pn::NT), 0, \
                        s, buf, N, pn, L, thres, nl, (int)nblk, best, mag)

@@ -11,6 +11,11 @@
 //   k_shift_rows     shiftOneRow (gpuLS.cu:109-125), out of place
 //   k_dist_sqrd      findDistSqrd (gpuLS.cu:185-209, cpuLS.hpp:211-228) on an
 //                    arbitrary R x K matrix, rows summed in order
+//   k_export_estimate one frame's LS estimate from a frame workspace (the
+//                    fused kernels' lane-ordered Hc rows, or the bin layout of
+//                    the staged path) into the reference's layout: Hconj
+//                    [R][K], Hsqrd [K] -- what demodOneFrameCUDA leaves in its
+//                    Hconj / Hsqrd arguments (gpuLS.cu:617-629)
 #include "common.hpp"
 #include "launch.hpp"
 
@@ -55,6 +60,52 @@ __global__ void __launch_bounds__(256) k_dist_sqrd(const float2 *__restrict__ H,
         p = (r == 0) ? (h.x * h.x) + (h.y * h.y) : p + (h.x * h.x) + (h.y * h.y);
     }
     P[j] = p;
+}
+
+// Position of bin b (1 <= b < C) inside one lane-ordered Hc row of C float2
+// (frame_td.hip / frame_td2048.hip / frame_td4096.hip: lane t of a wave owns
+// the bins b0(t) + 16 k, b0(t) = (t >> 2) + 256 c(t & 3), c(a) = (a >> 1) + 2 (a & 1)).
+// Other C: bin layout (position = b).
+__device__ __forceinline__ int lane_of(int b, int &k) {  // b < 1024
+    const int q = b & 15, c = b >> 8;
+    k = (b >> 4) & 15;
+    return 4 * q + (((c & 1) << 1) | (c >> 1));
+}
+__device__ __forceinline__ int hc_pos(int b, int C) {  // C = 0: bin layout
+    int k;
+    if (C == 1024) {  // float4 (k >> 1) * 64 + t holds bins (k & ~1, k | 1) of lane t
+        const int t = lane_of(b, k);
+        return 2 * ((k >> 1) * 64 + t) + (k & 1);
+    }
+    if (C == 2048) {  // float4 k * 64 + t = (Hc[2 b'], Hc[2 b' + 1]), b' = b0(t) + 16 k
+        const int t = lane_of(b >> 1, k);
+        return 2 * (k * 64 + t) + (b & 1);
+    }
+    if (C == 4096) {  // float2 e * 2048 + h * 1024 + k * 64 + t = Hc[4 b' + 2 h + e]
+        const int t = lane_of(b >> 2, k);
+        return (b & 1) * 2048 + ((b >> 1) & 1) * 1024 + k * 64 + t;
+    }
+    return b;
+}
+
+__global__ void __launch_bounds__(256) k_export_estimate(const float2 *__restrict__ Hc,
+                                                         const float *__restrict__ P, int R, int C,
+                                                         int lay, float2 *__restrict__ Hconj,
+                                                         float *__restrict__ Hsqrd) {
+    const int K = C - 1;
+    const int r = blockIdx.y;
+    for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < K; j += gridDim.x * blockDim.x) {
+        Hconj[(long long)r * K + j] = Hc[(long long)r * C + hc_pos(j + 1, lay)];
+        if (r == 0 && Hsqrd) Hsqrd[j] = P[j + 1];
+    }
+}
+
+hipError_t launch_export_estimate(const float2 *Hc, const float *P, int R, int C, bool lane_order,
+                                  float2 *Hconj, float *Hsqrd, hipStream_t s) {
+    if (R > 65535) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_export_estimate, dim3((unsigned)((C - 1 + 255) / 256), (unsigned)R), dim3(256), 0, s,
+                       Hc, P, R, C, lane_order ? C : 0, Hconj, Hsqrd);
+    return hipGetLastError();
 }
 
 static dim3 grid_rows(int K, long long rows) {

@@ -633,9 +633,7 @@ __device__ __forceinline__ void dma_rows8(const float *const (&g)[16], unsigned 
                  : "memory");
 }
 
-// DBG = 1: diagnostic only (wrong results) -- the data movement (DMA, LDS
-// reads, stores) without the MFMAs, bounding what the MAC side costs.
-template <int SG, bool CONJ, int DBG = 0>
+template <int SG, bool CONJ>
 __global__ void __attribute__((amdgpu_flat_work_group_size(256, 256), amdgpu_waves_per_eu(SG == 4 ? 2 : 1)))
 k_zf_mfma_lds(const float2 *__restrict__ Wt, int a_m, int a_n,
                                                      const float2 *__restrict__ in, int N, int M, int K,
@@ -728,12 +726,6 @@ k_zf_mfma_lds(const float2 *__restrict__ Wt, int a_m, int a_n,
             float2 xv[SG];
 #pragma unroll
             for (int g = 0; g < SG; ++g) xv[g] = sb[(MB + 4 * g + i) * 64];
-            if constexpr (DBG == 1) {
-#pragma unroll
-                for (int p = 0; p < MP; ++p)
-#pragma unroll
-                    for (int g = 0; g < SG; ++g) acc[p][g][g & 3] += are[p] * xv[g].x + aim[p] * xv[g].y;
-            } else {
 #pragma unroll
             for (int p = 0; p < MP; ++p)
 #pragma unroll
@@ -747,7 +739,6 @@ k_zf_mfma_lds(const float2 *__restrict__ Wt, int a_m, int a_n,
 #pragma unroll
                 for (int g = 0; g < SG; ++g)
                     acc[p][g] = __builtin_amdgcn_mfma_f32_4x4x1f32(aim[p], xv[g].y, acc[p][g], 0, 0, 0);
-            }
         }
         // store this step's tile and reset
         const long long s0 = (step0 + st) * SB;
@@ -1267,21 +1258,16 @@ hipError_t gemm_launch(const float2 *Wt, int a_m, int a_n, const float2 *in, int
     return hipGetLastError();
 }
 
-// A/B knobs, read per launch: OFDM_ZF_ST (symbols per register tile, 4 or 8)
-// and OFDM_ZF_PF (0 = no register double buffering).
-int env_int(const char *name, int def) {
-    const char *v = getenv(name);
-    return v && *v ? atoi(v) : def;
-}
-
 template <int MT, int MG, bool CONJ>
 hipError_t gemm_variant(const float2 *Wt, int a_m, int a_n, const float2 *in, int N, int M, int K,
                         long long nsym, float2 *out, hipStream_t s) {
-    const bool st4 = env_int("OFDM_ZF_ST", 8) == 4, pf = env_int("OFDM_ZF_PF", 1) != 0;
+#ifdef OFDM_AB_KNOBS  // ZF_ST=4: 4 symbols per register tile; ZF_PF=0: no register double buffering
+    const bool st4 = ab_knob("ZF_ST", 8) == 4, pf = ab_knob("ZF_PF", 1) != 0;
     if (st4) return pf ? gemm_launch<MT, 4, MG, CONJ, true>(Wt, a_m, a_n, in, N, M, K, nsym, out, s)
                        : gemm_launch<MT, 4, MG, CONJ, false>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-    return pf ? gemm_launch<MT, 8, MG, CONJ, true>(Wt, a_m, a_n, in, N, M, K, nsym, out, s)
-              : gemm_launch<MT, 8, MG, CONJ, false>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+    if (!pf) return gemm_launch<MT, 8, MG, CONJ, false>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+#endif
+    return gemm_launch<MT, 8, MG, CONJ, true>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
 }
 
 template <int MG, bool CONJ, bool DMA, int ST = 8>
@@ -1296,7 +1282,7 @@ hipError_t gemm_lds_launch(const float2 *Wt, int a_m, int a_n, const float2 *in,
     if (chunk_steps < 4) chunk_steps = 4;
     nchunk = (nsteps + chunk_steps - 1) / chunk_steps;
     const long long blocks = 8LL * tpx * nchunk;
-    if (env_int("OFDM_ZF_XMAP", 0) && ST == 8 && !DMA) {
+    if (ab_knob("ZF_XMAP", 0) && ST == 8 && !DMA) {
         const long long nc8 = (nchunk + 7) / 8 * 8;  // one chunk per XCD per round; empty chunks return
         hipLaunchKernelGGL((zf::k_zf_gemm_lds<MG, CONJ, false, 8, 2, true>), dim3((unsigned)(ntile * nc8)), dim3(256),
                            0, s, Wt, a_m, a_n, in, N, M, K, nsym, out, ntile, tpx, nkb, chunk_steps);
@@ -1308,7 +1294,7 @@ hipError_t gemm_lds_launch(const float2 *Wt, int a_m, int a_n, const float2 *in,
     else if (DMA)
         hipLaunchKernelGGL((zf::k_zf_gemm_dma<MG, CONJ>), dim3((unsigned)blocks), dim3(256), 0, s, Wt, a_m,
                            a_n, in, N, M, K, nsym, out, ntile, tpx, nkb, chunk_steps);
-    else if (env_int("OFDM_ZF_NT", 0))  // nontemporal input stream
+    else if (ab_knob("ZF_NT", 0))  // nontemporal input stream
         hipLaunchKernelGGL((zf::k_zf_gemm_lds<MG, CONJ, true>), dim3((unsigned)blocks), dim3(256), 0, s, Wt,
                            a_m, a_n, in, N, M, K, nsym, out, ntile, tpx, nkb, chunk_steps);
     else
@@ -1317,6 +1303,7 @@ hipError_t gemm_lds_launch(const float2 *Wt, int a_m, int a_n, const float2 *in,
     return hipGetLastError();
 }
 
+#ifdef OFDM_AB_KNOBS
 template <int MP, int SG, bool CONJ>
 hipError_t mfma_launch(const float2 *Wt, int a_m, int a_n, const float2 *in, int N, int M, int K,
                        long long nsym, float2 *out, hipStream_t s) {
@@ -1339,7 +1326,7 @@ template <bool CONJ>
 hipError_t mfma_dispatch(const float2 *Wt, int a_m, int a_n, const float2 *in, int N, int M, int K,
                          long long nsym, float2 *out, hipStream_t s) {
     // OFDM_ZF_SG: symbol quads per wave (2, 4 or 8)
-    const int sg = env_int("OFDM_ZF_SG", 4);
+    const int sg = ab_knob("ZF_SG", 4);
     if (M <= 4) return mfma_launch<2, 8, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
     if (M <= 8) return mfma_launch<4, 8, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
     if (sg == 8) return mfma_launch<8, 8, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
@@ -1361,13 +1348,15 @@ hipError_t mfma_lds_launch(const float2 *Wt, int a_m, int a_n, const float2 *in,
     nchunk = (nsteps + chunk_steps - 1) / chunk_steps;
     const long long blocks = 8LL * tpx * nchunk;
     if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
-    auto kern = env_int("OFDM_ZF_DEBUG", 0) == 1 ? zf::k_zf_mfma_lds<SG, CONJ, 1> : zf::k_zf_mfma_lds<SG, CONJ>;
+    auto kern = zf::k_zf_mfma_lds<SG, CONJ>;
     if (lds > 64 * 1024)
         if (hipError_t e = opt_in_lds(reinterpret_cast<const void *>(kern), (int)lds); e != hipSuccess) return e;
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), lds, s, Wt, a_m, a_n, in, N, M, K, nsym, out,
                        ntile, tpx, nkb, chunk_steps);
     return hipGetLastError();
 }
+
+#endif  // OFDM_AB_KNOBS
 
 template <int MPW, int SG, bool CONJ>
 hipError_t mfma_lds8_launch(const float2 *Wt, int a_m, int a_n, const float2 *in, int N, int M, int K,
@@ -1434,56 +1423,51 @@ hipError_t wstat_launch(const float2 *Wt, int a_m, int a_n, const float2 *in, in
     return hipGetLastError();
 }
 
+// Measured defaults (same-process A/B, R = 64, 10 000 symbols):
+//   detect, M = U > 8, N = R <= 72: W-stationary MFMA with one symbol chunk
+//     per XCD (k_zf_wstat<., true>): 1.87 vs 2.05 ms (VALU) at U = 16,
+//     3.34 vs 3.67 (k_zf_mfma_lds8<8,4>) / 4.09 (VALU) at U = 32;
+//   detect with N > 72: k_zf_mfma_lds8<8,4> (M > 16) / k_zf_mfma_w128;
+//   detect at U <= 8: the per-wave register-tiled VALU kernel (1.26-1.37 vs
+//     1.35-1.39 ms for the LDS VALU kernel at U = 8);
+//   apply at 32 <= N = U <= 72: k_zf_wstat<., true> (4.08 vs 4.28 ms);
+//   otherwise the LDS VALU kernel when both operands are wide enough (at
+//     N = 4 its per-chunk barriers and stores dominate), else the register-
+//     tiled one.
+// The A/B build (OFDM_AB_KNOBS) also reaches the measured-slower candidates
+// through OFDM_AB_ZF_LDS: 0 register tiles, 1 LDS VALU, 2 DMA-fed LDS, 3
+// MFMA from L1, 4 MFMA through LDS, 5/6 8-wave MFMA (16x32 / 32x16 tiles), 7
+// 128-subcarrier MFMA, 8/9 W-stationary (9: one symbol chunk per XCD), 10
+// W-stationary with 64-row tiles.
 template <bool CONJ>
 hipError_t gemm_dispatch(const float2 *Wt, int a_m, int a_n, const float2 *in, int N, int M, int K,
                          long long nsym, float2 *out, hipStream_t s) {
-    // OFDM_ZF_LDS=3: matrix cores, operands from L1 (k_zf_mfma); =4: matrix
-    // cores, operands DMA'd through LDS (k_zf_mfma_lds; OFDM_ZF_SG = 4 or 8)
-    // Default: the 8-wave LDS-fed MFMA kernel with 32-row tiles for detect at
-    // M = U >= 32 (same-process A/B at U = 32, R = 64: 3.66 ms vs 3.80 for
-    // k_zf_mfma_lds and 4.09 for the VALU kernel; the MFMA kernels are equal
-    // at U = 16 and slower for apply and U <= 8), the LDS VALU kernel otherwise.
-    // Measured defaults (same-process A/B, R = 64, 10 000 symbols):
-    //   detect, M = U > 8, N = R <= 72: W-stationary MFMA with one symbol chunk
-    //     per XCD (k_zf_wstat<., true>): 1.87 vs 2.05 ms (VALU) at U = 16,
-    //     3.34 vs 3.67 (k_zf_mfma_lds8<8,4>) / 4.09 (VALU) at U = 32;
-    //   detect with N > 72: k_zf_mfma_lds8<8,4> (M > 16) / k_zf_mfma_w128;
-    //   apply at N = U >= 32: k_zf_wstat<., true> (4.08 vs 4.28 ms);
-    //   detect at U <= 8: the per-wave register-tiled VALU kernel (1.26-1.37 vs
-    //     1.35-1.39 ms at U = 8);
-    //   apply at U < 32: the LDS VALU kernel.
     const int wdef = CONJ ? (N < 8 ? 1 : M <= 8 ? 0 : N <= 72 ? 9 : M > 16 ? 6 : 7) : (N >= 32 && N <= 72 ? 9 : 1);
-    const int mode = env_int("OFDM_ZF_LDS", wdef);
-    if (mode == 3) return mfma_dispatch<CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-    // =5: 8-wave workgroups, 16 rows x 32 symbols per step; =6: 32 rows x 16 symbols
-    if (mode == 5) return mfma_lds8_launch<4, 8, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-    if (mode == 6) return mfma_lds8_launch<8, 4, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-    if (mode == 7) return mfma_w128_launch<CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);  // 128-sc blocks
-    // =8 / 9: W-stationary MFMA (N <= 72; 16-row blocks), 9 with one symbol chunk per XCD
-    if (mode == 8 && N <= 72) return wstat_launch<CONJ, false>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+    const int mode = ab_knob("ZF_LDS", wdef);
     if (mode == 9 && N <= 72) return wstat_launch<CONJ, true>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-    // =10: W-stationary with 64-row tiles (N <= 18), one symbol chunk per XCD
+    if (mode == 6) return mfma_lds8_launch<8, 4, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+    if (mode == 7) return mfma_w128_launch<CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+#ifdef OFDM_AB_KNOBS
+    if (mode == 3) return mfma_dispatch<CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+    if (mode == 5) return mfma_lds8_launch<4, 8, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+    if (mode == 8 && N <= 72) return wstat_launch<CONJ, false>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
     if (mode == 10 && N <= 18) return wstat_launch<CONJ, true, 64>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
     if (mode == 4) {
-        if (env_int("OFDM_ZF_SG", 4) == 8) return mfma_lds_launch<8, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+        if (ab_knob("ZF_SG", 4) == 8) return mfma_lds_launch<8, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
         return mfma_lds_launch<4, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
     }
-    // LDS-shared tiles when both operands are wide enough (measured: at N = 4
-    // the per-chunk barriers and stores dominate); OFDM_ZF_LDS=0: the
-    // per-wave register-tiled kernel for every shape
-    // OFDM_ZF_LDS=2: LDS tiles DMA'd straight from global memory (k_zf_gemm_dma)
-    const int lds = env_int("OFDM_ZF_LDS", 1);
-    if (M > 4 && N >= 8 && lds == 2) {
+    if (M > 4 && N >= 8 && mode == 2) {
         if (M <= 8) return gemm_lds_launch<1, CONJ, true>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
         if (M <= 16) return gemm_lds_launch<2, CONJ, true>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
         return gemm_lds_launch<4, CONJ, true>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
     }
-    if (M > 4 && N >= 8 && lds && env_int("OFDM_ZF_ST", 8) == 4) {
+    if (M > 4 && N >= 8 && mode == 1 && ab_knob("ZF_ST", 8) == 4) {
         if (M <= 8) return gemm_lds_launch<1, CONJ, false, 4>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
         if (M <= 16) return gemm_lds_launch<2, CONJ, false, 4>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
         return gemm_lds_launch<4, CONJ, false, 4>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
     }
-    if (M > 4 && N >= 8 && lds) {
+#endif
+    if (M > 4 && N >= 8 && mode != 0) {
         if (M <= 8) return gemm_lds_launch<1, CONJ, false>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
         if (M <= 16) return gemm_lds_launch<2, CONJ, false>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
         return gemm_lds_launch<4, CONJ, false>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);

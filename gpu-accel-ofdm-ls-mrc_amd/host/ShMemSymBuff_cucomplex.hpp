@@ -1,6 +1,6 @@
-// ShMemSymBuff.hpp -- drop-in for the reference's ShMemSymBuff.hpp: the shared-memory
+// ShMemSymBuff_cucomplex.hpp -- drop-in for the reference's ShMemSymBuff_cucomplex.hpp: the shared-memory
 // symbol ring (ShMemSymBuff_impl.hpp) with this header's default geometry
-// (ShMemSymBuff.hpp:42-72): numOfRows 16, lenOfBuffer 10, dimension 1024, prefix 0, each
+// (ShMemSymBuff_cucomplex.hpp:48-83): numOfRows 1, lenOfBuffer 117, dimension 1024, prefix 0, each
 // overridable with -D.  Like the reference's three ring headers it uses the
 // include guard _SHMEMSYMBUFF_HPP_, so the first ring header a translation
 // unit includes fixes the geometry and the others are no-ops.
@@ -8,10 +8,10 @@
 #define _SHMEMSYMBUFF_HPP_
 
 #ifndef numOfRows
-#define numOfRows 16
+#define numOfRows 1
 #endif
 #ifndef lenOfBuffer
-#define lenOfBuffer 10
+#define lenOfBuffer 117
 #endif
 
 #include "ShMemSymBuff_impl.hpp"

@@ -1,6 +1,6 @@
-// ShMemSymBuff.hpp -- drop-in for the reference's ShMemSymBuff.hpp: the shared-memory
+// ShMemSymBuff_gpu.hpp -- drop-in for the reference's ShMemSymBuff_gpu.hpp: the shared-memory
 // symbol ring (ShMemSymBuff_impl.hpp) with this header's default geometry
-// (ShMemSymBuff.hpp:42-72): numOfRows 16, lenOfBuffer 10, dimension 1024, prefix 0, each
+// (ShMemSymBuff_gpu.hpp:48-80): numOfRows 16, lenOfBuffer 101, dimension 1024, prefix 0, each
 // overridable with -D.  Like the reference's three ring headers it uses the
 // include guard _SHMEMSYMBUFF_HPP_, so the first ring header a translation
 // unit includes fixes the geometry and the others are no-ops.
@@ -11,7 +11,7 @@
 #define numOfRows 16
 #endif
 #ifndef lenOfBuffer
-#define lenOfBuffer 10
+#define lenOfBuffer 101
 #endif
 
 #include "ShMemSymBuff_impl.hpp"

@@ -38,7 +38,7 @@
 
 #include "ofdm_engine.hpp"  // before the ring: its config macros are plain identifiers
 #include "CSharedMemSimple.hpp"
-#include "ShMemSymBuff.hpp"
+#include "ShMemSymBuff_cucomplex.hpp"  // as cpuLS.hpp:34; a ring header included first wins
 
 #define fileNameForX "Pilots.dat"
 #ifndef mode
@@ -47,65 +47,13 @@
 
 using namespace std;
 
-// ---- globals of the reference (cpuLS.hpp:61-66, ShMemSymBuff.hpp:62-83) --
+// ---- globals of the reference (cpuLS.hpp:61-66); outfile, numTimes, the
+// timing arrays, buffIter and printTimes/storeTimes come with the ring header
+// (ShMemSymBuff.hpp:62-191) --------------------------------------------------
 inline ShMemSymBuff *buffPtr = nullptr;
 inline string file = "Output_cpu.dat";
 inline string in_file = "Input_cpu.dat";
 inline int num_syms = 0;
-inline std::ofstream outfile;
-inline int numTimes = 1;
-inline float readT[numberOfSymbolsToTest];
-inline float decode[numberOfSymbolsToTest];
-inline float drop[numberOfSymbolsToTest];
-inline float fft[numberOfSymbolsToTest];
-inline int buffIter = 0;
-
-inline void printOutArr(complexF *a, int rows, int cols) {
-    for (int i = 0; i < rows; i++) {
-        for (int j = 0; j < cols; j++)
-            std::cout << "(" << a[i * cols + j].real << ", " << a[i * cols + j].imag << "), ";
-        std::printf("\n");
-    }
-}
-inline void printInfo() {
-    std::printf("\tSymbol Dimension(w/o prefix) = %d x %d \n", numOfRows, dimension);
-    std::printf("\tPrefix = %d\n", prefix);
-    std::printf("\t# Of Symbols To Test = %d\n", numberOfSymbolsToTest);
-}
-inline complexF findAvgAndVar(float *times, int amt) {
-    float mean = 0.f, var = 0.f;
-    for (int i = 0; i < amt; i++) mean += times[i];
-    mean /= amt;
-    for (int i = 0; i < amt; i++) var += (times[i] - mean) * (times[i] - mean);
-    return complexF{mean, var / amt};
-}
-// (ShMemSymBuff.hpp:149-189; readT comes from the ring object when present)
-inline void printTimes(bool cpu) {
-    float *rt = buffPtr ? buffPtr->readT : readT;
-    complexF rd = findAvgAndVar(rt, numberOfSymbolsToTest);
-    complexF dec = findAvgAndVar(&decode[1], numberOfSymbolsToTest - 1);
-    complexF ff = findAvgAndVar(fft, numberOfSymbolsToTest);
-    std::printf("\t \t Avg Time(s) \t Variance (s^2) \n");
-    std::printf("Read: \t \t %e \t %e \n", rd.real / numTimes, rd.imag / numTimes);
-    std::printf("ChanEst: \t %e \n", decode[0] / numTimes);
-    std::printf("Decode: \t %e \t %e \n", dec.real / numTimes, dec.imag / numTimes);
-    std::printf("FFT: \t \t %e \t %e \n", ff.real / numTimes, ff.imag / numTimes);
-    if (cpu) {
-        complexF dr = findAvgAndVar(buffPtr ? buffPtr->drop : drop, numberOfSymbolsToTest);
-        std::printf("Drop: \t \t %e \t %e \n", dr.real / numTimes, dr.imag / numTimes);
-    }
-}
-inline void storeTimes(bool cpu) {
-    float *rt = buffPtr ? buffPtr->readT : readT;
-    complexF rd = findAvgAndVar(rt, numberOfSymbolsToTest);
-    complexF dec = findAvgAndVar(&decode[1], numberOfSymbolsToTest - 1);
-    complexF ff = findAvgAndVar(fft, numberOfSymbolsToTest);
-    complexF dr = findAvgAndVar(buffPtr ? buffPtr->drop : drop, numberOfSymbolsToTest);
-    const float v[5] = {rd.real / numTimes, decode[0] / numTimes, dec.real / numTimes,
-                        ff.real / numTimes, dr.real / numTimes};
-    std::ofstream out(cpu ? "time_cpu.dat" : "time_gpu.dat", std::ofstream::binary);
-    out.write(reinterpret_cast<const char *>(v), sizeof v);
-}
 
 namespace ofdm_cpuls {
 inline clock_t tic() { return timerEn ? clock() : 0; }

@@ -31,7 +31,7 @@
 #include <vector>
 
 #include "ofdm_engine.hpp"
-#include "ShMemSymBuff.hpp"
+#include "ShMemSymBuff_gpu.hpp"  // as gpuLS.cuh:35
 
 #define FFT_size dimension
 #define cp_size prefix
@@ -188,26 +188,34 @@ class gpuLS {
         buffPtr->setReadT(secs(t0), 1);
         demodOneFrameCUDA(dY, Y, dX, Hconj, Hsqrd, rows1, cols1);
     }
-    // Y (device, lenOfBuffer symbols, time domain) is FFT'd in place; symbol 0
-    // gives Hconj / Hsqrd; the (lenOfBuffer-1) x K rotated outputs go to dY.
+    // Y (device): one frame of lenOfBuffer time-domain symbols, pilot first.
+    // One pass of the fused receiver (ofdm_frame_estimate + ofdm_frame_combine:
+    // FFT + LS, then FFT + MRC + normalise + rotate, each row read once) in
+    // place of the reference's cuFFT + findHs + findDistSqrd +
+    // multiplyWithChannelConj + combineForMRC + shiftOneRow chain
+    // (gpuLS.cu:599-662).  Outputs as the reference leaves them: the
+    // (lenOfBuffer-1) x (cols1-1) rotated symbols in dY (host or device),
+    // the LS estimate in Hconj (rows1 x (cols1-1), device) and |H|^2 in
+    // Hsqrd (cols1-1, device).  Unlike the reference, Y is left in the time
+    // domain (the transform never goes back to memory).
     void demodOneFrameCUDA(hipFloatComplex *dY, hipFloatComplex *Y, hipFloatComplex *dX,
                            hipFloatComplex *Hconj, float *Hsqrd, int rows1, int cols1) {
         const int K = cols1 - 1;
-        const size_t sym = (size_t)rows1 * cols1;
+        const size_t wsb = ofdm_frame_workspace_bytes(1, lenOfBuffer, rows1, cols1);
+        void *ws = ws_.get(wsb);
+        auto *out = scratch_.get<ofdm_cf32>((size_t)K * (lenOfBuffer - 1) * 8);
         clock_t t0 = clock();
-        batchedFFT(Y, rows1 * lenOfBuffer, cols1, nullptr);
+        ofdm::check(ofdm_frame_estimate(C(Y), 1, lenOfBuffer, rows1, cols1, 0, C(dX), ws, wsb, nullptr),
+                    "ofdm_frame_estimate");
+        ofdm::check(ofdm_frame_export_estimate(ws, wsb, 1, lenOfBuffer, rows1, cols1, 0, C(Hconj), Hsqrd,
+                                               nullptr),
+                    "ofdm_frame_export_estimate");
         sync();
-        buffPtr->setFft(secs(t0), 1);
-        t0 = clock();
-        ofdm::check(ofdm_ls_estimate(C(Y), C(dX), rows1, cols1, C(Hconj), Hsqrd, nullptr),
-                    "ofdm_ls_estimate");
-        sync();
+        buffPtr->setFft(0.f, 1);  // fused into the LS / MRC kernels
         buffPtr->setDecode(secs(t0), 0);
         t0 = clock();
-        auto *out = scratch_.get<ofdm_cf32>((size_t)K * (lenOfBuffer - 1) * 8);
-        ofdm::check(ofdm_mrc_demod(C(Y + sym), lenOfBuffer - 1, C(Hconj), Hsqrd, rows1, cols1, out,
-                                   nullptr),
-                    "ofdm_mrc_demod");
+        ofdm::check(ofdm_frame_combine(C(Y), 1, lenOfBuffer, rows1, cols1, 0, ws, wsb, out, nullptr),
+                    "ofdm_frame_combine");
         ofdm::copy_any(dY, out, (size_t)K * (lenOfBuffer - 1) * 8);
         buffPtr->setDecode(secs(t0), 1);
     }
@@ -299,7 +307,7 @@ class gpuLS {
         buffPtr->setReadT(secs(t0), it);
     }
 
-    ofdm::DevBuf scratch_, scratchP_;
+    ofdm::DevBuf scratch_, scratchP_, ws_;
 };
 
 #endif  // OFDM_GPULS_HPP_

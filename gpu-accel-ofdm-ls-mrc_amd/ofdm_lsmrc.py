@@ -17,7 +17,11 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libofdm_lsmrc.so")
+# OFDM_LSMRC_LIB=ab selects the A/B build (make ab: lib/libofdm_lsmrc_ab.so,
+# experiment switches read from OFDM_AB_* variables) for scripts/ comparisons;
+# the product library has no switches.
+LIB_PATH = os.path.join(HERE, "lib", "libofdm_lsmrc_ab.so" if os.environ.get("OFDM_LSMRC_LIB") == "ab"
+                        else "libofdm_lsmrc.so")
 HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "ofdm_lsmrc.h")
 
 _c = ctypes
@@ -45,8 +49,10 @@ _SIGS = {
     "ofdm_frame_estimate": (_I, [_P, _LL, _I, _I, _I, _I, _P, _P, _c.c_size_t, _P]),
     "ofdm_frame_combine": (_I, [_P, _LL, _I, _I, _I, _I, _P, _c.c_size_t, _P, _P]),
     "ofdm_frame_demod_freq": (_I, [_P, _LL, _I, _I, _I, _P, _P, _c.c_size_t, _P, _P]),
+    "ofdm_frame_demod_freq_mfma": (_I, [_P, _LL, _I, _I, _I, _P, _P, _c.c_size_t, _P, _P]),
     "ofdm_frame_ls_partial": (_I, [_P, _LL, _I, _I, _I, _I, _P, _P, _c.c_size_t, _P, _P]),
     "ofdm_frame_mrc_partial": (_I, [_P, _LL, _I, _I, _I, _I, _P, _c.c_size_t, _P, _P]),
+    "ofdm_frame_export_estimate": (_I, [_P, _c.c_size_t, _LL, _I, _I, _I, _LL, _P, _P, _P]),
     "ofdm_synth_frames": (_I, [_P, _LL, _I, _I, _I, _I, _P, _c.c_ulonglong, _LL, _c.c_float,
                                _I, _I, _P]),
     "ofdm_count_symbol_errors": (_I, [_P, _LL, _I, _I, _c.c_ulonglong, _LL, _P, _P]),
@@ -272,6 +278,18 @@ def frame_demod_freq(Y, X, ws=None, out=None, stream=None):
     return out
 
 
+def frame_demod_freq_mfma(Y, X, ws=None, out=None, stream=None):
+    """frame_demod_freq with the antenna combine on the matrix cores."""
+    F, S, R, C = Y.shape
+    if ws is None:
+        ws = workspace(F, S, R, C, Y.device)
+    if out is None:
+        out = c64((F, S - 1, C - 1), Y.device)
+    _check(lib().ofdm_frame_demod_freq_mfma(_dptr(Y), F, S, R, C, _dptr(X), _dptr(ws), ws.numel(),
+                                            _dptr(out), _stream(stream)), "ofdm_frame_demod_freq_mfma")
+    return out
+
+
 def frame_ls_partial(iq, X, prefix=0, ws=None, P=None, stream=None):
     import torch
     F, S, R, Cp = iq.shape
@@ -294,6 +312,16 @@ def frame_mrc_partial(iq, ws, prefix=0, num=None, stream=None):
     _check(lib().ofdm_frame_mrc_partial(_dptr(iq), F, S, R, C, prefix, _dptr(ws), ws.numel(),
                                         _dptr(num), _stream(stream)), "ofdm_frame_mrc_partial")
     return num
+
+
+def frame_export_estimate(ws, F, S, R, C, frame=0, stream=None):
+    """Frame `frame`'s estimate in the reference layout: (Hconj (R, K), Hsqrd (K,))."""
+    import torch
+    H = c64((R, C - 1), ws.device)
+    P = torch.empty(C - 1, dtype=torch.float32, device=ws.device)
+    _check(lib().ofdm_frame_export_estimate(_dptr(ws), ws.numel(), F, S, R, C, frame, _dptr(H), _dptr(P),
+                                            _stream(stream)), "ofdm_frame_export_estimate")
+    return H, P
 
 
 def synth_frames(F, S, R, C, X, prefix=0, seed=1234, frame0=0, noise_std=0.01,

@@ -126,9 +126,14 @@ int ofdm_dist_sqrd(const ofdm_cf32 *d_H, int R, int K, float *d_Hsqrd, ofdm_stre
 
 /* ------------------------------------------------------ device: frames --- */
 
-/* Workspace for ofdm_frame_demod / ofdm_frame_demod_freq (bytes, 256-aligned
- * pieces): per-frame channel estimates [F][R][C], |H|^2 [F][C] and, for FFT
- * sizes without a fused kernel, a frequency-domain staging buffer. */
+/* Workspace for ofdm_frame_demod / ofdm_frame_demod_freq and the two-stage
+ * and antenna-split calls (bytes, 256-aligned pieces): per-frame channel
+ * estimates [F][R][C], |H|^2 [F][C] and, for C outside {1024, 2048, 4096}
+ * (no fused kernel), a frequency-domain staging buffer of at most 256 MiB.
+ * A workspace carries the estimate of ONE geometry: the calls that consume it
+ * (ofdm_frame_combine, ofdm_frame_mrc_partial, ofdm_frame_export_estimate)
+ * must pass the nframes, S, R and C of the call that filled it, and return
+ * OFDM_E_ARG otherwise (checked per process, on the host). */
 size_t ofdm_frame_workspace_bytes(long long nframes, int S, int R, int C);
 
 /* Frame-batched receiver on time-domain IQ (what ShMemSymBuff delivers):
@@ -137,8 +142,10 @@ size_t ofdm_frame_workspace_bytes(long long nframes, int S, int R, int C);
  * each frame gives the LS estimate, symbols 1..S-1 are MRC-demodulated into
  * d_out = nframes x (S-1) x K.  Replaces demodOneFrameCUDA / demodOptimized
  * (gpuLS.cu:575-769) and the cpuLS_main loop (cpuLS_main.cpp:80-92), for a
- * whole batch of frames in one call.  C = 1024 runs the fused one-pass
- * kernels; other C run FFT + LS + MRC stages through the workspace. */
+ * whole batch of frames in one call.  C in {1024, 2048, 4096} runs the fused
+ * one-pass kernels (FFT + LS, FFT + MRC + normalise + rotate); other powers
+ * of two run FFT, LS and MRC as stages through the workspace's staging
+ * buffer. */
 int ofdm_frame_demod(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, int cp_len,
                      const ofdm_cf32 *d_X, void *d_ws, size_t ws_bytes, ofdm_cf32 *d_out,
                      ofdm_stream_t stream);
@@ -154,11 +161,31 @@ int ofdm_frame_estimate(const ofdm_cf32 *d_iq, long long nframes, int S, int R, 
 int ofdm_frame_combine(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, int cp_len,
                        void *d_ws, size_t ws_bytes, ofdm_cf32 *d_out, ofdm_stream_t stream);
 
+/* One frame's LS estimate out of a workspace filled by ofdm_frame_estimate /
+ * ofdm_frame_demod / ofdm_frame_demod_freq / ofdm_frame_ls_partial (same
+ * nframes, S, R, C), in the reference's layout: d_Hconj[r][j] = conj(Y0/X)
+ * (R x K), d_Hsqrd[j] = sum_r |Hconj[r][j]|^2 (K floats; NULL = not wanted;
+ * for an ls_partial workspace the local antennas' partial sum).  These are
+ * the Hconj / Hsqrd outputs of demodOneFrameCUDA (gpuLS.cu:617-629) and
+ * firstVector (gpuLS.cu:392-395), which the fused kernels keep in their own
+ * lane order. */
+int ofdm_frame_export_estimate(const void *d_ws, size_t ws_bytes, long long nframes, int S, int R, int C,
+                               long long frame, ofdm_cf32 *d_Hconj, float *d_Hsqrd, ofdm_stream_t stream);
+
 /* ofdm_frame_demod on frequency-domain symbols (FFT done upstream, no prefix):
  * d_Y = nframes x S x R x C. */
 int ofdm_frame_demod_freq(const ofdm_cf32 *d_Y, long long nframes, int S, int R, int C,
                           const ofdm_cf32 *d_X, void *d_ws, size_t ws_bytes, ofdm_cf32 *d_out,
                           ofdm_stream_t stream);
+
+/* ofdm_frame_demod_freq with the antenna combine on the matrix cores: per
+ * subcarrier the (S-1) x R x R-by-1 product sum_r Y[s][r] Hconj[r] as
+ * v_mfma_f32 tiles (mrc_mfma.hip) -- the MFMA-cgemm formulation BASELINE
+ * configs[4] asks to compare with the elementwise combine.  Same results
+ * within f32 rounding (antenna order per MFMA block); C >= 64. */
+int ofdm_frame_demod_freq_mfma(const ofdm_cf32 *d_Y, long long nframes, int S, int R, int C,
+                               const ofdm_cf32 *d_X, void *d_ws, size_t ws_bytes, ofdm_cf32 *d_out,
+                               ofdm_stream_t stream);
 
 /* Antenna-split pieces (time-domain frames holding this GPU's R antennas):
  * partial |H|^2 per frame into d_P ([nframes][K], sum over the local
@@ -192,6 +219,9 @@ int ofdm_frame_mrc_partial(const ofdm_cf32 *d_iq, long long nframes, int S, int 
  *       NULL = leave them in the slot) on the output stream.
  *   ofdm_pipeline_demod: acquire + copy + submit over nframes host frames.
  *   ofdm_pipeline_sync: waits for everything submitted.
+ * Each call makes the pipeline's device current and restores the caller's
+ * current device before returning.  A failed submit releases its slot (those
+ * frames are not demodulated); the pipeline stays usable.
  * Calls return before the copies finish: `iq` and `out` must stay valid until
  * ofdm_pipeline_sync.  For copies that overlap, host buffers must be
  * page-locked (ofdm_host_register); pageable buffers work but serialise. */

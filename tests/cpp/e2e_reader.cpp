@@ -67,6 +67,15 @@ static int run_gpuls(bool frame, bool dev_staging) {
         if (dev_staging) (void)hipFree(dY);
     }
     const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    // the estimate the flow leaves in Hconj / Hsqrd (firstVector, demodOneFrameCUDA)
+    std::vector<hipFloatComplex> h((size_t)rows * K);
+    std::vector<float> p(K);
+    ofdm::copy_any(h.data(), dH, h.size() * sizeof(hipFloatComplex));
+    ofdm::copy_any(p.data(), Hsqrd, p.size() * sizeof(float));
+    std::ofstream("Hconj_gpu.dat", std::ofstream::binary)
+        .write(reinterpret_cast<const char *>(h.data()), (std::streamsize)(h.size() * sizeof(hipFloatComplex)));
+    std::ofstream("Hsqrd_gpu.dat", std::ofstream::binary)
+        .write(reinterpret_cast<const char *>(p.data()), (std::streamsize)(p.size() * sizeof(float)));
     std::printf("{\"frames\": 1, \"seconds\": %.6f, \"data_symbols_per_s\": %.1f}\n", sec,
                 (lenOfBuffer - 1) / sec);
     (void)hipFree(Y); (void)hipFree(dH); (void)hipFree(dX); (void)hipFree(Hsqrd);

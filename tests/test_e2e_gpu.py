@@ -45,7 +45,9 @@ def build(tmp, name, R, C, prefix, S, shm):
                                           ("cfg1_r4_c1024_s10", "frame"),
                                           ("r8_c2048_s3_cp16", "symbol"),
                                           ("r8_c2048_s3_cp16", "cpuls"),
-                                          ("r4_c256_s5_cp32", "frame")])
+                                          ("r4_c256_s5_cp32", "frame"),
+                                          ("r8_c2048_s3_cp16", "frame"),
+                                          ("r64_c1024_s2", "frame")])
 def test_ring_to_output_file(tmp_path, fixture, flow):
     z = np.load(os.path.join(GOLDEN, fixture + ".npz"), allow_pickle=False)
     iq = z["iq"][0]  # first frame: S x R x (C + prefix)
@@ -71,6 +73,11 @@ def test_ring_to_output_file(tmp_path, fixture, flow):
     name = "Output_cpu.dat" if flow == "cpuls" else "Output_gpu.dat"
     got = np.fromfile(os.path.join(tmp, name), np.complex64).reshape(S - 1, C - 1)
     parity(got, z["out"][0])
+    if flow != "cpuls":  # the LS estimate the gpuLS flow leaves in its Hconj / Hsqrd arguments
+        H = np.fromfile(os.path.join(tmp, "Hconj_gpu.dat"), np.complex64).reshape(R, C - 1)
+        P = np.fromfile(os.path.join(tmp, "Hsqrd_gpu.dat"), np.float32)
+        parity(H, z["H"][0])
+        parity(P, z["P"][0])
 
 
 @pytest.mark.parametrize("fixture,repeat,chunk,depth", [("r16_c1024_s4_2frames", 1, 4, 3),

@@ -141,13 +141,12 @@ def test_frame_demod_freq_synth_vs_oracle(ofdm, oracle, dev, F, S, R, C):
 
 @pytest.mark.parametrize("F,S,R,C", [(2, 21, 16, 1024), (2, 18, 7, 256), (1, 5, 32, 4096),
                                      (3, 17, 1, 64)])
-def test_frame_demod_freq_mfma_vs_oracle(ofdm, oracle, dev, monkeypatch, F, S, R, C):
-    """The matrix-core combine (OFDM_MRC_FREQ_MFMA=1, mrc_mfma.hip): partial
-    symbol tiles (S-1 not a multiple of 16), odd antenna counts."""
-    monkeypatch.setenv("OFDM_MRC_FREQ_MFMA", "1")
+def test_frame_demod_freq_mfma_vs_oracle(ofdm, oracle, dev, F, S, R, C):
+    """The matrix-core combine (ofdm_frame_demod_freq_mfma, mrc_mfma.hip):
+    partial symbol tiles (S-1 not a multiple of 16), odd antenna counts."""
     X = to_dev(qpsk_pilots(C - 1), dev)
     Y = ofdm.synth_frames(F, S, R, C, X, seed=6, noise_std=0.05, freq_domain=True)
-    out = host(ofdm.frame_demod_freq(Y, X))
+    out = host(ofdm.frame_demod_freq_mfma(Y, X))
     ref = oracle.frames_demod_freq(host(Y), host(X), nthreads=8)
     parity(out, ref)
 
@@ -160,33 +159,17 @@ def test_empty_batch_is_noop(ofdm, dev):
     assert out.shape == (0, 2, 1023)
 
 
-@pytest.mark.parametrize("F,S,R,C,prefix", [c for c in CONFIGS if c[3] == 1024] + [(2, 9, 2, 1024, 3),
-                                                                                    (100, 101, 16, 1024, 0)])
-def test_frame_demod_rsplit_vs_oracle(ofdm, oracle, dev, monkeypatch, F, S, R, C, prefix):
-    """k_mrc_td1024_rsplit (OFDM_MRC_RSPLIT=1: two waves per symbol, antenna
-    halves summed in LDS), normalised outputs and partial numerators."""
-    import torch
-    monkeypatch.setenv("OFDM_MRC_RSPLIT", "1")
+def test_configs1_batch(ofdm, oracle, dev):
+    """BASELINE configs[1] in full: 100 frames x 101 symbols (10k data
+    symbols) x 16 antennas x 1024 subcarriers -- zero QPSK decision errors and
+    the oracle on the first, middle and last frames."""
+    F, S, R, C = 100, 101, 16, 1024
     X = to_dev(qpsk_pilots(C - 1), dev)
-    big = F * (S - 1) > 2000
-    seed = 7 + R if big else 99 + C  # small cases: the realisations of test_frame_demod_synth_vs_oracle
-    iq = ofdm.synth_frames(F, S, R, C, X, prefix=prefix, seed=seed, noise_std=0.01 if big else 0.05)
-    out = ofdm.frame_demod(iq, X, prefix)
-    if big:  # the configs[1] batch: size-independent check + oracle on two frames
-        assert int(ofdm.count_symbol_errors(out, S, seed=seed).item()) == 0
-        sel = [0, F - 1]
-        parity(host(out)[sel], oracle.frames_demod(host(iq)[sel], host(X), prefix, nthreads=8))
-        return
-    parity(host(out), oracle.frames_demod(host(iq), host(X), prefix, nthreads=8))
-    monkeypatch.setenv("OFDM_MRC_RSPLIT", "0")
-    parity(host(out), host(ofdm.frame_demod(iq, X, prefix)))  # vs the sequential-order kernel
-    monkeypatch.setenv("OFDM_MRC_RSPLIT", "1")
-    Pp, ws = ofdm.frame_ls_partial(iq, X, prefix)
-    num = ofdm.frame_mrc_partial(iq, ws, prefix)
-    monkeypatch.setenv("OFDM_MRC_RSPLIT", "0")
-    num_ref = ofdm.frame_mrc_partial(iq, ws, prefix)
-    torch.cuda.synchronize()
-    parity(host(num), host(num_ref))
+    iq = ofdm.synth_frames(F, S, R, C, X, seed=23, noise_std=0.01)
+    out = ofdm.frame_demod(iq, X)
+    assert int(ofdm.count_symbol_errors(out, S, seed=23).item()) == 0
+    sel = [0, F // 2, F - 1]
+    parity(host(out)[sel], oracle.frames_demod(host(iq)[sel], host(X), 0, nthreads=8))
 
 
 # ------------------------------------------ antenna split (partial MRC path)
@@ -244,6 +227,30 @@ def test_full_size_properties(ofdm, dev, F, S, R, C):
     for f in (0, F - 1):
         ref, _, _ = o.frame_demod(host(iq[f]), host(X))
         parity(host(out[f]), ref)
+
+
+@pytest.mark.parametrize("F,S,R,C", [(1000, 101, 64, 2048),   # BASELINE configs[2] in full: 100k symbols, 106 GB
+                                     (1250, 101, 64, 1024)])  # configs[3] per GPU in full: 125k symbols, 66 GB
+def test_full_size_baseline_batches(ofdm, oracle, dev, F, S, R, C):
+    """The whole BASELINE batch resident in HBM: zero QPSK decision errors,
+    exact invariance to a power-of-two IQ scale (applied in place, so the
+    batch is held once) and the oracle on the first, middle and last frames."""
+    import torch
+    X = to_dev(qpsk_pilots(C - 1), dev)
+    iq = ofdm.synth_frames(F, S, R, C, X, seed=13, noise_std=0.01)
+    try:
+        out = ofdm.frame_demod(iq, X)
+        assert int(ofdm.count_symbol_errors(out, S, seed=13).item()) == 0
+        sel = [0, F // 2, F - 1]
+        ref = oracle.frames_demod(host(iq[sel]), host(X), 0, nthreads=8)
+        parity(host(out[sel]), ref)
+        iq.mul_(4.0)
+        out2 = ofdm.frame_demod(iq, X)
+        torch.cuda.synchronize()
+        assert torch.allclose(out2, out, rtol=1e-6, atol=1e-6)
+    finally:
+        del iq
+        torch.cuda.empty_cache()
 
 
 # ------------------------------------------- stage-wise reference GPU API

@@ -48,24 +48,16 @@ def test_zf_precoder_single_output(ofdm, dev):
     assert np.array_equal(Wt_only.cpu().numpy(), W_only.cpu().numpy().transpose(1, 2, 0))
 
 
+# The shapes select every kernel of the shape-based dispatch (zf.hip
+# gemm_dispatch): detect -- register tiles (U <= 8 or R < 8), W-stationary
+# MFMA (U > 8, R <= 72), 8-wave MFMA (U > 16, R > 72), 128-subcarrier MFMA
+# (8 < U <= 16, R > 72); apply -- register tiles (U < 8 or R <= 4), LDS tiles,
+# W-stationary MFMA (32 <= U <= 72).
 @pytest.mark.parametrize("U,R,K,n", [(1, 1, 5, 1), (2, 4, 1023, 7), (3, 5, 64, 9), (4, 16, 1023, 33),
                                      (5, 12, 130, 17), (8, 64, 1023, 40), (12, 40, 200, 16),
                                      (16, 64, 1023, 100), (17, 64, 65, 3), (32, 64, 255, 25),
-                                     (16, 100, 1023, 8)])
-# LDS tiles (default) / per-wave registers / DMA-fed LDS / 8x4 LDS / matrix cores from L1 (3 symbol-quad counts) / through LDS (2 + two 8-wave + 128-subcarrier / W-stationary)
-@pytest.mark.parametrize("lds", ["1", "0", "2", "1st4", "3", "3sg2", "3sg8", "4", "4sg8", "5", "6", "7", "8", "9", "10", "1xmap", "default"])
-def test_zf_apply_detect_parity(ofdm, oracle, dev, monkeypatch, U, R, K, n, lds):
-    if lds == "default":  # the shape-based dispatch with no knob set
-        for v in ("OFDM_ZF_LDS", "OFDM_ZF_ST", "OFDM_ZF_SG", "OFDM_ZF_XMAP", "OFDM_ZF_DEBUG"):
-            monkeypatch.delenv(v, raising=False)
-    else:
-        monkeypatch.setenv("OFDM_ZF_LDS", lds[:2] if lds[:2].isdigit() else lds[0])
-    if lds.endswith("st4"):
-        monkeypatch.setenv("OFDM_ZF_ST", "4")
-    if "sg" in lds:
-        monkeypatch.setenv("OFDM_ZF_SG", lds[-1])
-    if lds.endswith("xmap"):
-        monkeypatch.setenv("OFDM_ZF_XMAP", "1")
+                                     (16, 100, 1023, 8), (24, 100, 130, 20)])
+def test_zf_apply_detect_parity(ofdm, oracle, dev, U, R, K, n):
     H = channel(U, R, K, seed=n)
     W = oracle.zf_precoder(H)
     X = qpsk(n, U, K, seed=n + 1)
