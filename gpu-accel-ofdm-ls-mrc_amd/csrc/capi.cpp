@@ -192,14 +192,11 @@ int set_error(int code, const char *msg) {
     return code;
 }
 #ifdef OFDM_AB_KNOBS
-int ab_knob(const char *name, int def) {  // OFDM_AB_<name>, read once
-    static std::mutex mu;
-    static std::map<std::string, int> cache;
-    std::lock_guard<std::mutex> lock(mu);
-    auto it = cache.find(name);
-    if (it != cache.end()) return it->second;
+// OFDM_AB_<name>, re-read on every launch so that one process can compare
+// candidates back to back (A/B build only)
+int ab_knob(const char *name, int def) {
     const char *v = getenv((std::string("OFDM_AB_") + name).c_str());
-    return cache[name] = (v && *v) ? atoi(v) : def;
+    return (v && *v) ? atoi(v) : def;
 }
 #endif
 }  // namespace ofdm

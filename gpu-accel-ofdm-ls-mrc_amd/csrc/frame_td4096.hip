@@ -198,7 +198,10 @@ __device__ __forceinline__ void dma_hc_row(const float2 *g, unsigned lds) {
 // this row's first barrier publishes it (after vmcnt(0)) and the DMA of row
 // r+1 (hnext, into LDS byte address hb_next) is issued right after that
 // barrier, into the buffer every wave finished with in row r-1.
-template <int E, int PK, bool PREF>
+// DBG (A/B build only, wrong results by design): bit 0 no workgroup barriers
+// (racy exchange and Hc), bit 1 no Hc DMA (Hc read from stale LDS), bit 2 no
+// output stores.
+template <int E, int PK, bool PREF, int DBG = 0>
 __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const float2 *__restrict__ hr,
                                       int t, float2 *T, const float2 *Tp, const float2 *tw1,
                                       const float2 *tw2, pk::v2f wb0, pk::v2f wb1, float2 (&a)[16],
@@ -216,14 +219,14 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
 #pragma unroll
     for (int m = 0; m < 16; ++m) T[hl::swz(m, t)] = F(E ? u[m] : v[m]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this row's Hc DMA landed
-    td1024::lds_barrier();
-    if (hnext) dma_hc_row(hnext, hb_next);
+    if (!(DBG & 1)) td1024::lds_barrier();
+    if (!(DBG & 2) && hnext) dma_hc_row(hnext, hb_next);
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
         if (E) u[m] = V(Tp[hl::swz(m, t)]);  // b
         else v[m] = V(Tp[hl::swz(m, t)]);    // c
     }
-    td1024::lds_barrier();  // the partner has read T before the FFT reuses it
+    if (!(DBG & 1)) td1024::lds_barrier();  // the partner has read T before the FFT reuses it
     // E = 0: u = a, v = c:  z0 = a + c, z2 = (a - c) W^(2 n0)
     // E = 1: u = b, v = d:  z1 = (b + (-i) d) W^(n0), z3 = (b - (-i) d) W^(3 n0)
 #pragma unroll
@@ -306,7 +309,7 @@ constexpr int H_PAIRS = 4;
 constexpr size_t H_LDS = (size_t)(X_TAB + 2 * H_PAIRS * hl::TS + 2 * C) * sizeof(float2);
 static_assert(H_LDS <= 160 * 1024, "one workgroup per CU");
 
-template <int E, int PK>
+template <int E, int PK, int DBG = 0>
 __device__ __forceinline__ void h_rows(const float2 *sym, int Cp, int R, const float2 *Hg, float2 *HB, int t,
                                        float2 *T, const float2 *Tp, const float2 *tw1, const float2 *tw2,
                                        pk::v2f wb0, pk::v2f wb1, float2 (&ae)[16], float2 (&ao)[16]) {
@@ -315,15 +318,16 @@ __device__ __forceinline__ void h_rows(const float2 *sym, int Cp, int R, const f
     row_load<true>(sym + 1024 * (E + 2), t, b);
     const unsigned hb0 = lds_addr(HB), hb1 = lds_addr(HB + C);
     for (int r = 0; r + 1 < R; ++r)
-        x_row<E, PK, true>(sym + (long long)(r + 1) * Cp, HB + (r & 1) * C + E * 2048, t, T, Tp,
+        x_row<E, PK, true, DBG>(sym + (long long)(r + 1) * Cp, HB + (r & 1) * C + E * 2048, t, T, Tp,
                                         tw1, tw2, wb0, wb1, a, b, ae, ao, Hg + (long long)(r + 1) * C,
                                         (r & 1) ? hb0 : hb1);
-    x_row<E, PK, false>(sym, HB + ((R - 1) & 1) * C + E * 2048, t, T, Tp, tw1, tw2, wb0, wb1, a,
+    x_row<E, PK, false, DBG>(sym, HB + ((R - 1) & 1) * C + E * 2048, t, T, Tp, tw1, tw2, wb0, wb1, a,
                                      b, ae, ao, nullptr, 0);
 }
 
 constexpr int H_PK = 7;  // packed-f32 split, FFT halves and MAC (pk.hpp)
 
+template <int DBG = 0>
 __global__ void __attribute__((amdgpu_flat_work_group_size(128 * H_PAIRS, 128 * H_PAIRS),
                                amdgpu_waves_per_eu(2, 2)))
 k_mrc_td4096h(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
@@ -358,11 +362,18 @@ k_mrc_td4096h(const float2 *__restrict__ iq, int S, int R, int prefix, const flo
 #pragma unroll
     for (int k = 0; k < 16; ++k) ae[k] = ao[k] = float2{0.f, 0.f};
     if (e)
-        h_rows<1, H_PK>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
+        h_rows<1, H_PK, DBG>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
     else
-        h_rows<0, H_PK>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
+        h_rows<0, H_PK, DBG>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
     if (!store) return;
     const long long q = f * nsym + j;
+    if (DBG & 4) {  // diagnostic: no output stores (keep the sums live)
+        float sacc = 0.f;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) sacc += ae[k].x + ao[k].y;
+        if (sacc == 1234.5f) out[q] = float2{sacc, 0.f};
+        return;
+    }
     const int b0 = lane_bin0(t);
     float2 *o = out + q * K;
     const float *Pf = P + f * C;
@@ -406,9 +417,19 @@ hipError_t launch_mrc_td4096(const float2 *iq, long long nframes, int S, int R, 
     if (nq <= 0) return hipSuccess;
     const long long bpf = ((S - 1) + H_PAIRS - 1) / H_PAIRS, nb = nframes * bpf, pxcd = (nb + 7) / 8;
     if (pxcd * 8 > 0x7fffffffll) return hipErrorInvalidValue;
-    if (hipError_t e = opt_in_lds(reinterpret_cast<const void *>(&k_mrc_td4096h), (int)H_LDS); e != hipSuccess)
+    auto kern = k_mrc_td4096h<0>;
+#ifdef OFDM_AB_KNOBS
+    switch (ab_knob("MRC4K_DBG", 0)) {
+        case 1: kern = k_mrc_td4096h<1>; break;
+        case 2: kern = k_mrc_td4096h<2>; break;
+        case 4: kern = k_mrc_td4096h<4>; break;
+        case 6: kern = k_mrc_td4096h<6>; break;
+        default: break;
+    }
+#endif
+    if (hipError_t e = opt_in_lds(reinterpret_cast<const void *>(kern), (int)H_LDS); e != hipSuccess)
         return e;  // > 64 KiB of dynamic LDS
-    hipLaunchKernelGGL(k_mrc_td4096h, dim3((unsigned)(pxcd * 8)), dim3(128 * H_PAIRS), H_LDS, s, iq, S, R, prefix,
+    hipLaunchKernelGGL(kern, dim3((unsigned)(pxcd * 8)), dim3(128 * H_PAIRS), H_LDS, s, iq, S, R, prefix,
                        Hc, P, out, nframes, nb, pxcd, mode);
     return hipGetLastError();
 }

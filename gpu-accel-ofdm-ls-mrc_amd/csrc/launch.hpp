@@ -32,8 +32,8 @@ inline hipError_t opt_in_lds(const void *kernel, int bytes) {
 // Experiment switches.  The product library (make) has none: ab_knob() is the
 // compile-time default and no environment variable changes what a kernel
 // computes or which kernel runs.  The A/B build (make ab ->
-// lib/libofdm_lsmrc_ab.so, -DOFDM_AB_KNOBS) reads OFDM_AB_<name> once per
-// process, for same-process comparisons of candidate kernels in scripts/.
+// lib/libofdm_lsmrc_ab.so, -DOFDM_AB_KNOBS) reads OFDM_AB_<name> on every
+// launch, for same-process comparisons of candidate kernels in scripts/.
 #ifdef OFDM_AB_KNOBS
 int ab_knob(const char *name, int def);
 #else

@@ -33,3 +33,18 @@ FUNCS="matrix_readX shiftOneRow matrixMultThenSum findDistSqrd divideOneRow rotC
 } | g++ -O2 -ffp-contract=off -fPIC -shared -DHAVE_UNISTD_H=1 -I"$REF" \
       -include "$HERE/ref_prelude.hpp" -x c++ - -o "$OUT/libref_cpuls.so"
 echo "built $OUT/libref_cpuls.so"
+
+# The PN correlator of the receive driver (rx_and_corr.cpp:329-360), spliced
+# into oracle/pn_ref_harness.cpp in place of its marker line: from the `temp`
+# vector's declaration to the closing brace of `if (corr_flag == false)`.
+awk -v harness="$HERE/pn_ref_harness.cpp" '
+  FNR == NR { if ($0 ~ /std::vector<std::complex<float> > temp\(num_rx_samps\);/) on = 1
+              if (on) { blk = blk $0 "\n"; if ($0 ~ /if \(corr_flag == false\)/) seen = 1
+                        if (seen && $0 ~ /^\t\t}$/) { on = 0; seen = 0; done = 1 } }
+              next }
+  /@@REFERENCE_CORRELATOR_BLOCK@@/ { if (!done) { print "#error correlator block not found"; next }
+                                     printf "%s", blk; next }
+  { print }
+' "$REF/rx_and_corr.cpp" "$HERE/pn_ref_harness.cpp" |
+  g++ -O2 -fPIC -shared -x c++ - -o "$OUT/libref_pn.so"
+echo "built $OUT/libref_pn.so"

@@ -1,18 +1,23 @@
 // rx_writer_harness.cpp -- TEST INFRASTRUCTURE ONLY (oracle/build_drivers.sh).
 //
 // main() for the reference's own ring-writer code: build_drivers.sh feeds
-// g++ rx_and_corr.cpp's include/configuration block (rx_and_corr.cpp:48-60:
-// #include "ShMemSymBuff_gpu.hpp", mode, buffPtr, copy_buff, cp_size) and its
-// copy_to_shared_mem (rx_and_corr.cpp:64-87) unchanged, straight from
-// /root/reference, in front of this file; the UHD/boost radio loop around
-// them cannot be built here.  This main plays the part of that loop after
-// frame sync (rx_and_corr.cpp:298-302, 366-399): it fills copy_buff with
+// g++ rx_and_corr.cpp's include/configuration block (rx_and_corr.cpp:48-61:
+// #include "ShMemSymBuff_gpu.hpp", mode, buffPtr, the SIGINT flag,
+// copy_buff, cp_size) and its copy_to_shared_mem (rx_and_corr.cpp:64-87)
+// unchanged, straight from /root/reference, in front of this file; the
+// UHD/boost radio loop around them cannot be built here.  This main plays the
+// part of that loop (rx_and_corr.cpp:296-305, 366-399): copy_buff holds
 // numOfRows channels of numSymbols*(FFT_size+cp_size) samples read from a
-// file (channel-major), opens the ring as master, calls
-// copy_to_shared_mem(numOfRows) -- numSymbols writeNextSymbolNoWait calls
-// with the cyclic prefix dropped -- and waits (bounded) for the reader to
-// detach.  usage: rx_writer <iq file> <cp_size>
+// file (channel-major), the ring is opened as master, and -- as the radio
+// loop hands over one synchronised frame per buffer pair until SIGINT -- the
+// same frame is pushed with copy_to_shared_mem(numOfRows) (numSymbols
+// writeNextSymbolNoWait calls, cyclic prefix dropped) every 50 ms until
+// SIGINT or until the reader detaches.  The repetition matters: the NoWait
+// writer never waits for the reader, so a reader that attaches late (a GPU
+// driver initialising HIP) catches a later frame, exactly as it would behind
+// the radio.  usage: rx_writer <iq file> <cp_size>
 #include <chrono>
+#include <csignal>
 #include <thread>
 
 int main(int argc, char **argv) {
@@ -28,13 +33,16 @@ int main(int argc, char **argv) {
         std::fprintf(stderr, "rx_writer: short input file\n");
         return 1;
     }
+    std::signal(SIGINT, &sig_int_handler);
     buffPtr = new ShMemSymBuff(shmemID, mode);
-    copy_to_shared_mem(numOfRows);
     CSharedMemSimple view(shmemID, sizeof(symbolBuffer));
     auto *sb = static_cast<symbolBuffer *>(view.ptr());
-    for (int t = 0; t < 120000 && __atomic_load_n(&sb->size, __ATOMIC_ACQUIRE) != -1; ++t)
-        std::this_thread::sleep_for(std::chrono::milliseconds(1));
-    std::printf("rx_writer: %d symbols\n", numSymbols);
+    int frames = 0;
+    for (; frames < 2400 && !stop_signal_called && __atomic_load_n(&sb->size, __ATOMIC_ACQUIRE) != -1; ++frames) {
+        copy_to_shared_mem(numOfRows);
+        std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    }
+    std::printf("rx_writer: %d frames of %d symbols\n", frames, numSymbols);
     delete buffPtr;
     return 0;
 }

@@ -14,6 +14,7 @@ the 157.3 TFLOPS vector peak counts an FMA as 2).  CPU baseline: the oracle
 import argparse
 import json
 import os
+os.environ.setdefault("OFDM_LSMRC_LIB", "ab")  # the A/B build: OFDM_AB_* switches
 import sys
 import time
 
@@ -43,7 +44,7 @@ def main():
     # A/B of the exact MAC form (packed VOP3P vs scalar; bit-identical), same process
     ab = {}
     for pk in ("0", "1", "0", "1"):
-        os.environ["OFDM_PN_PK"] = pk
+        os.environ["OFDM_AB_PN_PK"] = pk
         ofdm.pn_correlate(db, dp, 0.5)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
@@ -52,7 +53,7 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         ab["packed" if pk == "1" else "scalar"] = e0.elapsed_time(e1) / a.reps
-    os.environ.pop("OFDM_PN_PK")
+    os.environ.pop("OFDM_AB_PN_PK")
     res["ab_ms"] = ab
     for want_mag in (False, True):
         pos, _ = ofdm.pn_correlate(db, dp, 0.5, mag=want_mag)  # warm-up

@@ -15,6 +15,7 @@ plain C, 1 thread) on a bounded sample."""
 import argparse
 import json
 import os
+os.environ.setdefault("OFDM_LSMRC_LIB", "ab")  # the A/B build: OFDM_AB_* switches
 import sys
 import time
 
@@ -68,22 +69,22 @@ def main():
         t_tr = timed(lambda: ofdm.zf_transpose(W), a.reps)
         ab = {}
         if a.ab:  # same-process A/B of the kernel variants (env knobs are read per launch)
-            variants = {"lds": {"OFDM_ZF_LDS": "1"}, "lds_8x4": {"OFDM_ZF_LDS": "1", "OFDM_ZF_ST": "4"},
-                        "lds_nt": {"OFDM_ZF_LDS": "1", "OFDM_ZF_NT": "1"},
-                        "dma": {"OFDM_ZF_LDS": "2"}, "regtile": {"OFDM_ZF_LDS": "0"},
-                        "mfma_sg2": {"OFDM_ZF_LDS": "3", "OFDM_ZF_SG": "2"},
-                        "mfma_sg4": {"OFDM_ZF_LDS": "3", "OFDM_ZF_SG": "4"},
-                        "mfma_sg8": {"OFDM_ZF_LDS": "3", "OFDM_ZF_SG": "8"},
-                        "mfma_lds_sg4": {"OFDM_ZF_LDS": "4", "OFDM_ZF_SG": "4"},
-                        "mfma_lds_sg8": {"OFDM_ZF_LDS": "4", "OFDM_ZF_SG": "8"},
-                        "mfma_lds8": {"OFDM_ZF_LDS": "5"}, "mfma_lds8_m32": {"OFDM_ZF_LDS": "6"}, "mfma_w128": {"OFDM_ZF_LDS": "7"}, "mfma_wstat": {"OFDM_ZF_LDS": "8"}, "mfma_wstat_xmap": {"OFDM_ZF_LDS": "9"}, "mfma_wstat64": {"OFDM_ZF_LDS": "10"}, "lds_xmap": {"OFDM_ZF_LDS": "1", "OFDM_ZF_XMAP": "1"},
-                        "diag_nomac_lds_sg4": {"OFDM_ZF_LDS": "4", "OFDM_ZF_SG": "4", "OFDM_ZF_DEBUG": "1"}}
+            variants = {"lds": {"OFDM_AB_ZF_LDS": "1"}, "lds_8x4": {"OFDM_AB_ZF_LDS": "1", "OFDM_AB_ZF_ST": "4"},
+                        "lds_nt": {"OFDM_AB_ZF_LDS": "1", "OFDM_AB_ZF_NT": "1"},
+                        "dma": {"OFDM_AB_ZF_LDS": "2"}, "regtile": {"OFDM_AB_ZF_LDS": "0"},
+                        "mfma_sg2": {"OFDM_AB_ZF_LDS": "3", "OFDM_AB_ZF_SG": "2"},
+                        "mfma_sg4": {"OFDM_AB_ZF_LDS": "3", "OFDM_AB_ZF_SG": "4"},
+                        "mfma_sg8": {"OFDM_AB_ZF_LDS": "3", "OFDM_AB_ZF_SG": "8"},
+                        "mfma_lds_sg4": {"OFDM_AB_ZF_LDS": "4", "OFDM_AB_ZF_SG": "4"},
+                        "mfma_lds_sg8": {"OFDM_AB_ZF_LDS": "4", "OFDM_AB_ZF_SG": "8"},
+                        "mfma_lds8": {"OFDM_AB_ZF_LDS": "5"}, "mfma_lds8_m32": {"OFDM_AB_ZF_LDS": "6"}, "mfma_w128": {"OFDM_AB_ZF_LDS": "7"}, "mfma_wstat": {"OFDM_AB_ZF_LDS": "8"}, "mfma_wstat_xmap": {"OFDM_AB_ZF_LDS": "9"}, "mfma_wstat64": {"OFDM_AB_ZF_LDS": "10"}, "lds_xmap": {"OFDM_AB_ZF_LDS": "1", "OFDM_AB_ZF_XMAP": "1"},
+                        "diag_nomac_lds_sg4": {"OFDM_AB_ZF_LDS": "4", "OFDM_AB_ZF_SG": "4", "OFDM_AB_ZF_DEBUG": "1"}}
             ref_d = ofdm.zf_detect(Wt, Y)  # default dispatch: every variant's outputs are checked against it
             ref_a = ofdm.zf_apply(Wt, X)
             diffs = {}
             for rnd in range(2):
                 for key, env in variants.items():
-                    for v in ("OFDM_ZF_LDS", "OFDM_ZF_NT", "OFDM_ZF_ST", "OFDM_ZF_SG", "OFDM_ZF_DEBUG", "OFDM_ZF_XMAP"):
+                    for v in ("OFDM_AB_ZF_LDS", "OFDM_AB_ZF_NT", "OFDM_AB_ZF_ST", "OFDM_AB_ZF_SG", "OFDM_AB_ZF_DEBUG", "OFDM_AB_ZF_XMAP"):
                         os.environ.pop(v, None)
                     os.environ.update(env)
                     d = timed(lambda: ofdm.zf_detect(Wt, Y, out=Xo), a.reps)
@@ -93,7 +94,7 @@ def main():
                     if rnd == 0:  # max |out - default| / max |default|, detect and apply
                         diffs[key] = [float((Xo - ref_d).abs().max() / ref_d.abs().max()),
                                       float((Yo - ref_a).abs().max() / ref_a.abs().max())]
-            for v in ("OFDM_ZF_LDS", "OFDM_ZF_NT", "OFDM_ZF_ST", "OFDM_ZF_SG", "OFDM_ZF_DEBUG", "OFDM_ZF_XMAP"):
+            for v in ("OFDM_AB_ZF_LDS", "OFDM_AB_ZF_NT", "OFDM_AB_ZF_ST", "OFDM_AB_ZF_SG", "OFDM_AB_ZF_DEBUG", "OFDM_AB_ZF_XMAP"):
                 os.environ.pop(v, None)
         t_det = timed(lambda: ofdm.zf_detect(Wt, Y, out=Xo), a.reps)
         t_app = timed(lambda: ofdm.zf_apply(Wt, X, out=Yo), a.reps)

@@ -47,7 +47,7 @@ def build(tmp, name, R, C, prefix, S, shm):
                                           ("r8_c2048_s3_cp16", "cpuls"),
                                           ("r4_c256_s5_cp32", "frame"),
                                           ("r8_c2048_s3_cp16", "frame"),
-                                          ("r64_c1024_s2", "frame")])
+                                          ("r16_c1024_s4_2frames", "frame")])
 def test_ring_to_output_file(tmp_path, fixture, flow):
     z = np.load(os.path.join(GOLDEN, fixture + ".npz"), allow_pickle=False)
     iq = z["iq"][0]  # first frame: S x R x (C + prefix)
