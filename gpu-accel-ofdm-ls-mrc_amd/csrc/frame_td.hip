@@ -112,7 +112,9 @@ __global__ void __launch_bounds__(256) k_ls_td1024(const float2 *__restrict__ iq
 // One antenna row of the prefetching loop: a[] holds this row on entry and
 // the next row (`next`, when PREF) on exit.
 // DBG (A/B build only, wrong results by design): bit 0 no barriers around
-// the Hc exchange, bit 1 no Hc traffic at all, bit 2 no output stores.
+// the Hc exchange, bit 1 no Hc traffic at all, bit 2 no epilogue, bit 3 the
+// epilogue without its global stores, bit 4 no |H|^2 loads and divides, bit
+// 5 plain instead of nontemporal output stores (correct results).
 template <bool PREF, int DBG = 0>
 __device__ __forceinline__ void hlds_row_pf(const float2 *next, const float4 *hrow, int t, float2 (&a)[16],
                                             float2 *T, const float2 *tw1, const float2 *tw2,
@@ -239,7 +241,8 @@ k_mrc_td1024_hlds(const float2 *__restrict__ iq, int S, int R, int prefix, const
     // Stage the K outputs in this wave's transpose image (free after the last
     // row; its padding tails still hold other waves' Hc words, so index it as
     // [16][TP]) at their final positions, then store them as 16 contiguous
-    // 512-B wave stores instead of 4 scattered 128-B runs per instruction.
+    // 512-B nontemporal wave stores instead of 4 scattered 128-B runs per
+    // instruction.
     const int b0 = lane_bin0(t);
     float2 *o = out + q * K;
     const float *Pf = P + f * C + b0;
@@ -250,8 +253,10 @@ k_mrc_td1024_hlds(const float2 *__restrict__ iq, int S, int R, int prefix, const
         float2 v = acc[k];
         int j = b - 1;
         if ((mode & 1) == 0) {
-            const float pv = Pf[16 * k];
-            v = float2{acc[k].x / pv, acc[k].y / pv};
+            if (!(DBG & 16)) {
+                const float pv = Pf[16 * k];
+                v = float2{acc[k].x / pv, acc[k].y / pv};
+            }
             j = out_pos(b - 1, K);
         }
         T[(j >> 6) * hlds::TP + (j & 63)] = v;
@@ -260,9 +265,20 @@ k_mrc_td1024_hlds(const float2 *__restrict__ iq, int S, int R, int prefix, const
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
         const int j = t + 64 * m;
-        if (j < K) o[j] = T[m * hlds::TP + t];
+        if (j < K) {
+            const float2 v = T[m * hlds::TP + t];
+            if (DBG & 8) {  // diagnostic: the epilogue without its global stores
+                if (v.x == 1234.5f) o[j] = v;
+            } else if (DBG & 32) {  // A/B: plain stores
+                o[j] = v;
+            } else {  // nontemporal (streaming) stores: 2-3 % faster than plain ones
+                __builtin_nontemporal_store(__builtin_bit_cast(unsigned long long, v),
+                                            reinterpret_cast<unsigned long long *>(o + j));
+            }
+        }
     }
 }
+
 
 }  // namespace td1024
 
@@ -293,6 +309,9 @@ hipError_t launch_mrc_td1024(const float2 *iq, long long nframes, int S, int R, 
         case 2: kern = k_mrc_td1024_hlds<2>; break;
         case 4: kern = k_mrc_td1024_hlds<4>; break;
         case 6: kern = k_mrc_td1024_hlds<6>; break;
+        case 8: kern = k_mrc_td1024_hlds<8>; break;
+        case 16: kern = k_mrc_td1024_hlds<16>; break;
+        case 32: kern = k_mrc_td1024_hlds<32>; break;
         default: break;
     }
 #endif

@@ -127,8 +127,8 @@ __global__ void __launch_bounds__(256) k_ls_td2048(const float2 *__restrict__ iq
 // ---------------------------------------------------------------------------
 constexpr int MRC_WAVES = 4;
 
-// DBG (A/B build only, wrong results by design): bit 1 no Hc loads, bit 2 no
-// output stores.
+// DBG (A/B build only): bit 1 no Hc loads, bit 2 no output stores (both
+// wrong results by design), bit 3 the round-1 epilogue (scattered plain stores).
 template <int DBG = 0>
 __global__ void __attribute__((amdgpu_flat_work_group_size(256, 256), amdgpu_waves_per_eu(2, 2)))
 k_mrc_td2048(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
@@ -179,25 +179,61 @@ k_mrc_td2048(const float2 *__restrict__ iq, int S, int R, int prefix, const floa
     }
     const int b0 = lane_bin0(t);
     float2 *o = out + q * K;
+    if (DBG & 8) {  // A/B: the round-1 epilogue, scattered plain stores
+        if ((mode & 1) == 0) {
+            const float *Pf = P + f * C;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const int be = 2 * (b0 + 16 * k);
+                if (be > 0) {
+                    const float pv = Pf[be];
+                    o[out_pos(be - 1, K)] = float2{ae[k].x / pv, ae[k].y / pv};
+                }
+                const float pv = Pf[be + 1];
+                o[out_pos(be, K)] = float2{ao[k].x / pv, ao[k].y / pv};
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const int be = 2 * (b0 + 16 * k);
+                if (be > 0) o[be - 1] = ae[k];
+                o[be] = ao[k];
+            }
+        }
+        return;
+    }
+    // normalise, then stage the 2047 outputs through this wave's transpose
+    // image in two halves of 1024 positions and store each half as 16
+    // contiguous 512-B nontemporal wave stores (instead of 32 scattered ones)
     if ((mode & 1) == 0) {
         const float *Pf = P + f * C;
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             const int be = 2 * (b0 + 16 * k);
-            if (be > 0) {
-                const float pv = Pf[be];
-                o[out_pos(be - 1, K)] = float2{ae[k].x / pv, ae[k].y / pv};
-            }
-            const float pv = Pf[be + 1];
-            o[out_pos(be, K)] = float2{ao[k].x / pv, ao[k].y / pv};
+            const float pe = Pf[be], po = Pf[be + 1];  // Pf[0] = 1: the DC slot
+            ae[k] = float2{ae[k].x / pe, ae[k].y / pe};
+            ao[k] = float2{ao[k].x / po, ao[k].y / po};
         }
-    } else {
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             const int be = 2 * (b0 + 16 * k);
-            if (be > 0) o[be - 1] = ae[k];
-            o[be] = ao[k];
+            const int je = (mode & 1) ? be - 1 : out_pos(be - 1, K);  // be = 0: the DC bin, no output
+            const int jo = (mode & 1) ? be : out_pos(be, K);
+            if (be > 0 && (je >> 10) == h) T[((je & 1023) >> 6) * hl::TP + (je & 63)] = ae[k];
+            if ((jo >> 10) == h) T[((jo & 1023) >> 6) * hl::TP + (jo & 63)] = ao[k];
         }
+        td1024::wave_lds_sync();
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            const int j = 1024 * h + t + 64 * m;
+            if (j < K)
+                __builtin_nontemporal_store(__builtin_bit_cast(unsigned long long, T[m * hl::TP + t]),
+                                            reinterpret_cast<unsigned long long *>(o + j));
+        }
+        td1024::wave_lds_sync();
     }
 }
 
@@ -228,6 +264,7 @@ hipError_t launch_mrc_td2048(const float2 *iq, long long nframes, int S, int R, 
         case 2: kern = k_mrc_td2048<2>; break;
         case 4: kern = k_mrc_td2048<4>; break;
         case 6: kern = k_mrc_td2048<6>; break;
+        case 8: kern = k_mrc_td2048<8>; break;
         default: break;
     }
 #endif

@@ -200,7 +200,9 @@ __device__ __forceinline__ void dma_hc_row(const float2 *g, unsigned lds) {
 // barrier, into the buffer every wave finished with in row r-1.
 // DBG (A/B build only, wrong results by design): bit 0 no workgroup barriers
 // (racy exchange and Hc), bit 1 no Hc DMA (Hc read from stale LDS), bit 2 no
-// output stores.
+// output stores, bit 3 no second (exchange-read) barrier, bit 4 no first
+// (exchange-write / Hc-publish) barrier, bit 5 the round-1 epilogue
+// (scattered plain stores; correct results).
 template <int E, int PK, bool PREF, int DBG = 0>
 __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const float2 *__restrict__ hr,
                                       int t, float2 *T, const float2 *Tp, const float2 *tw1,
@@ -219,14 +221,14 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
 #pragma unroll
     for (int m = 0; m < 16; ++m) T[hl::swz(m, t)] = F(E ? u[m] : v[m]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this row's Hc DMA landed
-    if (!(DBG & 1)) td1024::lds_barrier();
+    if (!(DBG & 1) && !(DBG & 16)) td1024::lds_barrier();
     if (!(DBG & 2) && hnext) dma_hc_row(hnext, hb_next);
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
         if (E) u[m] = V(Tp[hl::swz(m, t)]);  // b
         else v[m] = V(Tp[hl::swz(m, t)]);    // c
     }
-    if (!(DBG & 1)) td1024::lds_barrier();  // the partner has read T before the FFT reuses it
+    if (!(DBG & 1) && !(DBG & 8)) td1024::lds_barrier();  // the partner has read T before the FFT reuses it
     // E = 0: u = a, v = c:  z0 = a + c, z2 = (a - c) W^(2 n0)
     // E = 1: u = b, v = d:  z1 = (b + (-i) d) W^(n0), z3 = (b - (-i) d) W^(3 n0)
 #pragma unroll
@@ -365,36 +367,79 @@ k_mrc_td4096h(const float2 *__restrict__ iq, int S, int R, int prefix, const flo
         h_rows<1, H_PK, DBG>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
     else
         h_rows<0, H_PK, DBG>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
-    if (!store) return;
     const long long q = f * nsym + j;
+    const int b0 = lane_bin0(t);
+    float2 *o = out + q * K;
+    const float *Pf = P + f * C;
     if (DBG & 4) {  // diagnostic: no output stores (keep the sums live)
         float sacc = 0.f;
 #pragma unroll
         for (int k = 0; k < 16; ++k) sacc += ae[k].x + ao[k].y;
-        if (sacc == 1234.5f) out[q] = float2{sacc, 0.f};
+        if (store && sacc == 1234.5f) out[q] = float2{sacc, 0.f};
         return;
     }
-    const int b0 = lane_bin0(t);
-    float2 *o = out + q * K;
-    const float *Pf = P + f * C;
+    if (DBG & 32) {  // A/B: the round-1 epilogue, scattered plain stores
+        if (!store) return;
+        if ((mode & 1) == 0) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const int be = 4 * (b0 + 16 * k) + e;
+                if (be > 0) {
+                    const float pv = Pf[be];
+                    o[out_pos(be - 1, K)] = float2{ae[k].x / pv, ae[k].y / pv};
+                }
+                const float pv = Pf[be + 2];
+                o[out_pos(be + 1, K)] = float2{ao[k].x / pv, ao[k].y / pv};
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const int be = 4 * (b0 + 16 * k) + e;
+                if (be > 0) o[be - 1] = ae[k];
+                o[be + 1] = ao[k];
+            }
+        }
+        return;
+    }
+    // Normalise, then stage the pair's 4095 outputs through its two transpose
+    // images, 1024 positions per image and pass (pass h in image h & 1), and
+    // store them as contiguous 512-B nontemporal wave stores: wave e stores
+    // the image it owns.  Every wave (tail pairs too) takes part in the
+    // workgroup barriers; only storing pairs write memory.
     if ((mode & 1) == 0) {
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             const int be = 4 * (b0 + 16 * k) + e;
-            if (be > 0) {
-                const float pv = Pf[be];
-                o[out_pos(be - 1, K)] = float2{ae[k].x / pv, ae[k].y / pv};
-            }
-            const float pv = Pf[be + 2];
-            o[out_pos(be + 1, K)] = float2{ao[k].x / pv, ao[k].y / pv};
+            const float pe = Pf[be], po = Pf[be + 2];  // Pf[0] = 1: the DC slot
+            ae[k] = float2{ae[k].x / pe, ae[k].y / pe};
+            ao[k] = float2{ao[k].x / po, ao[k].y / po};
         }
-    } else {
+    }
+    float2 *Tpair = lds + X_TAB + 2 * pair * hl::TS;  // images of waves 2 pair, 2 pair + 1
+    td1024::lds_barrier();  // both waves are done with their last transposes
+#pragma unroll
+    for (int h0 = 0; h0 < 4; h0 += 2) {
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             const int be = 4 * (b0 + 16 * k) + e;
-            if (be > 0) o[be - 1] = ae[k];
-            o[be + 1] = ao[k];
+            const int je = (mode & 1) ? be - 1 : out_pos(be - 1, K);  // be = 0: the DC bin, no output
+            const int jo = (mode & 1) ? be + 1 : out_pos(be + 1, K);
+            const int he = je >> 10, ho = jo >> 10;
+            if (be > 0 && (he >> 1) == (h0 >> 1))
+                Tpair[(he & 1) * hl::TS + ((je & 1023) >> 6) * hl::TP + (je & 63)] = ae[k];
+            if ((ho >> 1) == (h0 >> 1)) Tpair[(ho & 1) * hl::TS + ((jo & 1023) >> 6) * hl::TP + (jo & 63)] = ao[k];
         }
+        td1024::lds_barrier();
+        if (store) {
+#pragma unroll
+            for (int m = 0; m < 16; ++m) {
+                const int jj = 1024 * (h0 + e) + t + 64 * m;
+                if (jj < K)
+                    __builtin_nontemporal_store(__builtin_bit_cast(unsigned long long, T[m * hl::TP + t]),
+                                                reinterpret_cast<unsigned long long *>(o + jj));
+            }
+        }
+        td1024::lds_barrier();
     }
 }
 
@@ -424,6 +469,9 @@ hipError_t launch_mrc_td4096(const float2 *iq, long long nframes, int S, int R, 
         case 2: kern = k_mrc_td4096h<2>; break;
         case 4: kern = k_mrc_td4096h<4>; break;
         case 6: kern = k_mrc_td4096h<6>; break;
+        case 8: kern = k_mrc_td4096h<8>; break;
+        case 16: kern = k_mrc_td4096h<16>; break;
+        case 32: kern = k_mrc_td4096h<32>; break;
         default: break;
     }
 #endif

@@ -8,9 +8,10 @@
 // U*R <= 8192): G = A A^H is U x U x R, the inverse U^3, W = A^H G^-1 is
 // R x U x U.  One 1023-subcarrier channel set at U = 16, R = 64 is ~0.3 GFLOP
 // -- a few microseconds of VALU next to ~16 MB of HBM traffic.
-//   k_zf_precoder: one 256-thread workgroup per subcarrier; A (U x R) and the
-//     augmented [G | I] in LDS; Gauss-Jordan with partial pivoting (pivot =
-//     first max of |re| + |im|, LAPACK's icamax in cgetrf).  W is written in
+//   k_zf_precoder: one 256-thread workgroup per subcarrier; A (U x R) and G
+//     in LDS; LU with partial pivoting (pivot = first max of |re| + |im|,
+//     LAPACK's icamax in cgetrf) and the inverse in cgetri's order, with no
+//     fused multiply-adds -- bit-identical to the oracle.  W is written in
 //     the reference's layout W[k][u][r] (per subcarrier R x U column-major)
 //     and/or the subcarrier-fastest layout Wt[u][r][k] the apply / detect
 //     kernels read with coalesced loads.
@@ -51,75 +52,137 @@ __device__ __forceinline__ float2 crcp(float2 a) {  // 1 / a
 
 constexpr int MAXU = 32;
 
+// 1 / a by Smith's algorithm (what LAPACK's ONE / A(J,J) compiles to under
+// gfortran's complex-division rules): the oracle (oracle/zf_oracle.c) uses
+// the same formula, so with contraction off the precoder is bit-identical.
+__device__ __forceinline__ float2 crcp_smith(float2 a) {
+#pragma clang fp contract(off)
+    if (fabsf(a.x) >= fabsf(a.y)) {
+        const float r = a.y / a.x, den = a.x + a.y * r;
+        return float2{1.f / den, -r / den};
+    }
+    const float r = a.x / a.y, den = a.x * r + a.y;
+    return float2{r / den, -1.f / den};
+}
+__device__ __forceinline__ float2 cmul_nc(float2 a, float2 b) {  // a * b, no contraction
+#pragma clang fp contract(off)
+    return float2{a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x};
+}
+
+// One 256-thread workgroup per subcarrier.  G = A A^H, its LU factors with
+// partial pivoting (LAPACK cgetf2: pivot = first max of |re| + |im|), the
+// inverse from them as cgetri computes it (ctrti2 on U, then inv(A) L =
+// inv(U) column by column from the right, then the column interchanges), and
+// W = A^H G^-1 -- every element accumulated in the oracle's order with no
+// fused multiply-adds, the independent elements of each step in parallel.
 __global__ void __launch_bounds__(256) k_zf_precoder(const float2 *__restrict__ Hin, int U, int R, int K,
                                                      float2 *__restrict__ W, float2 *__restrict__ Wt) {
+#pragma clang fp contract(off)
     extern __shared__ float2 sm[];
     float2 *A = sm;          // A(u, r) at A[r*U + u]: X[col] after rotCube (cpuLS.hpp:404-410)
-    float2 *M = sm + U * R;  // [U][2U] augmented [G | I], row-major
-    __shared__ float2 fac[MAXU];
-    __shared__ int piv;
-    const int t = threadIdx.x, k = blockIdx.x, U2 = 2 * U;
+    float2 *G = sm + U * R;  // U x U column-major: G(i, c) at G[c*U + i]
+    __shared__ float2 col[MAXU];
+    __shared__ int ipiv[MAXU];
+    const int t = threadIdx.x, k = blockIdx.x, n = U;
 
     for (int e = t; e < U * R; e += 256) {
         const int u = e / R, r = e - u * R;
         A[r * U + u] = Hin[((long long)u * R + r) * K + k];
     }
     __syncthreads();
-    // G(a, b) = sum_r A(a, r) conj(A(b, r))   (cgemm NoTrans / ConjTrans, 437)
+    // G(a, b) = sum_r A(a, r) conj(A(b, r))   (cgemm NoTrans / ConjTrans, cpuLS.hpp:437)
     for (int e = t; e < U * U; e += 256) {
         const int a = e % U, b = e / U;
         float2 s{0.f, 0.f};
         for (int r = 0; r < R; ++r) {
             const float2 x = A[r * U + a], y = A[r * U + b];
-            s.x += x.x * y.x + x.y * y.y;
-            s.y += x.y * y.x - x.x * y.y;
+            s.x = s.x + (x.x * y.x + x.y * y.y);
+            s.y = s.y + (x.y * y.x - x.x * y.y);
         }
-        M[a * U2 + b] = s;
-        M[a * U2 + U + b] = float2{a == b ? 1.f : 0.f, 0.f};
+        G[b * n + a] = s;
     }
     __syncthreads();
-    // Gauss-Jordan with partial pivoting: [G | I] -> [I | G^-1]  (cgetrf + cgetri, 438-439)
-    for (int j = 0; j < U; ++j) {
+    // cgetrf (unblocked cgetf2), cpuLS.hpp:438
+    for (int j = 0; j < n; ++j) {
         if (t == 0) {
             int p = j;
-            float best = cabs1(M[j * U2 + j]);
-            for (int i = j + 1; i < U; ++i) {
-                const float v = cabs1(M[i * U2 + j]);
-                if (v > best) { best = v; p = i; }
-            }
-            piv = p;
+            for (int i = j + 1; i < n; ++i)
+                if (cabs1(G[j * n + i]) > cabs1(G[j * n + p])) p = i;
+            ipiv[j] = p;
         }
         __syncthreads();
-        const int p = piv;
-        if (p != j)
-            for (int c = t; c < U2; c += 256) {
-                const float2 tmp = M[j * U2 + c];
-                M[j * U2 + c] = M[p * U2 + c];
-                M[p * U2 + c] = tmp;
+        const int p = ipiv[j];
+        const float2 gp = G[j * n + p];
+        const bool nz = gp.x != 0.f || gp.y != 0.f;
+        if (nz && p != j)
+            for (int c = t; c < n; c += 256) {
+                const float2 tmp = G[c * n + j];
+                G[c * n + j] = G[c * n + p];
+                G[c * n + p] = tmp;
             }
         __syncthreads();
-        const float2 inv = crcp(M[j * U2 + j]);
-        for (int i = t; i < U; i += 256) fac[i] = M[i * U2 + j];
-        __syncthreads();  // pivot and column j read before row j is scaled
-        for (int c = t; c < U2; c += 256) M[j * U2 + c] = cmul(M[j * U2 + c], inv);
+        if (nz) {
+            const float2 rj = crcp_smith(G[j * n + j]);
+            for (int i = j + 1 + t; i < n; i += 256) G[j * n + i] = cmul_nc(G[j * n + i], rj);
+        }
         __syncthreads();
-        for (int e = t; e < U * U2; e += 256) {
-            const int i = e / U2, c = e - i * U2;
-            if (i == j) continue;
-            const float2 f = fac[i], m = M[j * U2 + c];
-            M[i * U2 + c] = float2{M[i * U2 + c].x - (f.x * m.x - f.y * m.y),
-                                   M[i * U2 + c].y - (f.x * m.y + f.y * m.x)};
+        for (int e = t; e < (n - j - 1) * (n - j - 1); e += 256) {
+            const int c = j + 1 + e / (n - j - 1), i = j + 1 + e % (n - j - 1);
+            const float2 m = cmul_nc(G[j * n + i], G[c * n + j]);
+            G[c * n + i] = float2{G[c * n + i].x - m.x, G[c * n + i].y - m.y};
         }
         __syncthreads();
     }
-    // W(r, u) = sum_a conj(A(a, r)) Ginv(a, u)   (cgemm ConjTrans / NoTrans, 440)
+    // cgetri, cpuLS.hpp:439.  ctrti2: column j of inv(U) from the inverted
+    // columns 0..j-1: x(i) = orig(i,j) U^-1(i,i) + sum_{c=i+1}^{j-1} orig(c,j)
+    // U^-1(i,c), then x(i) * (-U^-1(j,j))
+    for (int j = 0; j < n; ++j) {
+        if (t < j) col[t] = G[j * n + t];
+        const float2 djj = crcp_smith(G[j * n + j]);  // read before thread 0 overwrites it
+        __syncthreads();
+        if (t < j) {
+            float2 x = cmul_nc(col[t], G[t * n + t]);
+            for (int c = t + 1; c < j; ++c) {
+                const float2 m = cmul_nc(col[c], G[c * n + t]);
+                x = float2{x.x + m.x, x.y + m.y};
+            }
+            G[j * n + t] = cmul_nc(x, float2{-djj.x, -djj.y});
+        }
+        if (t == 0) G[j * n + j] = djj;
+        __syncthreads();
+    }
+    // inv(A) L = inv(U), columns right to left: column j -= sum_{c>j} col c * L(c, j)
+    for (int j = n - 1; j >= 0; --j) {
+        if (t > j && t < n) col[t] = G[j * n + t];
+        __syncthreads();
+        if (t < n) {
+            float2 x = t > j ? float2{0.f, 0.f} : G[j * n + t];
+            for (int c = j + 1; c < n; ++c) {
+                const float2 m = cmul_nc(G[c * n + t], col[c]);
+                x = float2{x.x - m.x, x.y - m.y};
+            }
+            G[j * n + t] = x;
+        }
+        __syncthreads();
+    }
+    // the row interchanges, undone as column interchanges, last first
+    for (int j = n - 2; j >= 0; --j) {
+        const int p = ipiv[j];
+        if (p != j && t < n) {
+            const float2 tmp = G[j * n + t];
+            G[j * n + t] = G[p * n + t];
+            G[p * n + t] = tmp;
+        }
+        __syncthreads();
+    }
+    // W(r, u) = sum_a conj(A(a, r)) Ginv(a, u)   (cgemm ConjTrans / NoTrans, cpuLS.hpp:440)
     for (int e = t; e < R * U; e += 256) {
         const int u = e / R, r = e - u * R;
         float2 s{0.f, 0.f};
         for (int a = 0; a < U; ++a) {
-            const float2 c = cmulc(A[r * U + a], M[a * U2 + U + u]);
-            s.x += c.x;
-            s.y += c.y;
+            const float2 x = A[r * U + a], g = G[u * n + a];
+            s.x = s.x + (x.x * g.x + x.y * g.y);
+            s.y = s.y + (x.x * g.y - x.y * g.x);
         }
         if (W) W[(long long)k * R * U + u * R + r] = s;
         if (Wt) Wt[((long long)u * R + r) * K + k] = s;
@@ -1216,7 +1279,7 @@ k_zf_wstat(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__rest
 }  // namespace zf
 
 size_t zf_precoder_lds_bytes(int U, int R) {
-    return ((size_t)U * R + (size_t)U * 2 * U) * sizeof(float2);
+    return ((size_t)U * R + (size_t)U * U) * sizeof(float2);
 }
 
 hipError_t launch_zf_precoder(const float2 *Hin, int U, int R, int K, float2 *W, float2 *Wt,

@@ -11,7 +11,8 @@
  * restated in single-precision complex: straightforward cgemm / cgemv sums,
  * unblocked LU with partial pivoting (LAPACK cgetf2: pivot = first max of
  * |re| + |im|, icamax), and cgetri's inverse (invert U, solve inv(A) L =
- * inv(U), undo the column interchanges).
+ * inv(U), undo the column interchanges); complex reciprocals by Smith's
+ * algorithm, as gfortran compiles LAPACK's ONE / A(J,J).
  */
 #include <complex.h>
 #include <math.h>
@@ -29,6 +30,19 @@ static inline void st(oracle_cf32 *p, cf v) {
 }
 static inline float cabs1(cf v) { return fabsf(crealf(v)) + fabsf(cimagf(v)); }
 
+/* 1 / a by Smith's algorithm: LAPACK's ONE / A(J,J) (cgetf2, ctrti2) under
+ * gfortran's complex-division rules (-fcx-fortran-rules: Smith, no scaling),
+ * rather than C's __divsc3. */
+static inline cf crcp(cf a) {
+    const float c = crealf(a), d = cimagf(a);
+    if (fabsf(c) >= fabsf(d)) {
+        const float r = d / c, den = c + d * r;
+        return CMPLXF(1.0f / den, -r / den);
+    }
+    const float r = c / d, den = c * r + d;
+    return CMPLXF(r / den, -1.0f / den);
+}
+
 /* cgetrf (unblocked cgetf2) on an n x n column-major matrix a (lda = n) */
 static int lu(cf *a, int n, int *ipiv) {
     int info = 0;
@@ -44,7 +58,7 @@ static int lu(cf *a, int n, int *ipiv) {
                     a[c * n + j] = a[c * n + p];
                     a[c * n + p] = t;
                 }
-            const cf r = 1.0f / a[j * n + j];
+            const cf r = crcp(a[j * n + j]);
             for (int i = j + 1; i < n; i++) a[j * n + i] *= r;
         } else if (!info) {
             info = j + 1;
@@ -59,7 +73,7 @@ static int lu(cf *a, int n, int *ipiv) {
 static void lu_inverse(cf *a, int n, const int *ipiv) {
     /* ctrtri: invert the upper triangle U in place (unblocked ctrti2, non-unit) */
     for (int j = 0; j < n; j++) {
-        a[j * n + j] = 1.0f / a[j * n + j];
+        a[j * n + j] = crcp(a[j * n + j]);
         const cf ajj = -a[j * n + j];
         /* x = triu(inv(U))[0..j-1, 0..j-1] * a[0..j-1, j]  (ctrmv, upper, no-trans) */
         for (int c = 0; c < j; c++) {

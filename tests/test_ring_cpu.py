@@ -54,3 +54,20 @@ def test_host_mirror_headers_compile(tmp_path):
                     f"-I{HOST}", f"-I{os.path.join(ROOT, 'include')}", str(src),
                     "-o", str(tmp_path / "t"), f"-L{lib}", "-lofdm_lsmrc",
                     "-L/opt/rocm/lib", "-lamdhip64", "-lrt"], check=True)
+
+
+@pytest.mark.parametrize("L,prefix,n,mode", [(5, 3, 40, "wait"), (101, 0, 250, "wait"), (8, 2, 30, "nowait")])
+def test_ring_protocol_under_tsan(tmp_path, L, prefix, n, mode):
+    """Writer and reader threads on ONE ring object under ThreadSanitizer
+    (the reference's plain-int ring races; here the slots and
+    indices must be ordered by the acquire/release protocol)."""
+    exe = tmp_path / "ring_tsan"
+    subprocess.run(["g++", "-O1", "-g", "-fsanitize=thread", "-std=c++17", f"-I{HOST}", "-DnumOfRows=2",
+                    "-Ddimension=16", f"-Dprefix={prefix}", f"-DlenOfBuffer={L}",
+                    f"-DshmemID=\"/ofdm_tsan_{os.getpid()}_{L}_{mode}\"", os.path.join(CPP, "ring_tsan.cpp"),
+                    "-o", str(exe), "-lrt"], check=True)
+    r = subprocess.run([str(exe), str(n), mode], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, TSAN_OPTIONS="halt_on_error=1 exitcode=66"))
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ThreadSanitizer" not in r.stderr, r.stderr
+    assert r.stdout.startswith("ok")

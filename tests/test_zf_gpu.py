@@ -3,10 +3,10 @@ SURVEY.md 8(f) rank 4) against the oracle restatement of
 createZeroForcingMatrix / multiplyWithChannelInv (cpuLS.hpp:400-463).
 
 Tolerances (floating point, written here as the north_star asks):
-  * precoder: the reference inverts G = A A^H with LAPACK cgetrf + cgetri,
-    the oracle restates that LU algorithm, the GPU runs Gauss-Jordan with the
-    same partial pivoting -- equal up to f32 rounding amplified by cond(G):
-    per-subcarrier norm-relative <= 2e-4 on these well-conditioned channels;
+  * precoder: the reference inverts G = A A^H with LAPACK cgetrf + cgetri;
+    the oracle restates that LU algorithm and the GPU computes it in the same
+    order (every element accumulated in the oracle's order, no fused
+    multiply-adds, Smith's reciprocal on both sides): bit-identical;
   * apply / detect: the same sums in a different association (FMA
     contraction): norm-relative <= 1e-5;
   * transpose and the two output layouts of the precoder: bit-equal.
@@ -33,7 +33,7 @@ def test_zf_precoder_parity(ofdm, oracle, dev, U, R, K):
     ref = oracle.zf_precoder(H)
     W, Wt = ofdm.zf_precoder(dev_t(H, dev))
     W, Wt = W.cpu().numpy(), Wt.cpu().numpy()
-    assert rel_err_per_subcarrier(W, ref) < 2e-4
+    assert np.array_equal(W, ref), f"max per-subcarrier rel. err {rel_err_per_subcarrier(W, ref):.2e}"
     assert np.array_equal(Wt, W.transpose(1, 2, 0))
     Wt2 = ofdm.zf_transpose(dev_t(W, dev)).cpu().numpy()
     assert np.array_equal(Wt2, Wt)
@@ -86,7 +86,7 @@ def test_cpuls_zf_call_sequence(oracle, dev, tmp_path):
     subprocess.run([exe, str(R), str(cols), str(U)], cwd=tmp_path, check=True, timeout=120)
     W = np.fromfile(tmp_path / "W.bin", np.complex64).reshape(K, U, R)
     ref = oracle.zf_precoder(H)
-    assert rel_err_per_subcarrier(W, ref) < 2e-4
+    assert np.array_equal(W, ref)
     Xrot = np.fromfile(tmp_path / "Xrot.bin", np.complex64)
     assert np.array_equal(Xrot, H.transpose(2, 1, 0).ravel())  # [col][row][user]
     HX = np.fromfile(tmp_path / "HX.bin", np.complex64).reshape(R, K)
