@@ -114,7 +114,8 @@ __global__ void __launch_bounds__(256) k_ls_td1024(const float2 *__restrict__ iq
 // DBG (A/B build only, wrong results by design): bit 0 no barriers around
 // the Hc exchange, bit 1 no Hc traffic at all, bit 2 no epilogue, bit 3 the
 // epilogue without its global stores, bit 4 no |H|^2 loads and divides, bit
-// 5 plain instead of nontemporal output stores (correct results).
+// 5 plain instead of nontemporal output stores (correct results), bit 6 no
+// IQ loads after the first row (compute and synchronisation only).
 template <bool PREF, int DBG = 0>
 __device__ __forceinline__ void hlds_row_pf(const float2 *next, const float4 *hrow, int t, float2 (&a)[16],
                                             float2 *T, const float2 *tw1, const float2 *tw2,
@@ -126,7 +127,7 @@ __device__ __forceinline__ void hlds_row_pf(const float2 *next, const float4 *hr
     // a row is 512 float4: each of the 512 threads moves 16 B
     const float4 hreg = (DBG & 2) ? float4{1.f, 0.f, 0.f, 1.f} : hrow[threadIdx.x];
     __builtin_amdgcn_sched_barrier(0);
-    if (PREF) row_load<true>(next, t, a);
+    if (PREF && !(DBG & 64)) row_load<true>(next, t, a);
     row_fft_b(t, T, tw2, x);
     if (!(DBG & 1)) lds_barrier();  // every wave is done with the previous Hc row
     if (!(DBG & 2)) *mine = hreg;
@@ -234,7 +235,7 @@ k_mrc_td1024_hlds(const float2 *__restrict__ iq, int S, int R, int prefix, const
     if (DBG & 4) {  // diagnostic: no output stores (keep the sums live)
         float sacc = 0.f;
 #pragma unroll
-        for (int k = 0; k < 16; ++k) sacc += acc[k].x;
+        for (int k = 0; k < 16; ++k) sacc += acc[k].x * acc[k].y;
         if (sacc == 1234.5f) out[q] = float2{sacc, 0.f};
         return;
     }
@@ -312,6 +313,7 @@ hipError_t launch_mrc_td1024(const float2 *iq, long long nframes, int S, int R, 
         case 8: kern = k_mrc_td1024_hlds<8>; break;
         case 16: kern = k_mrc_td1024_hlds<16>; break;
         case 32: kern = k_mrc_td1024_hlds<32>; break;
+        case 64: kern = k_mrc_td1024_hlds<64>; break;
         default: break;
     }
 #endif

@@ -41,13 +41,21 @@ __device__ __forceinline__ void fill_tables(float2 *lds) {
 }
 
 // FFT of one 2048-sample row (src) -> xe[k] = X[2 b], xo[k] = X[2 b + 1]
-template <bool NT>
+template <bool NT, bool LOAD = true>
 __device__ __forceinline__ void row_fft2048(const float2 *__restrict__ src, int t, float2 *T,
                                             const float2 *lds, float2 (&xe)[16], float2 (&xo)[16]) {
     const float2 *tw1 = lds, *tw2 = lds + hl::TW1S, *twv = lds + hl::TW1S + hl::TW2S;
     float2 u[16], v[16];
-    row_load<NT>(src, t, u);
-    row_load<NT>(src + HALF, t, v);
+    if (LOAD) {
+        row_load<NT>(src, t, u);
+        row_load<NT>(src + HALF, t, v);
+    } else {  // diagnostic: the previous row's spectrum stands in for the samples
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            u[m] = xe[m];
+            v[m] = xo[m];
+        }
+    }
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
         const float2 d = csub(u[m], v[m]);
@@ -128,7 +136,8 @@ __global__ void __launch_bounds__(256) k_ls_td2048(const float2 *__restrict__ iq
 constexpr int MRC_WAVES = 4;
 
 // DBG (A/B build only): bit 1 no Hc loads, bit 2 no output stores (both
-// wrong results by design), bit 3 the round-1 epilogue (scattered plain stores).
+// wrong results by design), bit 3 the round-1 epilogue (scattered plain stores),
+// bit 6 no IQ loads after the first row (compute only).
 template <int DBG = 0>
 __global__ void __attribute__((amdgpu_flat_work_group_size(256, 256), amdgpu_waves_per_eu(2, 2)))
 k_mrc_td2048(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
@@ -155,9 +164,12 @@ k_mrc_td2048(const float2 *__restrict__ iq, int S, int R, int prefix, const floa
     float2 ae[16], ao[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) ae[k] = ao[k] = float2{0.f, 0.f};
+    float2 xe[16], xo[16];
     for (int r = 0; r < R; ++r) {
-        float2 xe[16], xo[16];
-        row_fft2048<true>(sym + (long long)r * Cp, t, T, lds, xe, xo);
+        if ((DBG & 64) && r > 0)
+            row_fft2048<true, false>(sym, t, T, lds, xe, xo);
+        else
+            row_fft2048<true>(sym + (long long)r * Cp, t, T, lds, xe, xo);
         __builtin_amdgcn_sched_barrier(0);
         const float4 *hr = Hf + (long long)r * (C / 2);
         // matrixMultThenSum (cpuLS.hpp:203-204), antennas in order
@@ -173,7 +185,7 @@ k_mrc_td2048(const float2 *__restrict__ iq, int S, int R, int prefix, const floa
     if (DBG & 4) {  // diagnostic: no output stores (keep the sums live)
         float sacc = 0.f;
 #pragma unroll
-        for (int k = 0; k < 16; ++k) sacc += ae[k].x + ao[k].y;
+        for (int k = 0; k < 16; ++k) sacc += ae[k].x * ae[k].y + ao[k].x * ao[k].y;
         if (sacc == 1234.5f) out[q] = float2{sacc, 0.f};
         return;
     }
@@ -265,6 +277,7 @@ hipError_t launch_mrc_td2048(const float2 *iq, long long nframes, int S, int R, 
         case 4: kern = k_mrc_td2048<4>; break;
         case 6: kern = k_mrc_td2048<6>; break;
         case 8: kern = k_mrc_td2048<8>; break;
+        case 64: kern = k_mrc_td2048<64>; break;
         default: break;
     }
 #endif

@@ -202,8 +202,14 @@ __device__ __forceinline__ void dma_hc_row(const float2 *g, unsigned lds) {
 // (racy exchange and Hc), bit 1 no Hc DMA (Hc read from stale LDS), bit 2 no
 // output stores, bit 3 no second (exchange-read) barrier, bit 4 no first
 // (exchange-write / Hc-publish) barrier, bit 5 the round-1 epilogue
-// (scattered plain stores; correct results).
-template <int E, int PK, bool PREF, int DBG = 0>
+// (scattered plain stores; correct results), bit 6 no IQ loads after the
+// first row (compute and synchronisation only), bit 7 the row loads alone
+// (no FFT, MAC or Hc; with bit 0 not even the per-row barrier).
+// TW: twiddles by recurrence from one per-lane base (hlds::tw_powers) in the
+// first (bit 0) / second (bit 1) half of each 1024-point FFT instead of 15
+// table reads each: 3-3.5 % faster here (2 waves/SIMD, where the table reads
+// issue one LDS round trip at a time), slower in the C = 1024 / 2048 kernels.
+template <int E, int PK, bool PREF, int DBG = 0, int TW = 3>
 __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const float2 *__restrict__ hr,
                                       int t, float2 *T, const float2 *Tp, const float2 *tw1,
                                       const float2 *tw2, pk::v2f wb0, pk::v2f wb1, float2 (&a)[16],
@@ -272,8 +278,8 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
     };
 #pragma unroll
     for (int m = 0; m < 16; ++m) z[m] = F(u[m]);
-    hl::row_fft_a<PK>(z, t, T, tw1);
-    hl::row_fft_b<PK>(t, T, tw2, x);
+    hl::row_fft_a<PK, (TW & 1) != 0>(z, t, T, tw1);
+    hl::row_fft_b<PK, (TW & 2) != 0>(t, T, tw2, x);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int k = 0; k < 16; ++k) h[k] = hr[k * 64 + t];  // plane 0: bins 4 b + E, from LDS
@@ -282,7 +288,7 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
     mac(ae);
     __builtin_amdgcn_sched_barrier(0);
     // next row in flight during the second FFT and the next row's exchange
-    if (PREF) {
+    if (PREF && !(DBG & 64)) {
         row_load<true>(next + 1024 * E, t, a);
         row_load<true>(next + 1024 * (E + 2), t, b);
     }
@@ -290,8 +296,8 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
     for (int k = 0; k < 16; ++k) h[k] = h1[k];
 #pragma unroll
     for (int m = 0; m < 16; ++m) z[m] = F(v[m]);
-    hl::row_fft_a<PK>(z, t, T, tw1);
-    hl::row_fft_b<PK>(t, T, tw2, x);
+    hl::row_fft_a<PK, (TW & 1) != 0>(z, t, T, tw1);
+    hl::row_fft_b<PK, (TW & 2) != 0>(t, T, tw2, x);
     mac(ao);
 }
 
@@ -311,25 +317,42 @@ constexpr int H_PAIRS = 4;
 constexpr size_t H_LDS = (size_t)(X_TAB + 2 * H_PAIRS * hl::TS + 2 * C) * sizeof(float2);
 static_assert(H_LDS <= 160 * 1024, "one workgroup per CU");
 
-template <int E, int PK, int DBG = 0>
+template <int E, int PK, int DBG = 0, int TW = 3>
 __device__ __forceinline__ void h_rows(const float2 *sym, int Cp, int R, const float2 *Hg, float2 *HB, int t,
                                        float2 *T, const float2 *Tp, const float2 *tw1, const float2 *tw2,
                                        pk::v2f wb0, pk::v2f wb1, float2 (&ae)[16], float2 (&ao)[16]) {
     float2 a[16], b[16];
     row_load<true>(sym + 1024 * E, t, a);
     row_load<true>(sym + 1024 * (E + 2), t, b);
+    if constexpr ((DBG & 128) != 0) {  // diagnostic: the row loads alone, one row prefetched
+        for (int r = 0; r < R; ++r) {
+            float2 a2[16], b2[16];
+            const float2 *nx = sym + (long long)(r + 1 < R ? r + 1 : r) * Cp;
+            row_load<true>(nx + 1024 * E, t, a2);
+            row_load<true>(nx + 1024 * (E + 2), t, b2);
+#pragma unroll
+            for (int m = 0; m < 16; ++m) {
+                ae[m] = float2{ae[m].x + a[m].x, ae[m].y + a[m].y};
+                ao[m] = float2{ao[m].x + b[m].x, ao[m].y + b[m].y};
+                a[m] = a2[m];
+                b[m] = b2[m];
+            }
+            if (!(DBG & 1)) td1024::lds_barrier();
+        }
+        return;
+    }
     const unsigned hb0 = lds_addr(HB), hb1 = lds_addr(HB + C);
     for (int r = 0; r + 1 < R; ++r)
-        x_row<E, PK, true, DBG>(sym + (long long)(r + 1) * Cp, HB + (r & 1) * C + E * 2048, t, T, Tp,
+        x_row<E, PK, true, DBG, TW>(sym + (long long)(r + 1) * Cp, HB + (r & 1) * C + E * 2048, t, T, Tp,
                                         tw1, tw2, wb0, wb1, a, b, ae, ao, Hg + (long long)(r + 1) * C,
                                         (r & 1) ? hb0 : hb1);
-    x_row<E, PK, false, DBG>(sym, HB + ((R - 1) & 1) * C + E * 2048, t, T, Tp, tw1, tw2, wb0, wb1, a,
+    x_row<E, PK, false, DBG, TW>(sym, HB + ((R - 1) & 1) * C + E * 2048, t, T, Tp, tw1, tw2, wb0, wb1, a,
                                      b, ae, ao, nullptr, 0);
 }
 
 constexpr int H_PK = 7;  // packed-f32 split, FFT halves and MAC (pk.hpp)
 
-template <int DBG = 0>
+template <int DBG = 0, int TW = 3>
 __global__ void __attribute__((amdgpu_flat_work_group_size(128 * H_PAIRS, 128 * H_PAIRS),
                                amdgpu_waves_per_eu(2, 2)))
 k_mrc_td4096h(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
@@ -364,9 +387,9 @@ k_mrc_td4096h(const float2 *__restrict__ iq, int S, int R, int prefix, const flo
 #pragma unroll
     for (int k = 0; k < 16; ++k) ae[k] = ao[k] = float2{0.f, 0.f};
     if (e)
-        h_rows<1, H_PK, DBG>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
+        h_rows<1, H_PK, DBG, TW>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
     else
-        h_rows<0, H_PK, DBG>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
+        h_rows<0, H_PK, DBG, TW>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
     const long long q = f * nsym + j;
     const int b0 = lane_bin0(t);
     float2 *o = out + q * K;
@@ -374,7 +397,7 @@ k_mrc_td4096h(const float2 *__restrict__ iq, int S, int R, int prefix, const flo
     if (DBG & 4) {  // diagnostic: no output stores (keep the sums live)
         float sacc = 0.f;
 #pragma unroll
-        for (int k = 0; k < 16; ++k) sacc += ae[k].x + ao[k].y;
+        for (int k = 0; k < 16; ++k) sacc += ae[k].x * ae[k].y + ao[k].x * ao[k].y;
         if (store && sacc == 1234.5f) out[q] = float2{sacc, 0.f};
         return;
     }
@@ -443,6 +466,7 @@ k_mrc_td4096h(const float2 *__restrict__ iq, int S, int R, int prefix, const flo
     }
 }
 
+
 }  // namespace td4096
 
 hipError_t launch_ls_td4096(const float2 *iq, long long nframes, int S, int R, int prefix,
@@ -468,12 +492,15 @@ hipError_t launch_mrc_td4096(const float2 *iq, long long nframes, int S, int R, 
         case 1: kern = k_mrc_td4096h<1>; break;
         case 2: kern = k_mrc_td4096h<2>; break;
         case 4: kern = k_mrc_td4096h<4>; break;
-        case 6: kern = k_mrc_td4096h<6>; break;
         case 8: kern = k_mrc_td4096h<8>; break;
         case 16: kern = k_mrc_td4096h<16>; break;
         case 32: kern = k_mrc_td4096h<32>; break;
+        case 64: kern = k_mrc_td4096h<64>; break;
+        case 65: kern = k_mrc_td4096h<65>; break;
+        case 128: kern = k_mrc_td4096h<128>; break;
         default: break;
     }
+    if (ab_knob("MRC4K_TW", 3) == 0) kern = k_mrc_td4096h<0, 0>;  // table twiddles (round 1)
 #endif
     if (hipError_t e = opt_in_lds(reinterpret_cast<const void *>(kern), (int)H_LDS); e != hipSuccess)
         return e;  // > 64 KiB of dynamic LDS

@@ -241,10 +241,51 @@ __device__ __forceinline__ void fill(float2 *tw1, float2 *tw2) {
 // index of (row, col) in a transpose image
 __device__ __forceinline__ int swz(int row, int col) { return row * TP + col; }
 
+// Twiddles w^k, k = 1..15, of a per-lane base w (one LDS read) by two
+// interleaved recurrences of depth 7 (w^(k+2) = w^k w^2) instead of 15 table
+// reads: register-starved kernels otherwise issue the reads one round trip
+// at a time.  v[k] *= s w^k for k >= 1.
+template <int N>
+__device__ __forceinline__ void tw_powers(pk::v2f (&v)[N], pk::v2f w, pk::v2f sw) {
+    const pk::v2f w2 = pk::cmul(w, w);
+    pk::v2f po = sw, pe = pk::cmul(sw, w);
+    v[1] = pk::cmul(v[1], po);
+    v[2] = pk::cmul(v[2], pe);
+#pragma unroll
+    for (int k = 3; k < N; k += 2) {
+        po = pk::cmul(po, w2);
+        v[k] = pk::cmul(v[k], po);
+        if (k + 1 < N) {
+            pe = pk::cmul(pe, w2);
+            v[k + 1] = pk::cmul(v[k + 1], pe);
+        }
+    }
+}
+
 // first half: radix-16 over m, twiddles, transpose write.  PK: packed-f32
-// butterflies and twiddle multiplies (pk.hpp).
-template <int PK = 0>
+// butterflies and twiddle multiplies (pk.hpp).  TWR: twiddles by recurrence
+// from W1024^t (tw_powers) instead of 15 table reads.
+template <int PK = 0, bool TWR = false>
 __device__ __forceinline__ void row_fft_a(float2 (&a)[16], int t, float2 *T, const float2 *tw1) {
+    if constexpr (TWR) {
+        pk::v2f v[16];
+#pragma unroll
+        for (int m = 0; m < 16; ++m) v[m] = pk::V(a[m]);
+        if constexpr ((PK & 1) != 0) {
+            pk::fft_reg<16>(v);
+        } else {
+#pragma unroll
+            for (int m = 0; m < 16; ++m) a[m] = pk::F(v[m]);
+            fft_reg<16, false>(a);
+#pragma unroll
+            for (int m = 0; m < 16; ++m) v[m] = pk::V(a[m]);
+        }
+        const pk::v2f w = pk::V(tw1[t]);  // W1024^t
+        tw_powers(v, w, w);
+#pragma unroll
+        for (int k2 = 0; k2 < 16; ++k2) T[swz(k2, t)] = pk::F(v[k2]);
+        return;
+    }
     if constexpr (PK & 1) {
         pk::v2f v[16];
 #pragma unroll
@@ -262,8 +303,9 @@ __device__ __forceinline__ void row_fft_a(float2 (&a)[16], int t, float2 *T, con
 #pragma unroll
     for (int k2 = 0; k2 < 16; ++k2) T[swz(k2, t)] = a[k2];
 }
-// second half: transpose read, radix-16, twiddles, quad DFT
-template <int PK = 0>
+// second half: transpose read, radix-16, twiddles, quad DFT.  TWR: the
+// twiddles g(a) W64^(a k) by recurrence from tw2[4 + a] = g(a) W64^a.
+template <int PK = 0, bool TWR = false>
 __device__ __forceinline__ void row_fft_b(int t, float2 *T, const float2 *tw2, float2 (&x)[16]) {
     wave_lds_sync();
     const int q = t >> 2, qa = t & 3;
@@ -271,7 +313,23 @@ __device__ __forceinline__ void row_fft_b(int t, float2 *T, const float2 *tw2, f
     for (int l = 0; l < 16; ++l) x[l] = T[swz(q, qa + 4 * l)];
     wave_lds_sync();
     const float g = quad_g(qa);
-    if constexpr (PK & 2) {
+    if constexpr (TWR) {
+        pk::v2f v[16];
+        if constexpr ((PK & 2) != 0) {
+#pragma unroll
+            for (int m = 0; m < 16; ++m) v[m] = pk::V(x[m]);
+            pk::fft_reg<16>(v);
+        } else {
+            fft_reg<16, false>(x);
+#pragma unroll
+            for (int m = 0; m < 16; ++m) v[m] = pk::V(x[m]);
+        }
+        v[0] = pk::scale(v[0], g);
+        const pk::v2f gw = pk::V(tw2[4 + qa]);  // g W64^a
+        tw_powers(v, pk::scale(gw, g), gw);
+#pragma unroll
+        for (int m = 0; m < 16; ++m) x[m] = pk::F(v[m]);
+    } else if constexpr (PK & 2) {
         pk::v2f v[16];
 #pragma unroll
         for (int m = 0; m < 16; ++m) v[m] = pk::V(x[m]);
