@@ -23,6 +23,7 @@ python bench.py [--gpus N] [--steps K] [--warmup W]
 torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
 """
 import argparse
+import glob
 import json
 import os
 import sys
@@ -121,14 +122,19 @@ def cpu_baseline(args, X, ofdm, torch, dev):
 
 
 def pmc_traffic(path, cfg):
-    try:
-        with open(path) as fp:
-            d = json.load(fp)
-    except (OSError, ValueError):
-        return None, None
-    if any(d.get("config", {}).get(k) != cfg[k] for k in ("R", "C", "S", "frames_per_gpu", "prefix")):
-        return None, None
-    return d.get("mrc_hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+    """Corrected PMC HBM bytes per MRC launch for this exact config: `path`
+    (profiles/pmc_traffic.json, the default shape) or else the latest-tagged
+    profiles/r*_traffic.json written by scripts/pmc_summary.py for it."""
+    cands = [path] + sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")), reverse=True)
+    for p in cands:
+        try:
+            with open(p) as fp:
+                d = json.load(fp)
+        except (OSError, ValueError):
+            continue
+        if all(d.get("config", {}).get(k) == cfg[k] for k in ("R", "C", "S", "frames_per_gpu", "prefix")):
+            return d.get("mrc_hbm_bytes_per_launch"), os.path.relpath(p, ROOT)
+    return None, None
 
 
 def main():

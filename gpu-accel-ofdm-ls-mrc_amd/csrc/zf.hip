@@ -308,7 +308,7 @@ __global__ void __launch_bounds__(256) k_zf_gemm(const float2 *__restrict__ Wt, 
 // ST = 4, NC = 1 (OFDM_ZF_ST=4): 8x4 tiles, 64 accumulator VGPRs, 4 waves/SIMD.
 // XMAP (OFDM_ZF_XMAP=1): XCD x takes symbol chunks x, x + 8, ... with all
 // tiles (the k_zf_wstat map) instead of tiles x, x + 8, ... with all chunks.
-template <int MG, bool CONJ, bool NTIN = false, int ST = 8, int NC = 2, bool XMAP = false>
+template <int MG, bool CONJ, bool NTIN = false, int ST = 8, int NC = 2, bool XMAP = false, bool NTOUT = false>
 __global__ void __attribute__((amdgpu_flat_work_group_size(256, 256), amdgpu_waves_per_eu(ST == 4 ? 4 : 1)))
 k_zf_gemm_lds(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__restrict__ in, int N, int M,
               int K, long long nsym, float2 *__restrict__ out, int ntile, int tpx, int nkb,
@@ -399,8 +399,14 @@ k_zf_gemm_lds(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__r
                     if (s0 + jj >= nsym) break;
                     float2 *o = out + ((s0 + jj) * M) * (long long)K + k;
 #pragma unroll
-                    for (int i = 0; i < MT; ++i)
-                        if (m0 + i < M) o[(long long)(m0 + i) * K] = acc[i][jj];
+                    for (int i = 0; i < MT; ++i) {
+                        if (m0 + i >= M) continue;
+                        if constexpr (NTOUT)  // streamed out: keep the re-read A tiles in L2
+                            __builtin_nontemporal_store(__builtin_bit_cast(unsigned long long, acc[i][jj]),
+                                                        reinterpret_cast<unsigned long long *>(o + (long long)(m0 + i) * K));
+                        else
+                            o[(long long)(m0 + i) * K] = acc[i][jj];
+                    }
                 }
             }
 #pragma unroll
@@ -1345,24 +1351,36 @@ hipError_t gemm_lds_launch(const float2 *Wt, int a_m, int a_n, const float2 *in,
     if (chunk_steps < 4) chunk_steps = 4;
     nchunk = (nsteps + chunk_steps - 1) / chunk_steps;
     const long long blocks = 8LL * tpx * nchunk;
-    if (ab_knob("ZF_XMAP", 0) && ST == 8 && !DMA) {
-        const long long nc8 = (nchunk + 7) / 8 * 8;  // one chunk per XCD per round; empty chunks return
-        hipLaunchKernelGGL((zf::k_zf_gemm_lds<MG, CONJ, false, 8, 2, true>), dim3((unsigned)(ntile * nc8)), dim3(256),
-                           0, s, Wt, a_m, a_n, in, N, M, K, nsym, out, ntile, tpx, nkb, chunk_steps);
-        return hipGetLastError();
-    }
-    if (ST == 4)  // 8x4 tiles, one n per LDS chunk, 4 waves/SIMD
+#ifdef OFDM_AB_KNOBS
+    if constexpr (ST == 4) {  // 8x4 tiles, one n per LDS chunk, 4 waves/SIMD
         hipLaunchKernelGGL((zf::k_zf_gemm_lds<MG, CONJ, false, 4, 1>), dim3((unsigned)blocks), dim3(256), 0, s,
                            Wt, a_m, a_n, in, N, M, K, nsym, out, ntile, tpx, nkb, chunk_steps);
-    else if (DMA)
+        return hipGetLastError();
+    } else if constexpr (DMA) {
         hipLaunchKernelGGL((zf::k_zf_gemm_dma<MG, CONJ>), dim3((unsigned)blocks), dim3(256), 0, s, Wt, a_m,
                            a_n, in, N, M, K, nsym, out, ntile, tpx, nkb, chunk_steps);
-    else if (ab_knob("ZF_NT", 0))  // nontemporal input stream
-        hipLaunchKernelGGL((zf::k_zf_gemm_lds<MG, CONJ, true>), dim3((unsigned)blocks), dim3(256), 0, s, Wt,
-                           a_m, a_n, in, N, M, K, nsym, out, ntile, tpx, nkb, chunk_steps);
-    else
-        hipLaunchKernelGGL((zf::k_zf_gemm_lds<MG, CONJ>), dim3((unsigned)blocks), dim3(256), 0, s, Wt, a_m,
-                           a_n, in, N, M, K, nsym, out, ntile, tpx, nkb, chunk_steps);
+        return hipGetLastError();
+    } else {
+        if (ab_knob("ZF_XMAP", 0)) {
+            const long long nc8 = (nchunk + 7) / 8 * 8;  // one chunk per XCD per round; empty chunks return
+            hipLaunchKernelGGL((zf::k_zf_gemm_lds<MG, CONJ, false, 8, 2, true>), dim3((unsigned)(ntile * nc8)),
+                               dim3(256), 0, s, Wt, a_m, a_n, in, N, M, K, nsym, out, ntile, tpx, nkb, chunk_steps);
+            return hipGetLastError();
+        }
+        if (ab_knob("ZF_NT", 0)) {  // nontemporal input stream
+            hipLaunchKernelGGL((zf::k_zf_gemm_lds<MG, CONJ, true>), dim3((unsigned)blocks), dim3(256), 0, s, Wt,
+                               a_m, a_n, in, N, M, K, nsym, out, ntile, tpx, nkb, chunk_steps);
+            return hipGetLastError();
+        }
+        if (ab_knob("ZF_NTOUT", 0)) {  // nontemporal output stream
+            hipLaunchKernelGGL((zf::k_zf_gemm_lds<MG, CONJ, false, 8, 2, false, true>), dim3((unsigned)blocks),
+                               dim3(256), 0, s, Wt, a_m, a_n, in, N, M, K, nsym, out, ntile, tpx, nkb, chunk_steps);
+            return hipGetLastError();
+        }
+    }
+#endif
+    hipLaunchKernelGGL((zf::k_zf_gemm_lds<MG, CONJ>), dim3((unsigned)blocks), dim3(256), 0, s, Wt, a_m,
+                       a_n, in, N, M, K, nsym, out, ntile, tpx, nkb, chunk_steps);
     return hipGetLastError();
 }
 
