@@ -308,7 +308,7 @@ __global__ void __launch_bounds__(256) k_zf_gemm(const float2 *__restrict__ Wt, 
 // ST = 4, NC = 1 (OFDM_ZF_ST=4): 8x4 tiles, 64 accumulator VGPRs, 4 waves/SIMD.
 // XMAP (OFDM_ZF_XMAP=1): XCD x takes symbol chunks x, x + 8, ... with all
 // tiles (the k_zf_wstat map) instead of tiles x, x + 8, ... with all chunks.
-template <int MG, bool CONJ, bool NTIN = false, int ST = 8, int NC = 2, bool XMAP = false, bool NTOUT = false>
+template <int MG, bool CONJ, bool NTIN = false, int ST = 8, int NC = 2, bool XMAP = false>
 __global__ void __attribute__((amdgpu_flat_work_group_size(256, 256), amdgpu_waves_per_eu(ST == 4 ? 4 : 1)))
 k_zf_gemm_lds(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__restrict__ in, int N, int M,
               int K, long long nsym, float2 *__restrict__ out, int ntile, int tpx, int nkb,
@@ -399,14 +399,8 @@ k_zf_gemm_lds(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__r
                     if (s0 + jj >= nsym) break;
                     float2 *o = out + ((s0 + jj) * M) * (long long)K + k;
 #pragma unroll
-                    for (int i = 0; i < MT; ++i) {
-                        if (m0 + i >= M) continue;
-                        if constexpr (NTOUT)  // streamed out: keep the re-read A tiles in L2
-                            __builtin_nontemporal_store(__builtin_bit_cast(unsigned long long, acc[i][jj]),
-                                                        reinterpret_cast<unsigned long long *>(o + (long long)(m0 + i) * K));
-                        else
-                            o[(long long)(m0 + i) * K] = acc[i][jj];
-                    }
+                    for (int i = 0; i < MT; ++i)
+                        if (m0 + i < M) o[(long long)(m0 + i) * K] = acc[i][jj];
                 }
             }
 #pragma unroll
@@ -1370,11 +1364,6 @@ hipError_t gemm_lds_launch(const float2 *Wt, int a_m, int a_n, const float2 *in,
         if (ab_knob("ZF_NT", 0)) {  // nontemporal input stream
             hipLaunchKernelGGL((zf::k_zf_gemm_lds<MG, CONJ, true>), dim3((unsigned)blocks), dim3(256), 0, s, Wt,
                                a_m, a_n, in, N, M, K, nsym, out, ntile, tpx, nkb, chunk_steps);
-            return hipGetLastError();
-        }
-        if (ab_knob("ZF_NTOUT", 0)) {  // nontemporal output stream
-            hipLaunchKernelGGL((zf::k_zf_gemm_lds<MG, CONJ, false, 8, 2, false, true>), dim3((unsigned)blocks),
-                               dim3(256), 0, s, Wt, a_m, a_n, in, N, M, K, nsym, out, ntile, tpx, nkb, chunk_steps);
             return hipGetLastError();
         }
     }
