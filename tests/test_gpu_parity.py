@@ -115,6 +115,9 @@ CONFIGS = [
     (2, 3, 64, 2048, 0),
     (1, 2, 32, 4096, 0),
     (2, 3, 8, 4096, 5),
+    (2, 7, 1, 4096, 0),   # one antenna row; the second workgroup of each frame has two idle pairs
+    (1, 10, 3, 4096, 1),  # odd R, 9 data symbols: 4 + 4 + 1 pairs
+    (2, 6, 1, 2048, 0),
     (3, 4, 3, 2048, 9),
     (3, 6, 4, 256, 16),
     (2, 3, 2, 4, 1),
