@@ -182,13 +182,14 @@ __device__ __forceinline__ pk::v2f dif_tw(pk::v2f base) {  // base * W64^(CM * M
 using td1024::dma16;
 using td1024::lds_addr;
 
-// One 32 KiB Hc row (4096 float2) into LDS by a 512-thread workgroup: four
+// One 32 KiB Hc row (4096 float2) into LDS by an NW-wave workgroup: 32 / NW
 // wave-instructions of 1 KiB per wave, natural order.
+template <int NW = 8>
 __device__ __forceinline__ void dma_hc_row(const float2 *g, unsigned lds) {
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const char *src = reinterpret_cast<const char *>(g) + w * 1024 + lane * 16;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) dma16(src + j * 8192, lds + j * 8192 + w * 1024);
+    for (int j = 0; j < 32 / NW; ++j) dma16(src + j * NW * 1024, lds + j * NW * 1024 + w * 1024);
 }
 
 // One antenna row for wave E of the pair.  On entry a/b hold the row's
@@ -209,7 +210,11 @@ __device__ __forceinline__ void dma_hc_row(const float2 *g, unsigned lds) {
 // first (bit 0) / second (bit 1) half of each 1024-point FFT instead of 15
 // table reads each: 3-3.5 % faster here (2 waves/SIMD, where the table reads
 // issue one LDS round trip at a time), slower in the C = 1024 / 2048 kernels.
-template <int E, int PK, bool PREF, int DBG = 0, int TW = 3>
+// HP (pairs per workgroup) = 4: Hc double buffer, the DMA of row r + 1 issued
+// after this row's first barrier.  HP = 2 (A/B candidate): ONE Hc buffer,
+// refilled after a third barrier once every wave has read both planes of this
+// row (before its second FFT) and published at the next row's second barrier.
+template <int E, int PK, bool PREF, int DBG = 0, int TW = 3, int HP = 4>
 __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const float2 *__restrict__ hr,
                                       int t, float2 *T, const float2 *Tp, const float2 *tw1,
                                       const float2 *tw2, pk::v2f wb0, pk::v2f wb1, float2 (&a)[16],
@@ -226,14 +231,15 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
     // wave 0 sends d and keeps s (= a); wave 1 sends s (= c) and keeps d
 #pragma unroll
     for (int m = 0; m < 16; ++m) T[hl::swz(m, t)] = F(E ? u[m] : v[m]);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this row's Hc DMA landed
+    if (HP == 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this row's Hc DMA landed
     if (!(DBG & 1) && !(DBG & 16)) td1024::lds_barrier();
-    if (!(DBG & 2) && hnext) dma_hc_row(hnext, hb_next);
+    if (HP == 4 && !(DBG & 2) && hnext) dma_hc_row(hnext, hb_next);
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
         if (E) u[m] = V(Tp[hl::swz(m, t)]);  // b
         else v[m] = V(Tp[hl::swz(m, t)]);    // c
     }
+    if (HP != 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this row's Hc DMA landed
     if (!(DBG & 1) && !(DBG & 8)) td1024::lds_barrier();  // the partner has read T before the FFT reuses it
     // E = 0: u = a, v = c:  z0 = a + c, z2 = (a - c) W^(2 n0)
     // E = 1: u = b, v = d:  z1 = (b + (-i) d) W^(n0), z3 = (b - (-i) d) W^(3 n0)
@@ -287,6 +293,10 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
     for (int k = 0; k < 16; ++k) h1[k] = hr[1024 + k * 64 + t];  // plane 1: bins 4 b + 2 + E
     mac(ae);
     __builtin_amdgcn_sched_barrier(0);
+    if (HP != 4 && PREF) {  // every wave holds both planes of this row: refill the single buffer
+        td1024::lds_barrier();
+        if (!(DBG & 2) && hnext) dma_hc_row<2 * HP>(hnext, hb_next);
+    }
     // next row in flight during the second FFT and the next row's exchange
     if (PREF && !(DBG & 64)) {
         row_load<true>(next + 1024 * E, t, a);
@@ -314,10 +324,12 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
 // workgroup (8 waves, 2 per SIMD as the 242-VGPR x kernel) per CU.
 // ---------------------------------------------------------------------------
 constexpr int H_PAIRS = 4;
-constexpr size_t H_LDS = (size_t)(X_TAB + 2 * H_PAIRS * hl::TS + 2 * C) * sizeof(float2);
+constexpr size_t h_lds(int hp) { return (size_t)(X_TAB + 2 * hp * hl::TS + (hp == 4 ? 2 : 1) * C) * sizeof(float2); }
+constexpr size_t H_LDS = h_lds(H_PAIRS);
 static_assert(H_LDS <= 160 * 1024, "one workgroup per CU");
+static_assert(2 * h_lds(2) <= 160 * 1024, "two 2-pair workgroups per CU");
 
-template <int E, int PK, int DBG = 0, int TW = 3>
+template <int E, int PK, int DBG = 0, int TW = 3, int HP = 4>
 __device__ __forceinline__ void h_rows(const float2 *sym, int Cp, int R, const float2 *Hg, float2 *HB, int t,
                                        float2 *T, const float2 *Tp, const float2 *tw1, const float2 *tw2,
                                        pk::v2f wb0, pk::v2f wb1, float2 (&ae)[16], float2 (&ao)[16]) {
@@ -342,19 +354,19 @@ __device__ __forceinline__ void h_rows(const float2 *sym, int Cp, int R, const f
         return;
     }
     const unsigned hb0 = lds_addr(HB), hb1 = lds_addr(HB + C);
+    constexpr int NB = HP == 4 ? 2 : 1;  // Hc buffers
     for (int r = 0; r + 1 < R; ++r)
-        x_row<E, PK, true, DBG, TW>(sym + (long long)(r + 1) * Cp, HB + (r & 1) * C + E * 2048, t, T, Tp,
-                                        tw1, tw2, wb0, wb1, a, b, ae, ao, Hg + (long long)(r + 1) * C,
-                                        (r & 1) ? hb0 : hb1);
-    x_row<E, PK, false, DBG, TW>(sym, HB + ((R - 1) & 1) * C + E * 2048, t, T, Tp, tw1, tw2, wb0, wb1, a,
-                                     b, ae, ao, nullptr, 0);
+        x_row<E, PK, true, DBG, TW, HP>(sym + (long long)(r + 1) * Cp, HB + (NB == 2 ? (r & 1) * C : 0) + E * 2048,
+                                        t, T, Tp, tw1, tw2, wb0, wb1, a, b, ae, ao, Hg + (long long)(r + 1) * C,
+                                        NB == 2 && !(r & 1) ? hb1 : hb0);
+    x_row<E, PK, false, DBG, TW, HP>(sym, HB + (NB == 2 ? ((R - 1) & 1) * C : 0) + E * 2048, t, T, Tp, tw1, tw2,
+                                     wb0, wb1, a, b, ae, ao, nullptr, 0);
 }
 
 constexpr int H_PK = 7;  // packed-f32 split, FFT halves and MAC (pk.hpp)
 
-template <int DBG = 0, int TW = 3>
-__global__ void __attribute__((amdgpu_flat_work_group_size(128 * H_PAIRS, 128 * H_PAIRS),
-                               amdgpu_waves_per_eu(2, 2)))
+template <int DBG = 0, int TW = 3, int HP = H_PAIRS>
+__global__ void __attribute__((amdgpu_flat_work_group_size(128 * HP, 128 * HP), amdgpu_waves_per_eu(2, 2)))
 k_mrc_td4096h(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
               const float *__restrict__ P, float2 *__restrict__ out, long long nframes, long long nblocks,
               long long per_xcd, int mode) {
@@ -364,18 +376,18 @@ k_mrc_td4096h(const float2 *__restrict__ iq, int S, int R, int prefix, const flo
     const float2 *tw1 = lds, *tw2 = lds + hl::TW1S;
     float2 *T = lds + X_TAB + w * hl::TS;
     const float2 *Tp = lds + X_TAB + (w ^ 1) * hl::TS;
-    float2 *HB = lds + X_TAB + 2 * H_PAIRS * hl::TS;  // [2][C] Hc rows
+    float2 *HB = lds + X_TAB + 2 * HP * hl::TS;  // [2][C] Hc rows ([1][C] for HP = 2)
     const long long pb = blockIdx.x;
     const long long lb = (pb & 7) * per_xcd + (pb >> 3);  // XCD-grouped: a frame's blocks share an L2
     if (lb >= nblocks) return;  // whole workgroup
     const int nsym = S - 1;
-    const long long bpf = (nsym + H_PAIRS - 1) / H_PAIRS;
+    const long long bpf = (nsym + HP - 1) / HP;
     const long long f = lb / bpf;
-    const int j = (int)(lb - f * bpf) * H_PAIRS + pair;  // data symbol index within the frame
+    const int j = (int)(lb - f * bpf) * HP + pair;  // data symbol index within the frame
     const bool store = j < nsym;
     const int s = 1 + (store ? j : nsym - 1);
     const float2 *Hg = Hc + f * (long long)R * C;
-    dma_hc_row(Hg, lds_addr(HB));  // row 0; landed at the first row's barrier
+    dma_hc_row<2 * HP>(Hg, lds_addr(HB));  // row 0; landed at the first row's barrier
     hl::fill(lds, lds + hl::TW1S);
     __syncthreads();
 
@@ -387,9 +399,9 @@ k_mrc_td4096h(const float2 *__restrict__ iq, int S, int R, int prefix, const flo
 #pragma unroll
     for (int k = 0; k < 16; ++k) ae[k] = ao[k] = float2{0.f, 0.f};
     if (e)
-        h_rows<1, H_PK, DBG, TW>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
+        h_rows<1, H_PK, DBG, TW, HP>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
     else
-        h_rows<0, H_PK, DBG, TW>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
+        h_rows<0, H_PK, DBG, TW, HP>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
     const long long q = f * nsym + j;
     const int b0 = lane_bin0(t);
     float2 *o = out + q * K;
@@ -501,6 +513,15 @@ hipError_t launch_mrc_td4096(const float2 *iq, long long nframes, int S, int R, 
         default: break;
     }
     if (ab_knob("MRC4K_TW", 3) == 0) kern = k_mrc_td4096h<0, 0>;  // table twiddles (round 1)
+    if (ab_knob("MRC4K_HP", 4) == 2) {  // two independent 2-pair workgroups per CU, single Hc buffer
+        const long long bpf2 = ((S - 1) + 1) / 2, nb2 = nframes * bpf2, px2 = (nb2 + 7) / 8;
+        if (px2 * 8 > 0x7fffffffll) return hipErrorInvalidValue;
+        auto k2 = k_mrc_td4096h<0, 3, 2>;
+        if (hipError_t e = opt_in_lds(reinterpret_cast<const void *>(k2), (int)h_lds(2)); e != hipSuccess) return e;
+        hipLaunchKernelGGL(k2, dim3((unsigned)(px2 * 8)), dim3(256), h_lds(2), s, iq, S, R, prefix, Hc, P, out,
+                           nframes, nb2, px2, mode);
+        return hipGetLastError();
+    }
 #endif
     if (hipError_t e = opt_in_lds(reinterpret_cast<const void *>(kern), (int)H_LDS); e != hipSuccess)
         return e;  // > 64 KiB of dynamic LDS
