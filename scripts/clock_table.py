@@ -1,5 +1,6 @@
 """Mean effective clock per MRC kernel variant from a rocprofv3 run with
---kernel-trace and --pmc GRBM_GUI_ACTIVE: cycles / (end - start)."""
+--kernel-trace and --pmc GRBM_GUI_ACTIVE: cycles / 8 / (end - start) -- the
+counter is summed over the 8 XCDs (MI355X_MICROARCH.md, DVFS give-back)."""
 import csv
 import glob
 import os
@@ -25,6 +26,6 @@ for k, v in cyc.items():
         name = v[0][0]
         agg[name].append((sum(x[1] for x in v), dur[k]))
 for name, v in agg.items():
-    mhz = [c / ns * 1e3 for c, ns in v]
+    mhz = [c / 8 / ns * 1e3 for c, ns in v]
     print(f"{name}: {len(v)} dispatches, {sum(ns for _, ns in v) / len(v) / 1e6:.3f} ms avg, "
           f"clock {sum(mhz) / len(mhz):.0f} MHz (min {min(mhz):.0f}, max {max(mhz):.0f})")
