@@ -21,6 +21,21 @@ def test_library_exports_header(ofdm):
     assert L.ofdm_version() == 1
 
 
+def test_product_library_reads_no_environment(ofdm):
+    """The shipped library has no experiment switches: it does not even import
+    getenv (the A/B build, lib/libofdm_lsmrc_ab.so, is the one that does)."""
+    import subprocess
+    path = ofdm.LIB_PATH
+    if path.endswith("_ab.so"):
+        pytest.skip("OFDM_LSMRC_LIB=ab selects the A/B build")
+    syms = subprocess.run(["nm", "-D", "--undefined-only", path], capture_output=True, text=True, check=True).stdout
+    assert "getenv" not in syms, "the product library must not read environment variables"
+    ab = os.path.join(os.path.dirname(path), "libofdm_lsmrc_ab.so")
+    if os.path.exists(ab):
+        syms = subprocess.run(["nm", "-D", "--undefined-only", ab], capture_output=True, text=True, check=True).stdout
+        assert "getenv" in syms
+
+
 def test_pilot_rotate_matches_oracle(ofdm, oracle):
     for K in (3, 255, 1023, 4095):
         raw = (np.arange(K) - 1j * np.arange(K)).astype(np.complex64)
