@@ -332,10 +332,40 @@ k_zf_gemm_lds(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__r
     const long long nseq = (step1 - step0) * nnc;
     if (nseq <= 0) return;  // whole workgroup
 
+    // chunk c = (symbol step cs, n-chunk cn), walked with int counters: a
+    // 64-bit c / nnc per chunk made the loop SALU-bound (22 k scalar
+    // instructions per wave against 40 k VALU at U = 16)
     float2 stg[RPT];
-    auto load = [&](long long c) {
-        const long long s0 = (step0 + c / nnc) * SB;
-        const int n0 = (int)(c % nnc) * NC;
+    // per-row element offsets of the in-range fast path, relative to the
+    // chunk's n0 (A rows) / (s0, n0) (input rows): wave-uniform, loop-invariant
+    int roff[RPT];
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+        const int row = w + 4 * i;
+        if (i < AI)
+            roff[i] = (min(mb0 + row % MB, M - 1) * a_m + (row / MB) * a_n) * K;
+        else
+            roff[i] = (((row - AROWS) % SB) * N + (row - AROWS) / SB) * K;
+    }
+    auto load = [&](int cs, int cn) {
+        const long long s0 = (step0 + cs) * SB;
+        const int n0 = cn * NC;
+        if (n0 + NC <= N && s0 + SB <= nsym) {  // whole chunk in range: one 64-bit base per operand
+            const float2 *pa = Wt + (long long)n0 * a_n * K + kc;
+            const float2 *px = in + (s0 * N + n0) * (long long)K + kc;
+#pragma unroll
+            for (int i = 0; i < RPT; ++i) {
+                if (i < AI) {
+                    stg[i] = pa[roff[i]];
+                } else if constexpr (NTIN) {
+                    stg[i] = __builtin_bit_cast(float2, __builtin_nontemporal_load(
+                                                            reinterpret_cast<const unsigned long long *>(px + roff[i])));
+                } else {
+                    stg[i] = px[roff[i]];
+                }
+            }
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < RPT; ++i) {
             const int row = w + 4 * i;
@@ -365,15 +395,18 @@ k_zf_gemm_lds(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__r
     for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int jj = 0; jj < ST; ++jj) acc[i][jj] = float2{0.f, 0.f};
-    load(0);
+    load(0, 0);
     put(0);
     __syncthreads();
-    for (long long c = 0; c < nseq; ++c) {
-        const bool more = c + 1 < nseq;
-        if (more) load(c + 1);  // in flight during this chunk's MACs
-        const float2 *sa = sm[c & 1] + (mg * MT) * 64 + lane;
-        const float2 *sx = sm[c & 1] + (AROWS + sg * ST) * 64 + lane;
-        const int n0 = (int)(c % nnc) * NC, nn = min(NC, N - n0);
+    const int nst = (int)(step1 - step0);
+    int cs = 0, cn = 0, buf = 0;
+    for (;;) {
+        const int ncn = cn + 1 == nnc ? 0 : cn + 1, ncs = cn + 1 == nnc ? cs + 1 : cs;
+        const bool more = ncs < nst;
+        if (more) load(ncs, ncn);  // in flight during this chunk's MACs
+        const float2 *sa = sm[buf] + (mg * MT) * 64 + lane;
+        const float2 *sx = sm[buf] + (AROWS + sg * ST) * 64 + lane;
+        const int n0 = cn * NC, nn = min(NC, N - n0);
         for (int n = 0; n < nn; ++n) {
             float2 a[MT], x[ST];
 #pragma unroll
@@ -390,17 +423,24 @@ k_zf_gemm_lds(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__r
                 }
             }
         }
-        if (c % nnc == nnc - 1) {  // last n-chunk of a symbol step: store, reset
-            const long long s0 = (step0 + c / nnc) * SB + sg * ST;
+        if (cn == nnc - 1) {  // last n-chunk of a symbol step: store, reset
+            const long long s0 = (step0 + cs) * SB + sg * ST;
             const int m0 = mb0 + mg * MT;
             if (k < K) {
+                float2 *o = out + (s0 * M + m0) * (long long)K + k;
+                if (s0 + ST <= nsym && m0 + MT <= M) {  // whole tile in range: no per-store branches
 #pragma unroll
-                for (int jj = 0; jj < ST; ++jj) {
-                    if (s0 + jj >= nsym) break;
-                    float2 *o = out + ((s0 + jj) * M) * (long long)K + k;
+                    for (int jj = 0; jj < ST; ++jj)
 #pragma unroll
-                    for (int i = 0; i < MT; ++i)
-                        if (m0 + i < M) o[(long long)(m0 + i) * K] = acc[i][jj];
+                        for (int i = 0; i < MT; ++i) o[(long long)(jj * M + i) * K] = acc[i][jj];
+                } else {
+#pragma unroll
+                    for (int jj = 0; jj < ST; ++jj) {
+                        if (s0 + jj >= nsym) break;
+#pragma unroll
+                        for (int i = 0; i < MT; ++i)
+                            if (m0 + i < M) o[(long long)(jj * M + i) * K] = acc[i][jj];
+                    }
                 }
             }
 #pragma unroll
@@ -408,7 +448,11 @@ k_zf_gemm_lds(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__r
 #pragma unroll
                 for (int jj = 0; jj < ST; ++jj) acc[i][jj] = float2{0.f, 0.f};
         }
-        if (more) put((c + 1) & 1);  // that buffer was last read in chunk c - 1
+        if (!more) break;
+        buf ^= 1;
+        put(buf);  // that buffer was last read in the previous chunk
+        cs = ncs;
+        cn = ncn;
         __syncthreads();
     }
 }

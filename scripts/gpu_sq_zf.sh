@@ -1,0 +1,15 @@
+#!/usr/bin/env bash
+# SQ counters of the zero-forcing kernels (two passes) over scripts/zf_ab.py.
+set -o pipefail
+cd ${GRAFT_REPO_ROOT:-$(pwd)}
+export TMPDIR=/tmp
+OUT=gpurun_out/sqzf_${1:-x}; mkdir -p $OUT
+i=0
+for P in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" \
+         "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_ACTIVE_INST_VMEM SQ_INSTS_VMEM_WR"; do
+  i=$((i+1))
+  timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d $OUT/p$i -o run -- \
+    python3 scripts/zf_ab.py --U 16 --nsym 4000 --reps 1 > $OUT/p$i.jsonl 2> $OUT/p$i.err
+  rc=$?; echo "pass $i rc=$rc"; [ $rc -eq 0 ] || exit $rc
+done
+python3 scripts/sq_table.py $OUT k_zf_

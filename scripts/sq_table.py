@@ -1,5 +1,5 @@
 """Per-kernel-variant table of the SQ counters collected by scripts/gpu_sq_ab.sh.
-usage: python scripts/sq_table.py gpurun_out/sqab_<tag>
+usage: python scripts/sq_table.py gpurun_out/sqab_<tag> [kernel-name filter, default k_mrc_td]
 WAVE/WAIT/ACTIVE counters are quad-cycles (MI355X_MICROARCH.md); ratios are
 per wave lifetime (SQ_WAVE_CYCLES)."""
 import csv
@@ -9,12 +9,13 @@ import sys
 from collections import defaultdict
 
 d = sys.argv[1]
+flt = sys.argv[2] if len(sys.argv) > 2 else "k_mrc_td"
 val = defaultdict(lambda: defaultdict(list))
 for f in glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), recursive=True):
     with open(f) as fp:
         for row in csv.DictReader(fp):
             k = row["Kernel_Name"]
-            if "k_mrc_td" not in k:
+            if flt not in k:
                 continue
             k = k.split("(")[0].replace("void ", "").split("::")[-1]
             val[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
