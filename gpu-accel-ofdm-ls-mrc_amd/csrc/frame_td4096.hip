@@ -93,14 +93,16 @@ __device__ __forceinline__ void row_fft4096(const float2 *__restrict__ src, int 
 }
 
 // ---------------------------------------------------------------------------
-// LS: one workgroup (2 wave pairs) per frame; pair j takes antenna rows j,
-// j+2, ...  Pilots in LDS; partial |H|^2 per pair combined in pair order.
+// LS: one workgroup (4 wave pairs) per frame; pair j takes antenna rows j,
+// j+4, ...  Pilots in LDS; partial |H|^2 per pair combined in pair order.
+// 132 KiB of LDS, one workgroup per CU; round 1's 2-pair workgroups (98 KiB,
+// also one per CU, so one wave per SIMD) took 29-41 % longer (0.318 vs
+// 0.247 ms for 400 frames x 32 antennas; 0.134 vs 0.095 ms for 50).
 // ---------------------------------------------------------------------------
-constexpr int LS_WAVES = 4;
-constexpr int LS_PAIRS = LS_WAVES / 2;
-constexpr size_t LS_LDS = lds_bytes(LS_WAVES) + (size_t)C * sizeof(float2);
+constexpr int LS_WAVES = 8;
+constexpr size_t ls_lds(int nw) { return lds_bytes(nw) + (size_t)C * sizeof(float2); }
 
-template <int E>
+template <int E, int LS_PAIRS>
 __device__ __forceinline__ void ls_rows(const float2 *pilot, int Cp, int R, int j, int t, float2 *T,
                                         const float2 *lds, const float2 *xs, float2 *Hf, float *pp) {
     const int b0 = lane_bin0(t);
@@ -133,14 +135,16 @@ __device__ __forceinline__ void ls_rows(const float2 *pilot, int Cp, int R, int 
     }
 }
 
-__global__ void __launch_bounds__(256) k_ls_td4096(const float2 *__restrict__ iq, int S, int R,
-                                                   int prefix, const float2 *__restrict__ X,
-                                                   float2 *__restrict__ Hc, float *__restrict__ P,
-                                                   int partial) {
+template <int NW = LS_WAVES>
+__global__ void __launch_bounds__(64 * NW) k_ls_td4096(const float2 *__restrict__ iq, int S, int R,
+                                                       int prefix, const float2 *__restrict__ X,
+                                                       float2 *__restrict__ Hc, float *__restrict__ P,
+                                                       int partial) {
+    constexpr int LS_PAIRS = NW / 2;
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     const int w = threadIdx.x >> 6, t = threadIdx.x & 63;
     float2 *T = lds + TAB + w * hl::TS;
-    float2 *xs = lds + TAB + LS_WAVES * hl::TS;  // xs[b] = X[b - 1], xs[0] unused
+    float2 *xs = lds + TAB + NW * hl::TS;  // xs[b] = X[b - 1], xs[0] unused
     fill_tables(lds);
     for (int b = threadIdx.x; b < C; b += blockDim.x) xs[b] = b ? X[b - 1] : float2{1.f, 0.f};
     __syncthreads();
@@ -151,9 +155,9 @@ __global__ void __launch_bounds__(256) k_ls_td4096(const float2 *__restrict__ iq
     float2 *Hf = Hc + f * (long long)R * C;
     float *pp = reinterpret_cast<float *>(lds + TAB);  // [LS_PAIRS][C], reuses T
     if (w & 1)
-        ls_rows<1>(pilot, Cp, R, w >> 1, t, T, lds, xs, Hf, pp);
+        ls_rows<1, LS_PAIRS>(pilot, Cp, R, w >> 1, t, T, lds, xs, Hf, pp);
     else
-        ls_rows<0>(pilot, Cp, R, w >> 1, t, T, lds, xs, Hf, pp);
+        ls_rows<0, LS_PAIRS>(pilot, Cp, R, w >> 1, t, T, lds, xs, Hf, pp);
     __syncthreads();
     float *Pf = P + f * C;
     for (int b = threadIdx.x; b < C; b += blockDim.x) {
@@ -486,7 +490,10 @@ hipError_t launch_ls_td4096(const float2 *iq, long long nframes, int S, int R, i
     using namespace td4096;
     if (nframes <= 0) return hipSuccess;
     if (nframes > 0x7fffffffll) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_ls_td4096, dim3((unsigned)nframes), dim3(64 * LS_WAVES), LS_LDS, s, iq, S, R,
+    auto kern = k_ls_td4096<LS_WAVES>;
+    if (hipError_t e = opt_in_lds(reinterpret_cast<const void *>(kern), (int)ls_lds(LS_WAVES)); e != hipSuccess)
+        return e;  // > 64 KiB of dynamic LDS
+    hipLaunchKernelGGL(kern, dim3((unsigned)nframes), dim3(64 * LS_WAVES), ls_lds(LS_WAVES), s, iq, S, R,
                        prefix, X, Hc, P, partial);
     return hipGetLastError();
 }

@@ -28,6 +28,7 @@ ap.add_argument("--S", type=int, default=101)
 ap.add_argument("--frames", type=int, default=400)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--partial", action="store_true", help="time frame_mrc_partial (numerators)")
+ap.add_argument("--ls", action="store_true", help="time frame_estimate (the LS kernel) instead of the MRC")
 ap.add_argument("variants", nargs="*", default=["default"])
 a = ap.parse_args()
 
@@ -55,6 +56,9 @@ keys = {kv.split("=")[0] for v in a.variants if v != "default" for kv in v.split
 
 
 def run():
+    if a.ls:
+        ofdm.frame_estimate(iq, X, 0, ws)
+        return
     if a.partial:
         ofdm.frame_mrc_partial(iq, ws, 0, num=out)
     else:
@@ -81,6 +85,8 @@ for rep in range(a.reps):
         torch.cuda.synchronize()
         res[v].append(e0.elapsed_time(e1) / 5)
         if rep == 0 and "DBG" not in v:
+            if a.ls:  # check the variant's estimate end to end
+                ofdm.frame_combine(iq, 0, ws, out)
             errs = None if a.partial else int(ofdm.count_symbol_errors(out, S, seed=1).item())
             if ref is None:
                 ref = out.clone()
@@ -88,7 +94,7 @@ for rep in range(a.reps):
             else:
                 d = (out - ref).abs().max().item()
             chk[v] = (errs, d)
-b_sym = R * C * 8 + K * 8
+b_sym = (R * C * 8 * 2 / (S - 1)) if a.ls else (R * C * 8 + K * 8)  # LS: pilot rows in + Hc out
 for v in a.variants:
     ms = sorted(res[v])[len(res[v]) // 2]
     tbs = Q * b_sym / (ms * 1e-3) / 1e12
