@@ -44,8 +44,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--mode", choices=["frames", "split", "pcie"], default="frames",
-                    help="frames: frame-sharded receiver (configs[3], the headline); split: "
+    ap.add_argument("--mode", choices=["frames", "freq", "split", "pcie"], default="frames",
+                    help="frames: frame-sharded receiver (configs[3], the headline); freq: the "
+                         "same frames in the frequency domain (FFT upstream: LS + MRC alone, "
+                         "SURVEY.md 8(d) mode A); split: "
                          "antenna-split partial MRC + RCCL (configs[4]), --R antennas per GPU; "
                          "pcie: host-resident frames through ofdm_pipeline (H2D + receiver + "
                          "D2H overlapped; PCIe-inclusive rate, never the headline)")
@@ -74,7 +76,9 @@ def parse():
 
 
 def cpu_baseline(args, X, ofdm, torch, dev):
-    """Oracle (C restatement of cpuLS.hpp) on the host cores of this box."""
+    """Oracle (C restatement of cpuLS.hpp) on the host cores of this box
+    (--mode freq: its LS + MRC on frequency-domain frames, no FFT)."""
+    freq = args.mode == "freq"
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle_bindings import Oracle
     o = Oracle()
@@ -87,21 +91,30 @@ def cpu_baseline(args, X, ofdm, torch, dev):
 
     def sample(nf):
         iq = ofdm.synth_frames(nf, args.S, args.R, args.C, X, prefix=args.prefix,
-                               seed=args.seed + 7, noise_std=args.noise)
+                               seed=args.seed + 7, noise_std=args.noise, freq_domain=freq)
         torch.cuda.synchronize()
         return iq.cpu().numpy()
 
+    def run(iq):
+        if freq:
+            o.frames_demod_freq(iq, Xh, nthreads=threads)
+        else:
+            o.frames_demod(iq, Xh, args.prefix, nthreads=threads)
+
     iq1 = sample(threads)
     t0 = time.perf_counter()
-    o.frames_demod(iq1, Xh, args.prefix, nthreads=threads)
+    run(iq1)
     t1 = time.perf_counter() - t0
     nf = max(threads, int(args.cpu_seconds / max(t1, 1e-3) * threads) // threads * threads)
-    nf = min(nf, 64 * threads)
+    frame_bytes = args.S * args.R * (args.C + (0 if freq else args.prefix)) * 8
+    nf = min(nf, 64 * threads, max(threads, int(16e9 // frame_bytes) // threads * threads))  # <= 16 GB host
     iq = sample(nf) if nf != threads else iq1
-    t0 = time.perf_counter()
-    o.frames_demod(iq, Xh, args.prefix, nthreads=threads)
+    passes, t0 = 0, time.perf_counter()
+    while passes < 1 or time.perf_counter() - t0 < min(3.0, args.cpu_seconds):  # >= 3 s of host work
+        run(iq)
+        passes += 1
     dt = time.perf_counter() - t0
-    syms = nf * (args.S - 1)
+    syms = passes * nf * (args.S - 1)
     # BASELINE configs[0] / SURVEY.md 8(d)(a): the cpuLS.hpp shape (R=4, C=1024,
     # one frame of 100 symbols = 1 pilot + 99 data) on ONE host thread
     c1 = ofdm.synth_frames(1, 100, 4, 1024, X, prefix=0, seed=args.seed + 11, noise_std=args.noise)
@@ -113,8 +126,9 @@ def cpu_baseline(args, X, ofdm, torch, dev):
         reps += 1
     d1 = time.perf_counter() - t0
     return {"value": syms / dt, "unit": "symbols/s", "cores": threads, "kind": "port",
-            "sample": f"{nf} frames x {args.S} symbols (R={args.R}, C={args.C}, prefix="
-                      f"{args.prefix}), FFT+LS+MRC+rotate, OpenMP over frames, "
+            "sample": f"{passes} x {nf} frames x {args.S} symbols (R={args.R}, C={args.C}, prefix="
+                      f"{args.prefix}), {'LS+MRC+rotate (frequency domain)' if freq else 'FFT+LS+MRC+rotate'}, "
+                      f"OpenMP over frames, "
                       f"{dt:.1f} s wall", "seconds": dt,
             "configs0_single_thread": {"value": reps * 99 / d1, "unit": "symbols/s", "cores": 1,
                                        "sample": f"R=4, C=1024, 1 frame x 100 symbols, {reps} repetitions, "
@@ -132,7 +146,9 @@ def pmc_traffic(path, cfg):
                 d = json.load(fp)
         except (OSError, ValueError):
             continue
-        if all(d.get("config", {}).get(k) == cfg[k] for k in ("R", "C", "S", "frames_per_gpu", "prefix")):
+        dc = d.get("config", {})
+        if all(dc.get(k) == cfg[k] for k in ("R", "C", "S", "frames_per_gpu", "prefix")) and \
+                dc.get("domain", "time") == cfg["domain"]:
             return d.get("mrc_hbm_bytes_per_launch"), os.path.relpath(p, ROOT)
     return None, None
 
@@ -186,9 +202,12 @@ def main():
     if args.mode == "pcie":
         return bench_pcie(args, X, dev, world, rank, barrier)
 
+    freq = args.mode == "freq"
+    if freq:
+        prefix = args.prefix = 0
     t = time.perf_counter()
     iq = ofdm.synth_frames(F, S, R, C, X, prefix=prefix, seed=args.seed, frame0=rank * F,
-                           noise_std=args.noise)
+                           noise_std=args.noise, freq_domain=freq)
     ws = ofdm.workspace(F, S, R, C, dev)
     out = ofdm.c64((F, S - 1, K), dev)
     torch.cuda.synchronize()
@@ -199,10 +218,16 @@ def main():
     def step(evs=None):
         if evs:
             evs[0].record(stream)
-        ofdm.frame_estimate(iq, X, prefix, ws, stream)
+        if freq:
+            ofdm.frame_estimate_freq(iq, X, ws, stream)
+        else:
+            ofdm.frame_estimate(iq, X, prefix, ws, stream)
         if evs:
             evs[1].record(stream)
-        ofdm.frame_combine(iq, prefix, ws, out, stream)
+        if freq:
+            ofdm.frame_combine_freq(iq, ws, out, stream)
+        else:
+            ofdm.frame_combine(iq, prefix, ws, out, stream)
         if evs:
             evs[2].record(stream)
 
@@ -233,14 +258,18 @@ def main():
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         elapsed, errs = float(mx[0]), int(tot[1])
 
-    cfg = {"workload": f"OFDM uplink LS+MRC, time-domain IQ in HBM, {F} frames x {S} symbols "
+    dom = "frequency-domain symbols (FFT upstream)" if freq else "time-domain IQ"
+    cfg = {"workload": f"OFDM uplink LS+MRC, {dom} in HBM, {F} frames x {S} symbols "
                        f"(1 pilot + {S - 1} data) x {R} antennas x {C} subcarriers per GPU",
+           "domain": "freq" if freq else "time",
            "R": R, "C": C, "S": S, "prefix": prefix, "frames_per_gpu": F,
            "data_symbols_per_gpu": Q, "global_data_symbols": Q * world,
            "parallelism": f"frame-sharded x{world}, no collective"}
     b_sym = R * C * 8 + K * 8
     kern = {1024: "k_mrc_td1024_hlds", 2048: "k_mrc_td2048", 4096: "k_mrc_td4096h"}.get(C)
     mrc_name = f"{kern} (FFT+MRC+normalise+rotate)" if kern else "k_fft_rows + k_mrc_freq (staged)"
+    if freq:
+        mrc_name = "k_mrc_freq_frames (MRC+normalise+rotate)" if C >= 512 else "k_mrc_freq (MRC+normalise+rotate)"
     achieved = Q * b_sym / (mrc_ms * 1e-3) / 1e9
     traffic, tsrc = pmc_traffic(args.pmc, cfg)
     step_bytes = F * S * R * C * 8 + Q * K * 8

@@ -353,7 +353,11 @@ int ofdm_frame_combine(const ofdm_cf32 *d_iq, long long nframes, int S, int R, i
     int rc = check_frame_args(d_iq, nframes, S, R, C, prefix, d_out, "ofdm_frame_combine");
     if (rc) return rc;
     if (nframes == 0) return OFDM_OK;
-    if ((rc = ws_check(d_ws, nframes, S, R, C, true, "ofdm_frame_combine"))) return rc;
+    WsTag tag;
+    if ((rc = ws_check(d_ws, nframes, S, R, C, true, "ofdm_frame_combine", &tag))) return rc;
+    if (tag.lane_order != fused_c(C))
+        return fail(OFDM_E_ARG, "ofdm_frame_combine: the workspace holds a frequency-domain estimate "
+                                "(use ofdm_frame_combine_freq)");
     Workspace w;
     if ((rc = carve(d_ws, ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
     hipStream_t s = hs(stream);
@@ -387,26 +391,47 @@ int ofdm_frame_demod(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int
     return td_staged(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w, F2(d_out), 0, s);
 }
 
+int ofdm_frame_estimate_freq(const ofdm_cf32 *d_Y, long long nframes, int S, int R, int C,
+                             const ofdm_cf32 *d_X, void *d_ws, size_t ws_bytes_, ofdm_stream_t stream) {
+    int rc = check_frame_args(d_Y, nframes, S, R, C, 0, d_ws, "ofdm_frame_estimate_freq");
+    if (rc) return rc;
+    if (!d_X) return fail(OFDM_E_ARG, "ofdm_frame_estimate_freq: null pilots");
+    if (nframes == 0) return OFDM_OK;
+    Workspace w;
+    if ((rc = carve(d_ws, ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
+    rc = hip_check(ofdm::launch_ls_freq(F2(d_Y), (long long)S * R * C, nframes, R, C, F2(d_X), w.Hc,
+                                        (long long)R * C, C, 1, w.P, C, 1, hs(stream)),
+                   "ls_freq");
+    if (rc == OFDM_OK) ws_record(d_ws, nframes, S, R, C, false, false);
+    return rc;
+}
+
+int ofdm_frame_combine_freq(const ofdm_cf32 *d_Y, long long nframes, int S, int R, int C, void *d_ws,
+                            size_t ws_bytes_, ofdm_cf32 *d_out, ofdm_stream_t stream) {
+    int rc = check_frame_args(d_Y, nframes, S, R, C, 0, d_out, "ofdm_frame_combine_freq");
+    if (rc) return rc;
+    if (nframes == 0) return OFDM_OK;
+    WsTag tag;
+    if ((rc = ws_check(d_ws, nframes, S, R, C, true, "ofdm_frame_combine_freq", &tag))) return rc;
+    if (tag.lane_order)
+        return fail(OFDM_E_ARG, "ofdm_frame_combine_freq: the workspace holds a time-domain estimate in the "
+                                "fused kernels' lane order (use ofdm_frame_combine)");
+    Workspace w;
+    if ((rc = carve(d_ws, ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
+    const long long fst = (long long)S * R * C;
+    return hip_check(ofdm::launch_mrc_freq(F2(d_Y) + (long long)R * C, fst, (long long)R * C, nframes,
+                                           S - 1, R, C, w.Hc, (long long)R * C, C, 0, w.P, C, 1,
+                                           F2(d_out), 0, hs(stream)),
+                     "mrc_freq");
+}
+
 int ofdm_frame_demod_freq(const ofdm_cf32 *d_Y, long long nframes, int S, int R, int C,
                           const ofdm_cf32 *d_X, void *d_ws, size_t ws_bytes_, ofdm_cf32 *d_out,
                           ofdm_stream_t stream) {
     int rc = check_frame_args(d_Y, nframes, S, R, C, 0, d_out, "ofdm_frame_demod_freq");
     if (rc) return rc;
-    if (!d_X) return fail(OFDM_E_ARG, "ofdm_frame_demod_freq: null pilots");
-    if (nframes == 0) return OFDM_OK;
-    Workspace w;
-    if ((rc = carve(d_ws, ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
-    hipStream_t s = hs(stream);
-    const long long fst = (long long)S * R * C;
-    ws_record(d_ws, nframes, S, R, C, false, false);
-    rc = hip_check(ofdm::launch_ls_freq(F2(d_Y), fst, nframes, R, C, F2(d_X), w.Hc, (long long)R * C, C,
-                                        1, w.P, C, 1, s),
-                   "ls_freq");
-    if (rc) return rc;
-    return hip_check(ofdm::launch_mrc_freq(F2(d_Y) + (long long)R * C, fst, (long long)R * C, nframes,
-                                           S - 1, R, C, w.Hc, (long long)R * C, C, 0, w.P, C, 1,
-                                           F2(d_out), 0, s),
-                     "mrc_freq");
+    if ((rc = ofdm_frame_estimate_freq(d_Y, nframes, S, R, C, d_X, d_ws, ws_bytes_, stream))) return rc;
+    return ofdm_frame_combine_freq(d_Y, nframes, S, R, C, d_ws, ws_bytes_, d_out, stream);
 }
 
 int ofdm_frame_demod_freq_mfma(const ofdm_cf32 *d_Y, long long nframes, int S, int R, int C,

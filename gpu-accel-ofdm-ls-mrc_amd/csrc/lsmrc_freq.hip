@@ -115,12 +115,133 @@ __global__ void __launch_bounds__(256) k_mrc_freq(const float2 *__restrict__ Y, 
     }
 }
 
+// Bin-layout MRC over whole frames (ofdm_frame_demod_freq, the staged path):
+// one lane = two adjacent bins of G consecutive data symbols of ONE frame,
+// so each Hc float4 read from L2 serves G symbols, and the antenna loop is
+// unrolled by U with all U (G + 1) 16-byte loads of a step issued before
+// its MACs (U (G + 1) x 1 KiB in flight per wave).  Blocks are numbered
+// (frame, symbol group, bin chunk), bin chunk fastest, and mapped so that a
+// frame's blocks run on one XCD (its Hc rows stay in one L2).  Tail groups
+// repeat the frame's last symbol without storing it.
+typedef float f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 nt_load4(const float4 *p) {
+    return __builtin_bit_cast(float4, __builtin_nontemporal_load(reinterpret_cast<const f4v *>(p)));
+}
+
+template <int G, int U, bool NT = true>
+__global__ void __launch_bounds__(256) k_mrc_freq_frames(const float2 *__restrict__ Y, long long frame_stride,
+                                                         long long sym_stride, int nsym, int R, int C,
+                                                         const float2 *__restrict__ Hc, long long hc_fstride,
+                                                         const float *__restrict__ P, long long p_fstride,
+                                                         int p_jofs, float2 *__restrict__ out, int mode,
+                                                         long long nblocks, long long per_xcd, int bps) {
+    const long long pb = blockIdx.x;
+    const long long lb = (pb & 7) * per_xcd + (pb >> 3);
+    if (lb >= nblocks) return;
+    const int K = C - 1;
+    const int gpf = (nsym + G - 1) / G;
+    const long long rest = lb / bps;
+    const int m = (int)(lb - rest * bps) * blockDim.x + threadIdx.x;
+    if (m >= C / 2) return;
+    const long long f = rest / gpf;
+    const int s0 = (int)(rest - f * gpf) * G;
+    const float4 *Yq[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const int sd = s0 + g < nsym ? s0 + g : nsym - 1;
+        Yq[g] = reinterpret_cast<const float4 *>(Y + f * frame_stride + sd * sym_stride + 2 * m);
+    }
+    const float4 *Hq = reinterpret_cast<const float4 *>(Hc + f * hc_fstride + 2 * m);
+    const int ld4 = C / 2;  // row pitch in float4
+    float2 a0[G], a1[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) a0[g] = a1[g] = float2{0.f, 0.f};
+    auto mac = [&](const float4 &h, const float4 (&y)[G]) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            // matrixMultThenSum (cpuLS.hpp:203-204), antennas in order
+            a0[g].x = a0[g].x + (y[g].x * h.x - y[g].y * h.y);
+            a0[g].y = a0[g].y + (y[g].x * h.y + y[g].y * h.x);
+            a1[g].x = a1[g].x + (y[g].z * h.z - y[g].w * h.w);
+            a1[g].y = a1[g].y + (y[g].z * h.w + y[g].w * h.z);
+        }
+    };
+    int r = 0;
+    for (; r + U <= R; r += U) {
+        float4 h[U], y[U][G];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            h[u] = Hq[(long long)(r + u) * ld4];
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+                y[u][g] = NT ? nt_load4(Yq[g] + (long long)(r + u) * ld4) : Yq[g][(long long)(r + u) * ld4];
+        }
+        __builtin_amdgcn_sched_barrier(0);  // all U (G + 1) loads in flight before the first MAC
+#pragma unroll
+        for (int u = 0; u < U; ++u) mac(h[u], y[u]);
+    }
+    for (; r < R; ++r) {
+        float4 y[G];
+        const float4 h = Hq[(long long)r * ld4];
+#pragma unroll
+        for (int g = 0; g < G; ++g) y[g] = nt_load4(Yq[g] + (long long)r * ld4);
+        mac(h, y);
+    }
+    const int j0 = 2 * m - 1, j1 = 2 * m;  // subcarriers of bins 2m, 2m+1
+    const float *Pf = P + f * p_fstride + p_jofs;
+    const float p0 = m > 0 ? Pf[j0] : 1.f, p1 = Pf[j1];
+    const int o0 = mode == 0 ? out_pos(j0 < 0 ? 0 : j0, K) : j0, o1 = mode == 0 ? out_pos(j1, K) : j1;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        if (s0 + g >= nsym) break;
+        float2 *o = out + (f * nsym + s0 + g) * (long long)K;
+        float2 v0 = a0[g], v1 = a1[g];
+        if (mode == 0) {
+            v0 = float2{v0.x / p0, v0.y / p0};
+            v1 = float2{v1.x / p1, v1.y / p1};
+        }
+        if (m > 0)
+            __builtin_nontemporal_store(__builtin_bit_cast(unsigned long long, v0),
+                                        reinterpret_cast<unsigned long long *>(o + o0));
+        __builtin_nontemporal_store(__builtin_bit_cast(unsigned long long, v1),
+                                    reinterpret_cast<unsigned long long *>(o + o1));
+    }
+}
+
 hipError_t launch_mrc_freq(const float2 *Y, long long frame_stride, long long sym_stride,
                            long long nframes, int nsym, int R, int C, const float2 *Hc,
                            long long hc_fstride, int hc_ld, int hc_jofs, const float *P,
                            long long p_fstride, int p_jofs, float2 *out, int mode, hipStream_t s) {
     const long long nq = nframes * nsym;
     if (nq <= 0) return hipSuccess;
+    if (ab_knob("MRCF_V", 1) == 1 && C >= 512 && hc_jofs == 0 && hc_ld == C && (hc_fstride % 2) == 0 &&
+        (sym_stride % 2) == 0 &&
+        (frame_stride % 2) == 0 && ((uintptr_t)Hc % 16) == 0 && ((uintptr_t)Y % 16) == 0) {
+        const int bps = C / 2 / 256;
+        // same-process A/B (profiles/r2_ab/abf_*): 8 symbols per lane at C <= 2048
+        // (2 waves/SIMD, 32 KiB in flight per wave), 4 at C = 4096
+        auto kern = C >= 4096 ? k_mrc_freq_frames<4, 4> : k_mrc_freq_frames<8, 4>;
+        int g = C >= 4096 ? 4 : 8;
+#ifdef OFDM_AB_KNOBS
+        switch (ab_knob("MRCF_GU", 0)) {
+            case 24: kern = k_mrc_freq_frames<2, 4>; g = 2; break;
+            case 28: kern = k_mrc_freq_frames<2, 8>; g = 2; break;
+            case 42: kern = k_mrc_freq_frames<4, 2>; g = 4; break;
+            case 48: kern = k_mrc_freq_frames<4, 8>; g = 4; break;
+            case 82: kern = k_mrc_freq_frames<8, 2>; g = 8; break;
+            case 84: kern = k_mrc_freq_frames<8, 4>; g = 8; break;
+            case 18: kern = k_mrc_freq_frames<1, 8>; g = 1; break;
+            case 44: kern = k_mrc_freq_frames<4, 4>; g = 4; break;
+            case 144: kern = k_mrc_freq_frames<4, 4, false>; g = 4; break;
+            default: break;
+        }
+#endif
+        const long long nbg = nframes * ((nsym + g - 1) / g) * bps, pxg = (nbg + 7) / 8;
+        if (pxg * 8 > 0x7fffffffll) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(kern, dim3((unsigned)(pxg * 8)), dim3(256), 0, s, Y, frame_stride, sym_stride, nsym, R,
+                           C, Hc, hc_fstride, P, p_fstride, p_jofs, out, mode, nbg, pxg, bps);
+        return hipGetLastError();
+    }
     const int threads = C / 2 < 256 ? 64 * ((C / 2 + 63) / 64) : 256;
     const int bps = (C / 2 + threads - 1) / threads;
     const long long blocks = nq * bps;

@@ -49,6 +49,8 @@ _SIGS = {
     "ofdm_frame_estimate": (_I, [_P, _LL, _I, _I, _I, _I, _P, _P, _c.c_size_t, _P]),
     "ofdm_frame_combine": (_I, [_P, _LL, _I, _I, _I, _I, _P, _c.c_size_t, _P, _P]),
     "ofdm_frame_demod_freq": (_I, [_P, _LL, _I, _I, _I, _P, _P, _c.c_size_t, _P, _P]),
+    "ofdm_frame_estimate_freq": (_I, [_P, _LL, _I, _I, _I, _P, _P, _c.c_size_t, _P]),
+    "ofdm_frame_combine_freq": (_I, [_P, _LL, _I, _I, _I, _P, _c.c_size_t, _P, _P]),
     "ofdm_frame_demod_freq_mfma": (_I, [_P, _LL, _I, _I, _I, _P, _P, _c.c_size_t, _P, _P]),
     "ofdm_frame_ls_partial": (_I, [_P, _LL, _I, _I, _I, _I, _P, _P, _c.c_size_t, _P, _P]),
     "ofdm_frame_mrc_partial": (_I, [_P, _LL, _I, _I, _I, _I, _P, _c.c_size_t, _P, _P]),
@@ -275,6 +277,22 @@ def frame_demod_freq(Y, X, ws=None, out=None, stream=None):
         out = c64((F, S - 1, C - 1), Y.device)
     _check(lib().ofdm_frame_demod_freq(_dptr(Y), F, S, R, C, _dptr(X), _dptr(ws), ws.numel(),
                                        _dptr(out), _stream(stream)), "ofdm_frame_demod_freq")
+    return out
+
+
+def frame_estimate_freq(Y, X, ws, stream=None):
+    """LS stage of frame_demod_freq: estimates of every frame into the workspace."""
+    F, S, R, C = Y.shape
+    _check(lib().ofdm_frame_estimate_freq(_dptr(Y), F, S, R, C, _dptr(X), _dptr(ws), ws.numel(),
+                                          _stream(stream)), "ofdm_frame_estimate_freq")
+    return ws
+
+
+def frame_combine_freq(Y, ws, out, stream=None):
+    """MRC stage of frame_demod_freq against the estimates in the workspace."""
+    F, S, R, C = Y.shape
+    _check(lib().ofdm_frame_combine_freq(_dptr(Y), F, S, R, C, _dptr(ws), ws.numel(), _dptr(out),
+                                         _stream(stream)), "ofdm_frame_combine_freq")
     return out
 
 

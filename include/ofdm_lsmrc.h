@@ -173,10 +173,24 @@ int ofdm_frame_export_estimate(const void *d_ws, size_t ws_bytes, long long nfra
                                long long frame, ofdm_cf32 *d_Hconj, float *d_Hsqrd, ofdm_stream_t stream);
 
 /* ofdm_frame_demod on frequency-domain symbols (FFT done upstream, no prefix):
- * d_Y = nframes x S x R x C. */
+ * d_Y = nframes x S x R x C.  The LS + MRC of the reference's GPU path on
+ * its own (findHs + findDistSqrd, gpuLS.cu:158-209; multiplyWithChannelConj +
+ * combineForMRC + shiftOneRow, gpuLS.cu:109-125, 212-259, per frame as in
+ * demodOneFrameCUDA, gpuLS.cu:575-675, after its cuFFT). */
 int ofdm_frame_demod_freq(const ofdm_cf32 *d_Y, long long nframes, int S, int R, int C,
                           const ofdm_cf32 *d_X, void *d_ws, size_t ws_bytes, ofdm_cf32 *d_out,
                           ofdm_stream_t stream);
+
+/* Its two stages (as ofdm_frame_estimate / ofdm_frame_combine): the LS
+ * estimate of every frame's pilot symbol into d_ws, then the MRC of the data
+ * symbols against it.  ofdm_frame_combine_freq refuses a workspace filled by
+ * the time-domain ofdm_frame_estimate for C in {1024, 2048, 4096} (whose
+ * estimate is in the fused kernels' lane order), and ofdm_frame_combine one
+ * filled here, with OFDM_E_ARG. */
+int ofdm_frame_estimate_freq(const ofdm_cf32 *d_Y, long long nframes, int S, int R, int C,
+                             const ofdm_cf32 *d_X, void *d_ws, size_t ws_bytes, ofdm_stream_t stream);
+int ofdm_frame_combine_freq(const ofdm_cf32 *d_Y, long long nframes, int S, int R, int C, void *d_ws,
+                            size_t ws_bytes, ofdm_cf32 *d_out, ofdm_stream_t stream);
 
 /* ofdm_frame_demod_freq with the antenna combine on the matrix cores: per
  * subcarrier the (S-1) x R x R-by-1 product sum_r Y[s][r] Hconj[r] as

@@ -29,6 +29,8 @@ ap.add_argument("--frames", type=int, default=400)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--partial", action="store_true", help="time frame_mrc_partial (numerators)")
 ap.add_argument("--ls", action="store_true", help="time frame_estimate (the LS kernel) instead of the MRC")
+ap.add_argument("--freq", action="store_true",
+                help="frequency-domain frames: time frame_demod_freq (LS + MRC, no FFT)")
 ap.add_argument("variants", nargs="*", default=["default"])
 a = ap.parse_args()
 
@@ -45,10 +47,12 @@ rng = np.random.default_rng(1)
 amp = np.float32(0.70710678)
 X = torch.from_numpy((rng.choice([-amp, amp], K) + 1j * rng.choice([-amp, amp], K))
                      .astype(np.complex64)).to(dev)
-iq = ofdm.synth_frames(F, S, R, C, X, seed=1, noise_std=0.01)
+iq = ofdm.synth_frames(F, S, R, C, X, seed=1, noise_std=0.01, freq_domain=a.freq)
 ws = ofdm.workspace(F, S, R, C, dev)
 out = ofdm.c64((F, S - 1, K), dev)
-if a.partial:
+if a.freq:
+    pass
+elif a.partial:
     P, ws = ofdm.frame_ls_partial(iq, X, 0, ws=ws)
 else:
     ofdm.frame_estimate(iq, X, 0, ws)
@@ -56,6 +60,9 @@ keys = {kv.split("=")[0] for v in a.variants if v != "default" for kv in v.split
 
 
 def run():
+    if a.freq:
+        ofdm.frame_demod_freq(iq, X, ws=ws, out=out)
+        return
     if a.ls:
         ofdm.frame_estimate(iq, X, 0, ws)
         return

@@ -55,6 +55,9 @@ def main():
     with open(os.path.join(src, "bench_trace.json")) as fp:
         bench = json.loads([ln for ln in fp if ln.startswith("{")][-1])
     cfg = bench["config"]
+    global MRC, LS
+    if cfg.get("domain") == "freq":  # bench.py --mode freq
+        MRC, LS = "k_mrc_freq", "k_ls_freq"
 
     rows = []
     for k in sorted(fetch, key=lambda k: -fetch[k]):
@@ -73,7 +76,8 @@ def main():
     q = cfg["data_symbols_per_gpu"]
     b_sym = cfg["R"] * cfg["C"] * 8 + (cfg["C"] - 1) * 8
     alg = q * b_sym
-    out = {"tag": tag, "config": {k: cfg[k] for k in ("R", "C", "S", "prefix", "frames_per_gpu")},
+    out = {"tag": tag, "config": dict({k: cfg[k] for k in ("R", "C", "S", "prefix", "frames_per_gpu")},
+                                      domain=cfg.get("domain", "time")),
            "mrc_kernel": mrc[0][0] if mrc else None,
            "mrc_hbm_bytes_per_launch": mrc[0][4] if mrc else None,
            "mrc_algorithmic_bytes_per_launch": alg,

@@ -136,13 +136,37 @@ def test_frame_demod_synth_vs_oracle(ofdm, oracle, dev, F, S, R, C, prefix):
     parity(out, ref)
 
 
-@pytest.mark.parametrize("F,S,R,C", [(3, 11, 16, 1024), (2, 3, 64, 2048), (2, 4, 8, 256)])
+@pytest.mark.parametrize("F,S,R,C", [(3, 11, 16, 1024), (2, 3, 64, 2048), (2, 4, 8, 256),
+                                     # k_mrc_freq_frames: symbol groups cut by the frame end
+                                     # (S-1 = 1, 9, 13), antenna counts not a multiple of the
+                                     # unroll (1, 5, 7), the smallest (512) and largest C
+                                     (2, 2, 5, 512), (3, 10, 7, 1024), (2, 14, 1, 2048),
+                                     (1, 6, 33, 4096), (2, 101, 16, 1024)])
 def test_frame_demod_freq_synth_vs_oracle(ofdm, oracle, dev, F, S, R, C):
     X = to_dev(qpsk_pilots(C - 1), dev)
     Y = ofdm.synth_frames(F, S, R, C, X, seed=5, noise_std=0.05, freq_domain=True)
     out = host(ofdm.frame_demod_freq(Y, X))
     ref = oracle.frames_demod_freq(host(Y), host(X), nthreads=8)
     parity(out, ref)
+
+
+def test_frame_estimate_combine_freq_stages(ofdm, dev):
+    """estimate_freq + combine_freq == demod_freq; each combine refuses the
+    other domain's estimate (lane order vs bin layout) with OFDM_E_ARG."""
+    F, S, R, C = 2, 9, 8, 1024
+    X = to_dev(qpsk_pilots(C - 1), dev)
+    Y = ofdm.synth_frames(F, S, R, C, X, seed=8, noise_std=0.05, freq_domain=True)
+    ref = host(ofdm.frame_demod_freq(Y, X))
+    ws = ofdm.workspace(F, S, R, C, dev)
+    out = ofdm.c64((F, S - 1, C - 1), dev)
+    ofdm.frame_estimate_freq(Y, X, ws)
+    assert (host(ofdm.frame_combine_freq(Y, ws, out)) == ref).all()
+    with pytest.raises(ofdm.OfdmError):
+        ofdm.frame_combine(Y, 0, ws, out)
+    iq = ofdm.synth_frames(F, S, R, C, X, seed=8, noise_std=0.05)
+    ofdm.frame_estimate(iq, X, 0, ws)
+    with pytest.raises(ofdm.OfdmError):
+        ofdm.frame_combine_freq(Y, ws, out)
 
 
 @pytest.mark.parametrize("F,S,R,C", [(2, 21, 16, 1024), (2, 18, 7, 256), (1, 5, 32, 4096),
