@@ -259,23 +259,30 @@ def test_full_size_properties(ofdm, dev, F, S, R, C):
         parity(host(out[f]), ref)
 
 
-@pytest.mark.parametrize("F,S,R,C", [(1000, 101, 64, 2048),   # BASELINE configs[2] in full: 100k symbols, 106 GB
-                                     (1250, 101, 64, 1024)])  # configs[3] per GPU in full: 125k symbols, 66 GB
-def test_full_size_baseline_batches(ofdm, oracle, dev, F, S, R, C):
+@pytest.mark.parametrize("F,S,R,C,freq", [(1000, 101, 64, 2048, False),  # BASELINE configs[2] in full: 100k symbols, 106 GB
+                                          (1250, 101, 64, 1024, False),  # configs[3] per GPU in full: 125k symbols, 66 GB
+                                          (1000, 101, 64, 2048, True),   # the same two in the frequency domain
+                                          (1250, 101, 64, 1024, True),   # (mode A: LS + MRC alone)
+                                          (100, 101, 16, 1024, True)])   # configs[1]: 10k symbols, LS + MRC
+def test_full_size_baseline_batches(ofdm, oracle, dev, F, S, R, C, freq):
     """The whole BASELINE batch resident in HBM: zero QPSK decision errors,
     exact invariance to a power-of-two IQ scale (applied in place, so the
     batch is held once) and the oracle on the first, middle and last frames."""
     import torch
     X = to_dev(qpsk_pilots(C - 1), dev)
-    iq = ofdm.synth_frames(F, S, R, C, X, seed=13, noise_std=0.01)
+    iq = ofdm.synth_frames(F, S, R, C, X, seed=13, noise_std=0.01, freq_domain=freq)
+    demod = (lambda y: ofdm.frame_demod_freq(y, X)) if freq else (lambda y: ofdm.frame_demod(y, X))
     try:
-        out = ofdm.frame_demod(iq, X)
+        out = demod(iq)
         assert int(ofdm.count_symbol_errors(out, S, seed=13).item()) == 0
         sel = [0, F // 2, F - 1]
-        ref = oracle.frames_demod(host(iq[sel]), host(X), 0, nthreads=8)
+        if freq:
+            ref = oracle.frames_demod_freq(host(iq[sel]), host(X), nthreads=8)
+        else:
+            ref = oracle.frames_demod(host(iq[sel]), host(X), 0, nthreads=8)
         parity(host(out[sel]), ref)
         iq.mul_(4.0)
-        out2 = ofdm.frame_demod(iq, X)
+        out2 = demod(iq)
         torch.cuda.synchronize()
         assert torch.allclose(out2, out, rtol=1e-6, atol=1e-6)
     finally:
