@@ -1,0 +1,126 @@
+// bwprobe3.hip -- diagnostic: does the cache policy of the receiver's output
+// stores change what they cost the read stream?  The skeleton is bwprobe2's
+// mode 6 (k_mrc_td1024's access pattern without compute: one 512 KiB symbol
+// per wave, 8 waves per block, XCD-grouped blocks, 80 KiB LDS, then 1023
+// float2 of output per wave at pitch 1023), with the 16 output stores issued as
+// global_store_dwordx2 carrying each cache-policy combination.
+// Prints read GB/s (the stores are 1.5 % more bytes on top).
+#include <hip/hip_runtime.h>
+#include <cstdio>
+typedef unsigned long long u64;
+
+template <int POL>
+__device__ __forceinline__ void st(float2 *p, float2 v) {
+    const u64 x = __builtin_bit_cast(u64, v);
+    if constexpr (POL == 0) *reinterpret_cast<u64 *>(p) = x;
+    else if constexpr (POL == 1) asm volatile("global_store_dwordx2 %0, %1, off sc0" ::"v"(p), "v"(x) : "memory");
+    else if constexpr (POL == 2) asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(x) : "memory");
+    else if constexpr (POL == 3) asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1" ::"v"(p), "v"(x) : "memory");
+    else if constexpr (POL == 4) asm volatile("global_store_dwordx2 %0, %1, off nt" ::"v"(p), "v"(x) : "memory");
+    else if constexpr (POL == 5) asm volatile("global_store_dwordx2 %0, %1, off nt sc1" ::"v"(p), "v"(x) : "memory");
+    else if constexpr (POL == 6) asm volatile("global_store_dwordx2 %0, %1, off nt sc0 sc1" ::"v"(p), "v"(x) : "memory");
+}
+
+// POL < 0: no stores (read ceiling)
+template <int POL>
+__global__ void __launch_bounds__(512) rd(const u64 *__restrict__ p, long long nsym, float *out) {
+    extern __shared__ float lds[];
+    const int w = threadIdx.x >> 6, t = threadIdx.x & 63;
+    float acc = 0.f;
+    const long long pb = blockIdx.x, per_xcd = gridDim.x / 8;
+    const long long lb = (pb & 7) * per_xcd + (pb >> 3);
+    const long long q = lb * 8 + w;
+    if (q < nsym) {
+        const u64 *s = p + q * 65536;
+        for (int r = 0; r < 64; ++r) {
+#pragma unroll
+            for (int m = 0; m < 16; ++m) {
+                u64 v = __builtin_nontemporal_load(s + r * 1024 + t + 64 * m);
+                acc += __builtin_bit_cast(float, (unsigned)v);
+            }
+        }
+    }
+    if (acc == 1234.5f) lds[threadIdx.x] = acc;
+    if constexpr (POL >= 0) {
+        if (q < nsym) {
+            float2 *o = reinterpret_cast<float2 *>(out) + 16 + q * 1023;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const int j = t + 64 * k;
+                if (j < 1023) st<POL>(o + j, float2{acc, (float)k});
+            }
+        }
+    }
+    if (acc == 1234.5f) out[0] = acc;
+}
+
+template <int POL>
+double run(const u64 *p, long long nsym, float *out) {
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    const int blocks = (int)(nsym / 8);
+    rd<POL><<<blocks, 512, 80768>>>(p, nsym, out);
+    hipEventRecord(a);
+    for (int i = 0; i < 3; ++i) rd<POL><<<blocks, 512, 80768>>>(p, nsym, out);
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, a, b);
+    return nsym * 524288.0 * 3 / (ms * 1e-3) / 1e9;
+}
+
+__global__ void sweep(const u64 *__restrict__ p, long long n, float *out) {  // bwprobe2 mode 2
+    float acc = 0.f;
+    for (long long i = (long long)blockIdx.x * 512 + threadIdx.x; i < n; i += (long long)gridDim.x * 512)
+        acc += __builtin_bit_cast(float, (unsigned)__builtin_nontemporal_load(p + i));
+    if (acc == 1234.5f) out[0] = acc;
+}
+
+__global__ void fill_random(u64 *p, long long n) {
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        u64 z = (u64)i * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        p[i] = z ^ (z >> 31);
+    }
+}
+
+int main(int argc, char **argv) {
+    if (argc > 1) {  // placement test: the same kernels on 4 separately allocated 8 GiB inputs
+        const long long ns = 16384;
+        u64 *ps[4];
+        float *outs[2];
+        for (auto &q : ps)
+            if (hipMalloc(&q, ns * 524288) != hipSuccess) return 1;
+        for (auto &o : outs)
+            if (hipMalloc(&o, (size_t)ns * 8192 + 8192) != hipSuccess) return 1;
+        for (auto q : ps) fill_random<<<4096, 256>>>(q, ns * 65536);
+        if (hipDeviceSynchronize() != hipSuccess) return 1;
+        for (int rep = 0; rep < 2; ++rep)
+            for (int i = 0; i < 4; ++i)
+                printf("input %d (%p): no stores %5.0f | nt -> out0 %5.0f  nt -> out1 %5.0f GB/s\n", i, (void *)ps[i],
+                       run<-1>(ps[i], ns, outs[0]), run<4>(ps[i], ns, outs[0]), run<4>(ps[i], ns, outs[1]));
+        return 0;
+    }
+    const long long nsym = 65536;  // 32 GiB
+    u64 *p;
+    float *out;
+    if (hipMalloc(&p, nsym * 524288) != hipSuccess) return 1;
+    if (hipMalloc(&out, (size_t)nsym * 8192 + 8192) != hipSuccess) return 1;
+    // step 0: random input; 1: the same after a grid-stride sweep of the whole
+    // input (bwprobe2 runs such sweeps first); 2: after hipMemset of the output
+    fill_random<<<4096, 256>>>(p, nsym * 65536);
+    for (int step : {0, 1, 2, 0}) {
+        if (step == 1)
+            for (int b : {512, 1024, 4096}) sweep<<<b, 512>>>(p, nsym * 65536, out);
+        if (step == 2) hipMemset(out, 0, (size_t)nsym * 8192);
+        const int fill = step;
+        if (hipDeviceSynchronize() != hipSuccess) return 1;
+        printf("%s no stores %5.0f | plain %5.0f  sc0 %5.0f  sc1 %5.0f  sc0 sc1 %5.0f  nt %5.0f  nt sc1 %5.0f  "
+               "nt sc0 sc1 %5.0f GB/s\n", fill == 0 ? "as is " : fill == 1 ? "swept " : "outset",
+               run<-1>(p, nsym, out), run<0>(p, nsym, out), run<1>(p, nsym, out), run<2>(p, nsym, out),
+               run<3>(p, nsym, out), run<4>(p, nsym, out), run<5>(p, nsym, out), run<6>(p, nsym, out));
+    }
+    return 0;
+}
