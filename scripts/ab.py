@@ -31,6 +31,9 @@ ap.add_argument("--partial", action="store_true", help="time frame_mrc_partial (
 ap.add_argument("--ls", action="store_true", help="time frame_estimate (the LS kernel) instead of the MRC")
 ap.add_argument("--freq", action="store_true",
                 help="frequency-domain frames: time frame_demod_freq (LS + MRC, no FFT)")
+ap.add_argument("--allocs", type=int, default=1,
+                help="repeat the comparison on N separately allocated copies of the batch (what the "
+                     "output stores cost depends on where the input lives: DESIGN.md 4.3)")
 ap.add_argument("variants", nargs="*", default=["default"])
 a = ap.parse_args()
 
@@ -47,15 +50,21 @@ rng = np.random.default_rng(1)
 amp = np.float32(0.70710678)
 X = torch.from_numpy((rng.choice([-amp, amp], K) + 1j * rng.choice([-amp, amp], K))
                      .astype(np.complex64)).to(dev)
-iq = ofdm.synth_frames(F, S, R, C, X, seed=1, noise_std=0.01, freq_domain=a.freq)
+iqs = [ofdm.synth_frames(F, S, R, C, X, seed=1, noise_std=0.01, freq_domain=a.freq) for _ in range(a.allocs)]
 ws = ofdm.workspace(F, S, R, C, dev)
 out = ofdm.c64((F, S - 1, K), dev)
-if a.freq:
-    pass
-elif a.partial:
-    P, ws = ofdm.frame_ls_partial(iq, X, 0, ws=ws)
-else:
-    ofdm.frame_estimate(iq, X, 0, ws)
+
+
+def estimate():
+    global ws
+    if a.freq:
+        pass
+    elif a.partial:
+        _, ws = ofdm.frame_ls_partial(iq, X, 0, ws=ws)
+    else:
+        ofdm.frame_estimate(iq, X, 0, ws)
+
+
 keys = {kv.split("=")[0] for v in a.variants if v != "default" for kv in v.split(",")}
 
 
@@ -72,41 +81,43 @@ def run():
         ofdm.frame_combine(iq, 0, ws, out)
 
 
-res = {v: [] for v in a.variants}
-chk = {}
-ref = None
-for rep in range(a.reps):
+for ai, iq in enumerate(iqs):
+    estimate()
+    res = {v: [] for v in a.variants}
+    chk = {}
+    ref = None
+    for rep in range(a.reps):
+        for v in a.variants:
+            for k in keys:
+                os.environ.pop("OFDM_AB_" + k, None)
+            if v != "default":
+                for kv in v.split(","):
+                    k, val = kv.split("=")
+                    os.environ["OFDM_AB_" + k] = val
+            run()  # warm
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(5):
+                run()
+            e1.record()
+            torch.cuda.synchronize()
+            res[v].append(e0.elapsed_time(e1) / 5)
+            if rep == 0 and "DBG" not in v:
+                if a.ls:  # check the variant's estimate end to end
+                    ofdm.frame_combine(iq, 0, ws, out)
+                errs = None if a.partial else int(ofdm.count_symbol_errors(out, S, seed=1).item())
+                if ref is None:
+                    ref = out.clone()
+                    d = 0.0
+                else:
+                    d = (out - ref).abs().max().item()
+                chk[v] = (errs, d)
+    b_sym = (R * C * 8 * 2 / (S - 1)) if a.ls else (R * C * 8 + K * 8)  # LS: pilot rows in + Hc out
     for v in a.variants:
-        for k in keys:
-            os.environ.pop("OFDM_AB_" + k, None)
-        if v != "default":
-            for kv in v.split(","):
-                k, val = kv.split("=")
-                os.environ["OFDM_AB_" + k] = val
-        run()  # warm
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(5):
-            run()
-        e1.record()
-        torch.cuda.synchronize()
-        res[v].append(e0.elapsed_time(e1) / 5)
-        if rep == 0 and "DBG" not in v:
-            if a.ls:  # check the variant's estimate end to end
-                ofdm.frame_combine(iq, 0, ws, out)
-            errs = None if a.partial else int(ofdm.count_symbol_errors(out, S, seed=1).item())
-            if ref is None:
-                ref = out.clone()
-                d = 0.0
-            else:
-                d = (out - ref).abs().max().item()
-            chk[v] = (errs, d)
-b_sym = (R * C * 8 * 2 / (S - 1)) if a.ls else (R * C * 8 + K * 8)  # LS: pilot rows in + Hc out
-for v in a.variants:
-    ms = sorted(res[v])[len(res[v]) // 2]
-    tbs = Q * b_sym / (ms * 1e-3) / 1e12
-    e, d = chk.get(v, (None, None))
-    print(json.dumps({"variant": v, "C": C, "R": R, "frames": F, "ms": round(ms, 4),
-                      "all_ms": [round(x, 4) for x in res[v]], "TBps": round(tbs, 3),
-                      "frac_8TBps": round(tbs / 8.0, 4), "qpsk_errors": e, "max_abs_diff_vs_first": d}),
-          flush=True)
+        ms = sorted(res[v])[len(res[v]) // 2]
+        tbs = Q * b_sym / (ms * 1e-3) / 1e12
+        e, d = chk.get(v, (None, None))
+        print(json.dumps({"variant": v, "C": C, "R": R, "frames": F, "ms": round(ms, 4),
+                          "all_ms": [round(x, 4) for x in res[v]], "TBps": round(tbs, 3),
+                          "frac_8TBps": round(tbs / 8.0, 4), "alloc": ai, "qpsk_errors": e, "max_abs_diff_vs_first": d}),
+              flush=True)
