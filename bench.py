@@ -64,6 +64,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target wall time of the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-mode-a", action="store_true",
+                    help="skip the supplementary frequency-domain (mode A) measurement of the default mode")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="PMC traffic summary (profiles/) for roofline.traffic")
     args = ap.parse_args()
@@ -298,6 +300,10 @@ def main():
         "check": {"qpsk_symbol_errors": errs},
         "cpu_baseline": None,
     }
+    if world == 1 and not freq and not args.no_mode_a:
+        del iq
+        torch.cuda.empty_cache()
+        result["mode_a"] = mode_a(args, X, ofdm, torch, dev, stream)
     if rank == 0 and world == 1 and not args.no_cpu:
         result["cpu_baseline"] = cpu_baseline(args, X, ofdm, torch, dev)
         result["speedup_vs_cpu_baseline"] = result["value"] / result["cpu_baseline"]["value"]
@@ -305,6 +311,44 @@ def main():
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def mode_a(args, X, ofdm, torch, dev, stream):
+    """Supplementary, outside the headline: the same frames in the frequency
+    domain (FFT upstream), LS + MRC alone (SURVEY.md 8(d) mode A; DESIGN.md
+    4.3) -- the north-star kernels k_ls_freq + k_mrc_freq_frames on the same
+    shape, HIP events on the launch stream; `python bench.py --mode freq` is
+    the full line."""
+    F, S, R, C = args.frames, args.S, args.R, args.C
+    K, Q = C - 1, args.frames * (args.S - 1)
+    Y = ofdm.synth_frames(F, S, R, C, X, seed=args.seed, noise_std=args.noise, freq_domain=True)
+    ws = ofdm.workspace(F, S, R, C, dev)
+    out = ofdm.c64((F, S - 1, K), dev)
+    steps = max(3, args.steps // 2)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+    for i in range(-1, steps):
+        e = evs[i] if i >= 0 else None
+        if e:
+            e[0].record(stream)
+        ofdm.frame_estimate_freq(Y, X, ws, stream)
+        if e:
+            e[1].record(stream)
+        ofdm.frame_combine_freq(Y, ws, out, stream)
+        if e:
+            e[2].record(stream)
+    torch.cuda.synchronize()
+    errs = int(ofdm.count_symbol_errors(out, S, seed=args.seed).item())
+    step_ms = sum(e[0].elapsed_time(e[2]) for e in evs) / steps
+    mrc_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / steps
+    achieved = Q * (R * C * 8 + K * 8) / (mrc_ms * 1e-3) / 1e9
+    del Y, ws, out
+    torch.cuda.empty_cache()
+    return {"workload": f"the same {F} frames in the frequency domain (FFT upstream): LS + MRC alone",
+            "value": Q / (step_ms * 1e-3), "unit": "symbols/s", "ms_per_step": step_ms, "steps": steps,
+            "roofline": {"kernel": "k_mrc_freq_frames (MRC+normalise+rotate)", "bound": "hbm",
+                         "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBPS, "avg_launch_ms": mrc_ms},
+            "check": {"qpsk_symbol_errors": errs}}
 
 
 def bench_pcie(args, X, dev, world, rank, barrier):
