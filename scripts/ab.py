@@ -34,6 +34,8 @@ ap.add_argument("--freq", action="store_true",
 ap.add_argument("--allocs", type=int, default=1,
                 help="repeat the comparison on N separately allocated copies of the batch (what the "
                      "output stores cost depends on where the input lives: DESIGN.md 4.3)")
+ap.add_argument("--ls-per-variant", action="store_true",
+                help="re-run the LS estimate under each variant's switches (variants that change the Hc layout)")
 ap.add_argument("variants", nargs="*", default=["default"])
 a = ap.parse_args()
 
@@ -94,6 +96,8 @@ for ai, iq in enumerate(iqs):
                 for kv in v.split(","):
                     k, val = kv.split("=")
                     os.environ["OFDM_AB_" + k] = val
+            if a.ls_per_variant:
+                estimate()
             run()  # warm
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
