@@ -99,17 +99,32 @@ int carve(void *d_ws, size_t bytes, long long F, int S, int R, int C, bool need_
 // fused kernel's lane order and whether P is an antenna-split partial.  The
 // consumers (combine, mrc_partial, export) refuse a workspace whose estimate
 // was made for another geometry instead of dividing by the wrong |H|^2.
+// quad4k: the C = 4096 estimate is in the lane order of the wave-quad kernels
+// (frame_td4096r.hip, used when the rows are 16-byte aligned: even prefix),
+// not of the wave-pair ones.
 struct WsTag {
     long long F;
     int S, R, C;
-    bool lane_order, partial;
+    bool lane_order, partial, quad4k;
 };
 std::mutex g_ws_mu;
 std::map<const void *, WsTag> g_ws;
 
-void ws_record(const void *ws, long long F, int S, int R, int C, bool lane_order, bool partial) {
+void ws_record(const void *ws, long long F, int S, int R, int C, bool lane_order, bool partial,
+               bool quad4k = false) {
     std::lock_guard<std::mutex> lock(g_ws_mu);
-    g_ws[ws] = WsTag{F, S, R, C, lane_order, partial};
+    g_ws[ws] = WsTag{F, S, R, C, lane_order, partial, quad4k};
+}
+
+bool quad4k(const void *iq, int C, int prefix) {
+    return C == 4096 && ofdm::td4096r_ok(reinterpret_cast<const float2 *>(iq), prefix);
+}
+int quad4k_check(const WsTag &t, const void *iq, int C, int prefix, const char *fn) {
+    if (t.C == 4096 && t.lane_order && t.quad4k != quad4k(iq, C, prefix))
+        return fail(OFDM_E_ARG, "%s: the C=4096 estimate was made for %s rows (the kernel depends on "
+                                "16-byte row alignment: even prefix), these rows are %s", fn,
+                    t.quad4k ? "aligned" : "unaligned", t.quad4k ? "unaligned" : "aligned");
+    return OFDM_OK;
 }
 
 // need_full: the consumer divides by P, so a partial (antenna-split) P is refused
@@ -344,7 +359,7 @@ int ofdm_frame_estimate(const ofdm_cf32 *d_iq, long long nframes, int S, int R, 
         rc = hip_check(ls_fused(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w.Hc, w.P, 0, s), "ls_fused");
     else
         rc = td_staged(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w, nullptr, 2, s);
-    if (rc == OFDM_OK) ws_record(d_ws, nframes, S, R, C, fused_c(C), false);
+    if (rc == OFDM_OK) ws_record(d_ws, nframes, S, R, C, fused_c(C), false, quad4k(d_iq, C, prefix));
     return rc;
 }
 
@@ -358,6 +373,7 @@ int ofdm_frame_combine(const ofdm_cf32 *d_iq, long long nframes, int S, int R, i
     if (tag.lane_order != fused_c(C))
         return fail(OFDM_E_ARG, "ofdm_frame_combine: the workspace holds a frequency-domain estimate "
                                 "(use ofdm_frame_combine_freq)");
+    if ((rc = quad4k_check(tag, d_iq, C, prefix, "ofdm_frame_combine"))) return rc;
     Workspace w;
     if ((rc = carve(d_ws, ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
     hipStream_t s = hs(stream);
@@ -379,7 +395,7 @@ int ofdm_frame_demod(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int
     Workspace w;
     if ((rc = carve(d_ws, ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
     hipStream_t s = hs(stream);
-    ws_record(d_ws, nframes, S, R, C, fused_c(C), false);
+    ws_record(d_ws, nframes, S, R, C, fused_c(C), false, quad4k(d_iq, C, prefix));
     if (fused_c(C)) {
         rc = hip_check(ls_fused(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w.Hc, w.P, 0, s),
                        "ls_fused");
@@ -472,7 +488,7 @@ int ofdm_frame_ls_partial(const ofdm_cf32 *d_iq, long long nframes, int S, int R
     else
         rc = td_staged(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w, nullptr, 2, s);
     if (rc) return rc;
-    ws_record(d_ws, nframes, S, R, C, fused_c(C), true);
+    ws_record(d_ws, nframes, S, R, C, fused_c(C), true, quad4k(d_iq, C, prefix));
     // bins 1..C-1 of the bin-layout P -> [F][K]
     const int K = C - 1;
     return hip_check(hipMemcpy2DAsync(d_P, K * sizeof(float), w.P + 1, C * sizeof(float),
@@ -486,7 +502,9 @@ int ofdm_frame_mrc_partial(const ofdm_cf32 *d_iq, long long nframes, int S, int 
     int rc = check_frame_args(d_iq, nframes, S, R, C, prefix, d_num, "ofdm_frame_mrc_partial");
     if (rc) return rc;
     if (nframes == 0) return OFDM_OK;
-    if ((rc = ws_check(d_ws, nframes, S, R, C, false, "ofdm_frame_mrc_partial"))) return rc;
+    WsTag tag;
+    if ((rc = ws_check(d_ws, nframes, S, R, C, false, "ofdm_frame_mrc_partial", &tag))) return rc;
+    if ((rc = quad4k_check(tag, d_iq, C, prefix, "ofdm_frame_mrc_partial"))) return rc;
     Workspace w;
     if ((rc = carve(d_ws, ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
     hipStream_t s = hs(stream);
@@ -509,7 +527,7 @@ int ofdm_frame_export_estimate(const void *d_ws, size_t ws_bytes_, long long nfr
     Workspace w;
     if ((rc = carve(const_cast<void *>(d_ws), ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
     return hip_check(ofdm::launch_export_estimate(w.Hc + frame * R * C, w.P + frame * C, R, C, tag.lane_order,
-                                                  F2(d_Hconj), d_Hsqrd, hs(stream)),
+                                                  tag.quad4k, F2(d_Hconj), d_Hsqrd, hs(stream)),
                      "ofdm_frame_export_estimate");
 }
 

@@ -38,6 +38,7 @@ __host__ __device__ __forceinline__ constexpr int rfft_bin(int L, int j) {
 
 // Per-lane constants of the cross-lane stages (computed once per kernel).
 struct Consts {
+    v2f w1024;       // W1024^t (twiddles by recurrence, fft1024<true>)
     v2f w1, w2, w3;  // W64^(t_lo k_hi), k_hi = 1..3
     v2f c1;          // stage 1 (lane bit 3): 1, or -W16^(t_lo & 7)
     v2f c2;          // stage 2 (lane bit 2): g(a) (W8^(t_lo & 3) if bit 2), g of the quad DFT folded in
@@ -47,6 +48,7 @@ struct Consts {
 __device__ __forceinline__ Consts make_consts(int t) {
     Consts c;
     const int tl = t & 15;
+    c.w1024 = pk::V(g_tw[t * (OFDM_TW_N / 1024)]);
     c.w1 = pk::V(g_tw[(tl * 1) * (OFDM_TW_N / 64)]);
     c.w2 = pk::V(g_tw[(tl * 2) * (OFDM_TW_N / 64)]);
     c.w3 = pk::V(g_tw[(tl * 3) * (OFDM_TW_N / 64)]);
@@ -97,14 +99,20 @@ __device__ __forceinline__ void xor4_bfly8(const float *v, float *w) {
 }
 
 // Forward FFT of the row in a[] (a[m] = x[t + 64 m]); on return a[j] = X[rfft_bin(t, j)].
-// tw1: the hlds W1024^(t k2) table in LDS ([k2 - 1][t], k2 = 1..15).
+// tw1: the hlds W1024^(t k2) table in LDS ([k2 - 1][t], k2 = 1..15); TWR:
+// those twiddles by recurrence from c.w1024 instead (no table; tw1 unused).
+template <bool TWR = false>
 __device__ __forceinline__ void fft1024(float2 (&a)[16], int t, const float2 *tw1, const Consts &c) {
     v2f v[16];
 #pragma unroll
     for (int m = 0; m < 16; ++m) v[m] = pk::V(a[m]);
     pk::fft_reg<16>(v);
+    if constexpr (TWR) {
+        td1024::hlds::tw_powers(v, c.w1024, c.w1024);
+    } else {
 #pragma unroll
-    for (int k2 = 1; k2 < 16; ++k2) v[k2] = pk::cmul(v[k2], pk::V(tw1[(k2 - 1) * 64 + t]));
+        for (int k2 = 1; k2 < 16; ++k2) v[k2] = pk::cmul(v[k2], pk::V(tw1[(k2 - 1) * 64 + t]));
+    }
     // 1. t5 -> register bit 3, t4 -> register bit 2
     float re[16], im[16];
 #pragma unroll

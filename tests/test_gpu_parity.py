@@ -345,3 +345,37 @@ def test_concurrent_host_threads_large_lds_kernels(ofdm, dev):
     assert not errs, errs
     for o in outs:
         assert np.array_equal(o, ref)
+
+
+@pytest.mark.parametrize("R,C,prefix", [(8, 1024, 0), (8, 2048, 4), (12, 4096, 0), (5, 4096, 3), (1, 4096, 2)])
+def test_frame_export_estimate_vs_oracle(ofdm, oracle, dev, R, C, prefix):
+    """ofdm_frame_export_estimate (gpuLS's Hconj / Hsqrd view of a frame's
+    estimate) against the oracle's LS on the same pilot rows: every fused
+    kernel's lane order, incl. the C = 4096 wave-quad layout (even prefix)
+    and the wave-pair one (odd prefix)."""
+    F, S = 3, 3
+    X = qpsk_pilots(C - 1, seed=C + R)
+    iq = ofdm.synth_frames(F, S, R, C, to_dev(X, dev), prefix=prefix, seed=77, noise_std=0.02)
+    ws = ofdm.workspace(F, S, R, C, dev)
+    ofdm.frame_estimate(iq, to_dev(X, dev), prefix, ws)
+    a = iq.cpu().numpy()
+    for f in (0, F - 1):
+        Yp = np.fft.fft(a[f, 0, :, prefix:].astype(np.complex128), axis=-1).astype(np.complex64)
+        Hc_ref, P_ref = oracle.ls(Yp, X)
+        H, P = ofdm.frame_export_estimate(ws, F, S, R, C, frame=f)
+        parity(host(H), Hc_ref)
+        parity(host(P), P_ref)
+
+
+def test_combine_refuses_other_c4096_alignment(ofdm, dev):
+    """A C = 4096 estimate made on 16-byte aligned rows (even prefix: the
+    wave-quad kernels) cannot be combined on rows of another alignment."""
+    F, S, R, C = 1, 3, 4, 4096
+    X = to_dev(qpsk_pilots(C - 1), dev)
+    iq0 = ofdm.synth_frames(F, S, R, C, X, prefix=0, seed=3)
+    iq1 = ofdm.synth_frames(F, S, R, C, X, prefix=1, seed=3)
+    ws = ofdm.workspace(F, S, R, C, dev)
+    ofdm.frame_estimate(iq0, X, 0, ws)
+    out = ofdm.c64((F, S - 1, C - 1), dev)
+    with pytest.raises(ofdm.OfdmError):
+        ofdm.frame_combine(iq1, 1, ws, out)
