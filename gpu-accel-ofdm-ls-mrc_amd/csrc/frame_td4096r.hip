@@ -24,9 +24,13 @@
 // lane, issued before the next row's DMA and waited for by an explicit
 // vmcnt so the wait does not drain the DMA).
 //
+// A/B build only (OFDM_AB_KNOBS; switch MRC4K_R=1): correct and tested, but
+// 21 % slower than k_mrc_td4096h (profiles/r2_ab/quad4k_ab.jsonl).
+//
 // Hc layout (LS kernel below; stages.hip hc_pos): per (frame, antenna) four
 // planes c of 512 float4, float4 i*64 + t = (Hc[4 b(t, 2i) + c],
 // Hc[4 b(t, 2i+1) + c]), b(t, j) = rfft_bin(t, j).  P bin-indexed [F][C].
+#ifdef OFDM_AB_KNOBS
 #include "launch.hpp"
 #include "rfft1024.hpp"
 
@@ -425,3 +429,4 @@ hipError_t launch_mrc_td4096r(const float2 *iq, long long nframes, int S, int R,
 }
 
 }  // namespace ofdm
+#endif  // OFDM_AB_KNOBS

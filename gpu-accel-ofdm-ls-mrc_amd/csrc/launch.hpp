@@ -105,9 +105,13 @@ hipError_t launch_ls_td4096(const float2 *iq, long long nframes, int S, int R, i
 hipError_t launch_mrc_td4096(const float2 *iq, long long nframes, int S, int R, int prefix,
                              const float2 *Hc, const float *P, float2 *out, int mode, hipStream_t s);
 // C = 4096 on wave quads with the register-only FFT and row DMA
-// (frame_td4096r.hip); rows must be 16-byte aligned (td4096r_ok), and the
-// estimate is in its own lane order (stages.hip hc_pos)
+// (frame_td4096r.hip, A/B build only); rows must be 16-byte aligned
+// (td4096r_ok), and the estimate is in its own lane order (stages.hip hc_pos)
+#ifdef OFDM_AB_KNOBS
 bool td4096r_ok(const float2 *iq, int prefix);
+#else
+inline bool td4096r_ok(const float2 *, int) { return false; }
+#endif
 hipError_t launch_ls_td4096r(const float2 *iq, long long nframes, int S, int R, int prefix,
                              const float2 *X, float2 *Hc, float *P, int partial, hipStream_t s);
 hipError_t launch_mrc_td4096r(const float2 *iq, long long nframes, int S, int R, int prefix,
