@@ -20,8 +20,10 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # OFDM_LSMRC_LIB=ab selects the A/B build (make ab: lib/libofdm_lsmrc_ab.so,
 # experiment switches read from OFDM_AB_* variables) for scripts/ comparisons;
 # the product library has no switches.
-LIB_PATH = os.path.join(HERE, "lib", "libofdm_lsmrc_ab.so" if os.environ.get("OFDM_LSMRC_LIB") == "ab"
-                        else "libofdm_lsmrc.so")
+# (any other value <v>: lib/libofdm_lsmrc_<v>.so, a build of the same sources with
+# other compiler options, scripts/libab.py).
+_LIBSEL = os.environ.get("OFDM_LSMRC_LIB", "")
+LIB_PATH = os.path.join(HERE, "lib", f"libofdm_lsmrc_{_LIBSEL}.so" if _LIBSEL else "libofdm_lsmrc.so")
 HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "ofdm_lsmrc.h")
 
 _c = ctypes

@@ -17,7 +17,7 @@ import json
 import os
 import sys
 
-os.environ["OFDM_LSMRC_LIB"] = "ab"
+os.environ.setdefault("OFDM_LSMRC_LIB", "ab")  # or another non-product build (scripts/libab.py)
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "gpu-accel-ofdm-ls-mrc_amd"))
 
@@ -43,7 +43,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import ofdm_lsmrc as ofdm  # noqa: E402
 
-assert ofdm.LIB_PATH.endswith("_ab.so"), ofdm.LIB_PATH
+assert not ofdm.LIB_PATH.endswith("libofdm_lsmrc.so") or os.environ["OFDM_LSMRC_LIB"] == "", ofdm.LIB_PATH
 F, S, R, C = a.frames, a.S, a.R, a.C
 K = C - 1
 Q = F * (S - 1)
