@@ -41,7 +41,7 @@ __device__ __forceinline__ void fill_tables(float2 *lds) {
 }
 
 // FFT of one 2048-sample row (src) -> xe[k] = X[2 b], xo[k] = X[2 b + 1]
-template <bool NT, bool LOAD = true>
+template <bool NT, bool LOAD = true, int PK = 0>
 __device__ __forceinline__ void row_fft2048(const float2 *__restrict__ src, int t, float2 *T,
                                             const float2 *lds, float2 (&xe)[16], float2 (&xo)[16]) {
     const float2 *tw1 = lds, *tw2 = lds + hl::TW1S, *twv = lds + hl::TW1S + hl::TW2S;
@@ -62,10 +62,10 @@ __device__ __forceinline__ void row_fft2048(const float2 *__restrict__ src, int 
         u[m] = cadd(u[m], v[m]);
         v[m] = cmul(d, twv[m * 64 + t]);
     }
-    hl::row_fft_a(u, t, T, tw1);
-    hl::row_fft_b(t, T, tw2, xe);
-    hl::row_fft_a(v, t, T, tw1);
-    hl::row_fft_b(t, T, tw2, xo);
+    hl::row_fft_a<PK>(u, t, T, tw1);
+    hl::row_fft_b<PK>(t, T, tw2, xe);
+    hl::row_fft_a<PK>(v, t, T, tw1);
+    hl::row_fft_b<PK>(t, T, tw2, xo);
 }
 
 // ---------------------------------------------------------------------------
@@ -130,7 +130,7 @@ __global__ void __launch_bounds__(256) k_ls_td2048(const float2 *__restrict__ iq
 
 // ---------------------------------------------------------------------------
 // MRC: one wave per data symbol, MRC_WAVES consecutive symbols per workgroup,
-// XCD-grouped block order (as k_mrc_td1024).  ~190 VGPRs -> 2 waves/SIMD.
+// XCD-grouped block order (as k_mrc_td1024).  249 VGPRs (ILP scheduler) -> 2 waves/SIMD.
 // mode 0: out[q][out_pos(j)] = acc / P;  mode 1: out[q][j] = acc (numerator)
 // ---------------------------------------------------------------------------
 constexpr int MRC_WAVES = 4;
@@ -138,7 +138,9 @@ constexpr int MRC_WAVES = 4;
 // DBG (A/B build only): bit 1 no Hc loads, bit 2 no output stores (both
 // wrong results by design), bit 3 the round-1 epilogue (scattered plain stores),
 // bit 6 no IQ loads after the first row (compute only).
-template <int DBG = 0>
+// PK = 2: the second half of each 1024-point FFT (row_fft_b) in packed f32
+// (pk.hpp) -- 1.5-2 % faster under the ILP scheduler.
+template <int DBG = 0, int PK = 2>
 __global__ void __attribute__((amdgpu_flat_work_group_size(256, 256), amdgpu_waves_per_eu(2, 2)))
 k_mrc_td2048(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
              const float *__restrict__ P, float2 *__restrict__ out, long long nq, long long nblocks,
@@ -169,7 +171,7 @@ k_mrc_td2048(const float2 *__restrict__ iq, int S, int R, int prefix, const floa
         if ((DBG & 64) && r > 0)
             row_fft2048<true, false>(sym, t, T, lds, xe, xo);
         else
-            row_fft2048<true>(sym + (long long)r * Cp, t, T, lds, xe, xo);
+            row_fft2048<true, true, PK>(sym + (long long)r * Cp, t, T, lds, xe, xo);
         __builtin_amdgcn_sched_barrier(0);
         const float4 *hr = Hf + (long long)r * (C / 2);
         // matrixMultThenSum (cpuLS.hpp:203-204), antennas in order
@@ -278,6 +280,12 @@ hipError_t launch_mrc_td2048(const float2 *iq, long long nframes, int S, int R, 
         case 6: kern = k_mrc_td2048<6>; break;
         case 8: kern = k_mrc_td2048<8>; break;
         case 64: kern = k_mrc_td2048<64>; break;
+        default: break;
+    }
+    switch (ab_knob("MRC2K_PK", -1)) {  // packed-f32 FFT halves (pk.hpp): 0 none, 1 first, 3 both
+        case 0: kern = k_mrc_td2048<0, 0>; break;
+        case 1: kern = k_mrc_td2048<0, 1>; break;
+        case 3: kern = k_mrc_td2048<0, 3>; break;
         default: break;
     }
 #endif
