@@ -138,9 +138,10 @@ constexpr int MRC_WAVES = 4;
 // DBG (A/B build only): bit 1 no Hc loads, bit 2 no output stores (both
 // wrong results by design), bit 3 the round-1 epilogue (scattered plain stores),
 // bit 6 no IQ loads after the first row (compute only).
-// PK = 2: the second half of each 1024-point FFT (row_fft_b) in packed f32
-// (pk.hpp) -- 1.5-2 % faster under the ILP scheduler.
-template <int DBG = 0, int PK = 2>
+// PK: packed-f32 arithmetic (pk.hpp) -- bit 1 the first half of each
+// 1024-point FFT (row_fft_a), bit 2 the second (row_fft_b), bit 4 the MAC.
+// Default 6: 3-3.5 % faster than none under the ILP scheduler.
+template <int DBG = 0, int PK = 6>
 __global__ void __attribute__((amdgpu_flat_work_group_size(256, 256), amdgpu_waves_per_eu(2, 2)))
 k_mrc_td2048(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
              const float *__restrict__ P, float2 *__restrict__ out, long long nq, long long nblocks,
@@ -178,6 +179,14 @@ k_mrc_td2048(const float2 *__restrict__ iq, int S, int R, int prefix, const floa
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             const float4 h = (DBG & 2) ? float4{1.f, (float)k, (float)r, 1.f} : hr[k * 64 + t];
+            if constexpr ((PK & 4) != 0) {  // packed MAC: (acc + x.re h) + (-x.im) h~, as k_mrc_td4096h
+                pk::v2f a = pk::V(ae[k]), b = pk::V(ao[k]);
+                pk::mac(a, pk::V(xe[k]), (pk::v2f){h.x, h.y});
+                pk::mac(b, pk::V(xo[k]), (pk::v2f){h.z, h.w});
+                ae[k] = pk::F(a);
+                ao[k] = pk::F(b);
+                continue;
+            }
             ae[k].x = ae[k].x + (xe[k].x * h.x - xe[k].y * h.y);
             ae[k].y = ae[k].y + (xe[k].x * h.y + xe[k].y * h.x);
             ao[k].x = ao[k].x + (xo[k].x * h.z - xo[k].y * h.w);
@@ -282,10 +291,12 @@ hipError_t launch_mrc_td2048(const float2 *iq, long long nframes, int S, int R, 
         case 64: kern = k_mrc_td2048<64>; break;
         default: break;
     }
-    switch (ab_knob("MRC2K_PK", -1)) {  // packed-f32 FFT halves (pk.hpp): 0 none, 1 first, 3 both
+    switch (ab_knob("MRC2K_PK", -1)) {  // packed-f32 parts other than the default 6
         case 0: kern = k_mrc_td2048<0, 0>; break;
         case 1: kern = k_mrc_td2048<0, 1>; break;
+        case 2: kern = k_mrc_td2048<0, 2>; break;
         case 3: kern = k_mrc_td2048<0, 3>; break;
+        case 7: kern = k_mrc_td2048<0, 7>; break;
         default: break;
     }
 #endif
