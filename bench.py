@@ -15,9 +15,10 @@ value = data symbols demodulated per second, whole job (all ranks).
 roofline: dominant kernel (MRC), algorithmic bytes per data symbol
   B_sym = R*C*8 (IQ read once) + K*8 (output written once)  
   divided by its HIP-event-measured average launch time, vs 8 TB/s HBM3E.
-cpu_baseline: the oracle's C restatement of cpuLS.hpp (oracle/, FFT in
-  float64) timed on this host, rank 0 at N=1, on a bounded sample of frames of
-  the same shape, OpenMP over frames.
+cpu_baseline: the oracle's C restatement of cpuLS.hpp (oracle/) with its
+  single-precision radix-2 FFT (the reference's fftwf precision; the parity
+  oracle keeps a float64 FFT) timed on this host, rank 0 at N=1, on a bounded
+  sample of frames of the same shape, OpenMP over frames.
 
 python bench.py [--gpus N] [--steps K] [--warmup W]
 torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
@@ -100,8 +101,8 @@ def cpu_baseline(args, X, ofdm, torch, dev):
     def run(iq):
         if freq:
             o.frames_demod_freq(iq, Xh, nthreads=threads)
-        else:
-            o.frames_demod(iq, Xh, args.prefix, nthreads=threads)
+        else:  # single-precision FFT, the precision class of the reference's fftwf
+            o.frames_demod_fft32(iq, Xh, args.prefix, nthreads=threads)
 
     iq1 = sample(threads)
     t0 = time.perf_counter()
@@ -124,17 +125,19 @@ def cpu_baseline(args, X, ofdm, torch, dev):
     c1 = c1.cpu().numpy()
     reps, t0 = 0, time.perf_counter()
     while reps < 5 or time.perf_counter() - t0 < 1.0:
-        o.frames_demod(c1, Xh, 0, nthreads=1)
+        o.frames_demod_fft32(c1, Xh, 0, nthreads=1)
         reps += 1
     d1 = time.perf_counter() - t0
-    return {"value": syms / dt, "unit": "symbols/s", "cores": threads, "kind": "port",
+    fft = "none (frequency-domain input)" if freq else \
+        "float32 scalar radix-2 (oracle_fft_row_f32, twiddle table reused; FFTW's SIMD codelets are not available here)"
+    return {"value": syms / dt, "unit": "symbols/s", "cores": threads, "kind": "port", "fft": fft,
             "sample": f"{passes} x {nf} frames x {args.S} symbols (R={args.R}, C={args.C}, prefix="
                       f"{args.prefix}), {'LS+MRC+rotate (frequency domain)' if freq else 'FFT+LS+MRC+rotate'}, "
-                      f"OpenMP over frames, "
+                      f"FFT: {'none' if freq else 'float32 scalar radix-2'}, OpenMP over frames, "
                       f"{dt:.1f} s wall", "seconds": dt,
-            "configs0_single_thread": {"value": reps * 99 / d1, "unit": "symbols/s", "cores": 1,
+            "configs0_single_thread": {"value": reps * 99 / d1, "unit": "symbols/s", "cores": 1, "fft": fft,
                                        "sample": f"R=4, C=1024, 1 frame x 100 symbols, {reps} repetitions, "
-                                                 f"{d1:.2f} s wall"}}
+                                                 f"FFT float32 scalar radix-2, {d1:.2f} s wall"}}
 
 
 def pmc_traffic(path, cfg):
@@ -458,12 +461,12 @@ def bench_split(args, X, dev, world, rank, barrier):
     torch.cuda.synchronize()
     log(f"[rank {rank}] synthesised {iq.numel() * 8 / 1e9:.1f} GB in {time.perf_counter() - t:.1f} s")
     for _ in range(max(1, args.warmup)):
-        out.zero_()
         pipe.run(iq, X, out)
-    if world > 1:  # every position written by exactly one rank
-        dist.all_reduce(torch.view_as_real(out))
+    # the timed steps write every output position on exactly one rank (its
+    # reduce-scatter slice), so `out` is zeroed first and gathered ONCE after
+    # the timed loop: what is checked below is what the timed steps computed
+    out.zero_()
     torch.cuda.synchronize()
-    errs = int(ofdm.count_symbol_errors(out, S, seed=args.seed).item()) if rank == 0 else 0
 
     barrier()
     torch.cuda.synchronize()
@@ -477,6 +480,12 @@ def bench_split(args, X, dev, world, rank, barrier):
         mx = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         elapsed = float(mx[0])
+        dist.all_reduce(torch.view_as_real(out))  # the gather: each position is non-zero on one rank only
+    torch.cuda.synchronize()
+    errs = int(ofdm.count_symbol_errors(out, S, seed=args.seed).item()) if rank == 0 else 0
+    check = {"qpsk_symbol_errors": errs}
+    if rank == 0:
+        check["vs_full_receiver"] = split_vs_full(ofdm, torch, X, out, F, S, R * world, C, prefix, args)
 
     # roofline of the dominant kernel: the partial FFT+MRC over the whole
     # local batch, HIP events on its stream (outside the timed region)
@@ -521,12 +530,39 @@ def bench_split(args, X, dev, world, rank, barrier):
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
                      "bytes_per_launch": Q * b_sym, "avg_launch_ms": mrc_ms,
                      "median_launch_ms": mrc_median},
-        "check": {"qpsk_symbol_errors": errs},
+        "check": check,
         "cpu_baseline": None,
     }
     if rank == 0:
         print(json.dumps(result), flush=True)
     dist.destroy_process_group()
+
+
+def split_vs_full(ofdm, torch, X, out, F, S, R_total, C, prefix, args):
+    """Frames 0 and F-1 of the gathered antenna-split output against the
+    single-GPU receiver (ofdm.frame_demod, parity-tested against the oracle in
+    tests/) on ALL R_total antennas of the same frames, re-synthesised on this
+    rank: a wrong collective order or slice shows up here as a parity failure,
+    not only as a speed number.  Tolerance: north_star's 1e-5 (the split sums
+    the antennas per rank, then across ranks)."""
+    import numpy as np
+    worst_n, worst_e = 0.0, 0.0
+    for f in sorted({0, F - 1}):
+        full = ofdm.synth_frames(1, S, R_total, C, X, prefix=prefix, seed=args.seed, frame0=f,
+                                 noise_std=args.noise)
+        ref = ofdm.frame_demod(full, X, prefix)[0].cpu().numpy().astype(np.complex128).ravel()
+        got = out[f].cpu().numpy().astype(np.complex128).ravel()
+        del full
+        nrel = float(np.linalg.norm(got - ref) / max(np.linalg.norm(ref), 1e-30))
+        rms = float(np.sqrt(np.mean(np.abs(ref) ** 2)))
+        erel = float(np.max(np.abs(got - ref) / np.maximum(np.abs(ref), rms)))
+        worst_n, worst_e = max(worst_n, nrel), max(worst_e, erel)
+    torch.cuda.empty_cache()
+    ok = bool(np.isfinite(worst_n) and worst_n <= 1e-5 and worst_e <= 1e-5)
+    if not ok:
+        log(f"SPLIT PARITY FAILURE: norm-rel {worst_n:.3e}, elem-rel {worst_e:.3e} vs the full receiver")
+    return {"frames": sorted({0, F - 1}), "antennas": R_total, "norm_rel": worst_n, "max_elem_rel": worst_e,
+            "tolerance": 1e-5, "ok": ok}
 
 
 if __name__ == "__main__":

@@ -95,40 +95,38 @@ int carve(void *d_ws, size_t bytes, long long F, int S, int R, int C, bool need_
 }
 
 // What each frame workspace holds (host-side registry, per process): the
-// geometry of the estimate last stored in it, whether its Hc rows are in a
-// fused kernel's lane order and whether P is an antenna-split partial.  The
-// consumers (combine, mrc_partial, export) refuse a workspace whose estimate
-// was made for another geometry instead of dividing by the wrong |H|^2.
-// quad4k: the C = 4096 estimate is in the lane order of the wave-quad kernels
-// (frame_td4096r.hip, used when the rows are 16-byte aligned: even prefix),
-// not of the wave-pair ones.
+// geometry of the estimate last stored in it, the workspace size it was
+// carved for, whether its Hc rows are in a fused kernel's lane order and
+// whether P is an antenna-split partial.  The consumers (combine,
+// mrc_partial, export) refuse a workspace whose estimate was made for another
+// geometry or layout instead of dividing by the wrong |H|^2.  An estimate
+// call drops the workspace's entry before it launches anything and records
+// the new one only once every launch has been enqueued, so a failed estimate
+// leaves no tag behind; ofdm_workspace_release() drops the entry when the
+// caller frees the memory (the Python binding does it from the workspace
+// tensor's finaliser), so a new workspace at a recycled address holds no
+// estimate until one is made in it.
 struct WsTag {
     long long F;
     int S, R, C;
-    bool lane_order, partial, quad4k;
+    size_t bytes;
+    bool lane_order, partial;
 };
 std::mutex g_ws_mu;
 std::map<const void *, WsTag> g_ws;
 
-void ws_record(const void *ws, long long F, int S, int R, int C, bool lane_order, bool partial,
-               bool quad4k = false) {
+void ws_record(const void *ws, size_t bytes, long long F, int S, int R, int C, bool lane_order, bool partial) {
     std::lock_guard<std::mutex> lock(g_ws_mu);
-    g_ws[ws] = WsTag{F, S, R, C, lane_order, partial, quad4k};
+    g_ws[ws] = WsTag{F, S, R, C, bytes, lane_order, partial};
 }
 
-bool quad4k(const void *iq, int C, int prefix) {
-    return C == 4096 && ofdm::td4096r_ok(reinterpret_cast<const float2 *>(iq), prefix);
-}
-int quad4k_check(const WsTag &t, const void *iq, int C, int prefix, const char *fn) {
-    if (t.C == 4096 && t.lane_order && t.quad4k != quad4k(iq, C, prefix))
-        return fail(OFDM_E_ARG, "%s: the C=4096 estimate was made for %s rows (the kernel depends on "
-                                "16-byte row alignment: even prefix), these rows are %s", fn,
-                    t.quad4k ? "aligned" : "unaligned", t.quad4k ? "unaligned" : "aligned");
-    return OFDM_OK;
+void ws_forget(const void *ws) {
+    std::lock_guard<std::mutex> lock(g_ws_mu);
+    g_ws.erase(ws);
 }
 
 // need_full: the consumer divides by P, so a partial (antenna-split) P is refused
-int ws_check(const void *ws, long long F, int S, int R, int C, bool need_full, const char *fn,
+int ws_check(const void *ws, size_t bytes, long long F, int S, int R, int C, bool need_full, const char *fn,
              WsTag *out = nullptr) {
     std::lock_guard<std::mutex> lock(g_ws_mu);
     auto it = g_ws.find(ws);
@@ -139,6 +137,8 @@ int ws_check(const void *ws, long long F, int S, int R, int C, bool need_full, c
     if (t.F != F || t.S != S || t.R != R || t.C != C)
         return fail(OFDM_E_ARG, "%s: the workspace estimate is for nframes=%lld S=%d R=%d C=%d, "
                                 "called with nframes=%lld S=%d R=%d C=%d", fn, t.F, t.S, t.R, t.C, F, S, R, C);
+    if (t.bytes != bytes)
+        return fail(OFDM_E_ARG, "%s: the workspace was filled as %zu bytes, called with %zu", fn, t.bytes, bytes);
     if (need_full && t.partial)
         return fail(OFDM_E_ARG, "%s: the workspace holds a partial (antenna-split) |H|^2; "
                                 "finalise with ofdm_mrc_finalize instead", fn);
@@ -346,6 +346,11 @@ size_t ofdm_frame_workspace_bytes(long long nframes, int S, int R, int C) {
     return ws_bytes(nframes, S, R, C, !fused_c(C));
 }
 
+int ofdm_workspace_release(const void *d_ws) {
+    ws_forget(d_ws);
+    return OFDM_OK;
+}
+
 int ofdm_frame_estimate(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, int prefix,
                         const ofdm_cf32 *d_X, void *d_ws, size_t ws_bytes_, ofdm_stream_t stream) {
     int rc = check_frame_args(d_iq, nframes, S, R, C, prefix, d_ws, "ofdm_frame_estimate");
@@ -354,12 +359,13 @@ int ofdm_frame_estimate(const ofdm_cf32 *d_iq, long long nframes, int S, int R, 
     if (nframes == 0) return OFDM_OK;
     Workspace w;
     if ((rc = carve(d_ws, ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
+    ws_forget(d_ws);
     hipStream_t s = hs(stream);
     if (fused_c(C))
         rc = hip_check(ls_fused(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w.Hc, w.P, 0, s), "ls_fused");
     else
         rc = td_staged(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w, nullptr, 2, s);
-    if (rc == OFDM_OK) ws_record(d_ws, nframes, S, R, C, fused_c(C), false, quad4k(d_iq, C, prefix));
+    if (rc == OFDM_OK) ws_record(d_ws, ws_bytes_, nframes, S, R, C, fused_c(C), false);
     return rc;
 }
 
@@ -369,11 +375,10 @@ int ofdm_frame_combine(const ofdm_cf32 *d_iq, long long nframes, int S, int R, i
     if (rc) return rc;
     if (nframes == 0) return OFDM_OK;
     WsTag tag;
-    if ((rc = ws_check(d_ws, nframes, S, R, C, true, "ofdm_frame_combine", &tag))) return rc;
+    if ((rc = ws_check(d_ws, ws_bytes_, nframes, S, R, C, true, "ofdm_frame_combine", &tag))) return rc;
     if (tag.lane_order != fused_c(C))
         return fail(OFDM_E_ARG, "ofdm_frame_combine: the workspace holds a frequency-domain estimate "
                                 "(use ofdm_frame_combine_freq)");
-    if ((rc = quad4k_check(tag, d_iq, C, prefix, "ofdm_frame_combine"))) return rc;
     Workspace w;
     if ((rc = carve(d_ws, ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
     hipStream_t s = hs(stream);
@@ -395,16 +400,20 @@ int ofdm_frame_demod(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int
     Workspace w;
     if ((rc = carve(d_ws, ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
     hipStream_t s = hs(stream);
-    ws_record(d_ws, nframes, S, R, C, fused_c(C), false, quad4k(d_iq, C, prefix));
+    ws_forget(d_ws);
     if (fused_c(C)) {
         rc = hip_check(ls_fused(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w.Hc, w.P, 0, s),
                        "ls_fused");
         if (rc) return rc;
+        // the estimate is in the workspace once the LS launch is enqueued
+        ws_record(d_ws, ws_bytes_, nframes, S, R, C, true, false);
         return hip_check(mrc_fused(F2(d_iq), nframes, S, R, C, prefix, w.Hc, w.P,
                                                  F2(d_out), 0, s),
                          "mrc_fused");
     }
-    return td_staged(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w, F2(d_out), 0, s);
+    rc = td_staged(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w, F2(d_out), 0, s);
+    if (rc == OFDM_OK) ws_record(d_ws, ws_bytes_, nframes, S, R, C, false, false);
+    return rc;
 }
 
 int ofdm_frame_estimate_freq(const ofdm_cf32 *d_Y, long long nframes, int S, int R, int C,
@@ -415,10 +424,11 @@ int ofdm_frame_estimate_freq(const ofdm_cf32 *d_Y, long long nframes, int S, int
     if (nframes == 0) return OFDM_OK;
     Workspace w;
     if ((rc = carve(d_ws, ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
+    ws_forget(d_ws);
     rc = hip_check(ofdm::launch_ls_freq(F2(d_Y), (long long)S * R * C, nframes, R, C, F2(d_X), w.Hc,
                                         (long long)R * C, C, 1, w.P, C, 1, hs(stream)),
                    "ls_freq");
-    if (rc == OFDM_OK) ws_record(d_ws, nframes, S, R, C, false, false);
+    if (rc == OFDM_OK) ws_record(d_ws, ws_bytes_, nframes, S, R, C, false, false);
     return rc;
 }
 
@@ -428,7 +438,7 @@ int ofdm_frame_combine_freq(const ofdm_cf32 *d_Y, long long nframes, int S, int 
     if (rc) return rc;
     if (nframes == 0) return OFDM_OK;
     WsTag tag;
-    if ((rc = ws_check(d_ws, nframes, S, R, C, true, "ofdm_frame_combine_freq", &tag))) return rc;
+    if ((rc = ws_check(d_ws, ws_bytes_, nframes, S, R, C, true, "ofdm_frame_combine_freq", &tag))) return rc;
     if (tag.lane_order)
         return fail(OFDM_E_ARG, "ofdm_frame_combine_freq: the workspace holds a time-domain estimate in the "
                                 "fused kernels' lane order (use ofdm_frame_combine)");
@@ -462,11 +472,12 @@ int ofdm_frame_demod_freq_mfma(const ofdm_cf32 *d_Y, long long nframes, int S, i
     if ((rc = carve(d_ws, ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
     hipStream_t s = hs(stream);
     const long long fst = (long long)S * R * C;
-    ws_record(d_ws, nframes, S, R, C, false, false);
+    ws_forget(d_ws);
     rc = hip_check(ofdm::launch_ls_freq(F2(d_Y), fst, nframes, R, C, F2(d_X), w.Hc, (long long)R * C, C,
                                         1, w.P, C, 1, s),
                    "ls_freq");
     if (rc) return rc;
+    ws_record(d_ws, ws_bytes_, nframes, S, R, C, false, false);
     return hip_check(ofdm::launch_mrc_freq_mfma(F2(d_Y) + (long long)R * C, fst, (long long)R * C, nframes,
                                                 S - 1, R, C, w.Hc, (long long)R * C, w.P, C, F2(d_out), 0, s),
                      "mrc_freq_mfma");
@@ -482,13 +493,14 @@ int ofdm_frame_ls_partial(const ofdm_cf32 *d_iq, long long nframes, int S, int R
     Workspace w;
     if ((rc = carve(d_ws, ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
     hipStream_t s = hs(stream);
+    ws_forget(d_ws);
     if (fused_c(C))
         rc = hip_check(ls_fused(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w.Hc, w.P, 1, s),
                        "ls_fused");
     else
         rc = td_staged(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w, nullptr, 2, s);
     if (rc) return rc;
-    ws_record(d_ws, nframes, S, R, C, fused_c(C), true, quad4k(d_iq, C, prefix));
+    ws_record(d_ws, ws_bytes_, nframes, S, R, C, fused_c(C), true);
     // bins 1..C-1 of the bin-layout P -> [F][K]
     const int K = C - 1;
     return hip_check(hipMemcpy2DAsync(d_P, K * sizeof(float), w.P + 1, C * sizeof(float),
@@ -503,8 +515,10 @@ int ofdm_frame_mrc_partial(const ofdm_cf32 *d_iq, long long nframes, int S, int 
     if (rc) return rc;
     if (nframes == 0) return OFDM_OK;
     WsTag tag;
-    if ((rc = ws_check(d_ws, nframes, S, R, C, false, "ofdm_frame_mrc_partial", &tag))) return rc;
-    if ((rc = quad4k_check(tag, d_iq, C, prefix, "ofdm_frame_mrc_partial"))) return rc;
+    if ((rc = ws_check(d_ws, ws_bytes_, nframes, S, R, C, false, "ofdm_frame_mrc_partial", &tag))) return rc;
+    if (tag.lane_order != fused_c(C))
+        return fail(OFDM_E_ARG, "ofdm_frame_mrc_partial: the workspace holds a frequency-domain estimate, "
+                                "not the time-domain one of ofdm_frame_ls_partial / ofdm_frame_estimate");
     Workspace w;
     if ((rc = carve(d_ws, ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
     hipStream_t s = hs(stream);
@@ -522,12 +536,12 @@ int ofdm_frame_export_estimate(const void *d_ws, size_t ws_bytes_, long long nfr
         return fail(OFDM_E_ARG, "ofdm_frame_export_estimate: frame %lld outside [0, %lld)", frame, nframes);
     if (S < 2 || R < 1 || !pow2_c(C)) return fail(OFDM_E_ARG, "ofdm_frame_export_estimate: bad geometry");
     WsTag tag;
-    int rc = ws_check(d_ws, nframes, S, R, C, false, "ofdm_frame_export_estimate", &tag);
+    int rc = ws_check(d_ws, ws_bytes_, nframes, S, R, C, false, "ofdm_frame_export_estimate", &tag);
     if (rc) return rc;
     Workspace w;
     if ((rc = carve(const_cast<void *>(d_ws), ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
     return hip_check(ofdm::launch_export_estimate(w.Hc + frame * R * C, w.P + frame * C, R, C, tag.lane_order,
-                                                  tag.quad4k, F2(d_Hconj), d_Hsqrd, hs(stream)),
+                                                  F2(d_Hconj), d_Hsqrd, hs(stream)),
                      "ofdm_frame_export_estimate");
 }
 

@@ -175,7 +175,11 @@ k_mrc_td2048(const float2 *__restrict__ iq, int S, int R, int prefix, const floa
             row_fft2048<true, true, PK>(sym + (long long)r * Cp, t, T, lds, xe, xo);
         __builtin_amdgcn_sched_barrier(0);
         const float4 *hr = Hf + (long long)r * (C / 2);
-        // matrixMultThenSum (cpuLS.hpp:203-204), antennas in order
+        // matrixMultThenSum (cpuLS.hpp:191-206): antennas summed in order.  With
+        // PK & 4 (the default) the complex MAC is NOT the reference's
+        // expression acc + (x.re h.re - x.im h.im): it is two FMA-contracted
+        // packed steps (acc + x.re h) + (-x.im) h~, a reassociated sum that
+        // matches cpuLS.hpp within the parity tolerance (1e-5), not bit for bit.
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             const float4 h = (DBG & 2) ? float4{1.f, (float)k, (float)r, 1.f} : hr[k * 64 + t];

@@ -488,9 +488,6 @@ k_mrc_td4096h(const float2 *__restrict__ iq, int S, int R, int prefix, const flo
 hipError_t launch_ls_td4096(const float2 *iq, long long nframes, int S, int R, int prefix,
                             const float2 *X, float2 *Hc, float *P, int partial, hipStream_t s) {
     using namespace td4096;
-#ifdef OFDM_AB_KNOBS
-    if (td4096r_ok(iq, prefix)) return launch_ls_td4096r(iq, nframes, S, R, prefix, X, Hc, P, partial, s);
-#endif
     if (nframes <= 0) return hipSuccess;
     if (nframes > 0x7fffffffll) return hipErrorInvalidValue;
     auto kern = k_ls_td4096<LS_WAVES>;
@@ -504,9 +501,6 @@ hipError_t launch_ls_td4096(const float2 *iq, long long nframes, int S, int R, i
 hipError_t launch_mrc_td4096(const float2 *iq, long long nframes, int S, int R, int prefix,
                              const float2 *Hc, const float *P, float2 *out, int mode, hipStream_t s) {
     using namespace td4096;
-#ifdef OFDM_AB_KNOBS
-    if (td4096r_ok(iq, prefix)) return launch_mrc_td4096r(iq, nframes, S, R, prefix, Hc, P, out, mode, s);
-#endif
     const long long nq = nframes * (S - 1);
     if (nq <= 0) return hipSuccess;
     const long long bpf = ((S - 1) + H_PAIRS - 1) / H_PAIRS, nb = nframes * bpf, pxcd = (nb + 7) / 8;

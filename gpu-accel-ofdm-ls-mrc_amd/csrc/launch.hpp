@@ -104,18 +104,6 @@ hipError_t launch_ls_td4096(const float2 *iq, long long nframes, int S, int R, i
                             const float2 *X, float2 *Hc, float *P, int partial, hipStream_t s);
 hipError_t launch_mrc_td4096(const float2 *iq, long long nframes, int S, int R, int prefix,
                              const float2 *Hc, const float *P, float2 *out, int mode, hipStream_t s);
-// C = 4096 on wave quads with the register-only FFT and row DMA
-// (frame_td4096r.hip, A/B build only); rows must be 16-byte aligned
-// (td4096r_ok), and the estimate is in its own lane order (stages.hip hc_pos)
-#ifdef OFDM_AB_KNOBS
-bool td4096r_ok(const float2 *iq, int prefix);
-#else
-inline bool td4096r_ok(const float2 *, int) { return false; }
-#endif
-hipError_t launch_ls_td4096r(const float2 *iq, long long nframes, int S, int R, int prefix,
-                             const float2 *X, float2 *Hc, float *P, int partial, hipStream_t s);
-hipError_t launch_mrc_td4096r(const float2 *iq, long long nframes, int S, int R, int prefix,
-                              const float2 *Hc, const float *P, float2 *out, int mode, hipStream_t s);
 hipError_t launch_conj_product(const float2 *Y, long long nsyms, int R, int C, const float2 *Hc,
                                float2 *prod, hipStream_t s);
 hipError_t launch_combine(const float2 *prod, long long nsyms, int R, int K, const float *P,
@@ -123,10 +111,9 @@ hipError_t launch_combine(const float2 *prod, long long nsyms, int R, int K, con
 hipError_t launch_shift_rows(const float2 *in, long long nrows, int K, float2 *out, hipStream_t s);
 hipError_t launch_dist_sqrd(const float2 *H, int R, int K, float *P, hipStream_t s);
 // One frame's workspace estimate (Hc rows of C float2: lane_order = the
-// fused LS kernel for C wrote them, quad4k = the C = 4096 wave-quad one,
-// else bin layout; P bin-indexed) ->
+// fused LS kernel for C wrote them, else bin layout; P bin-indexed) ->
 // Hconj [R][K], Hsqrd [K] (may be null).
-hipError_t launch_export_estimate(const float2 *Hc, const float *P, int R, int C, bool lane_order, bool quad4k,
+hipError_t launch_export_estimate(const float2 *Hc, const float *P, int R, int C, bool lane_order,
                                   float2 *Hconj, float *Hsqrd, hipStream_t s);
 
 // Synthetic frames: time-domain (freq_domain=0, rows of C+prefix with a

@@ -184,12 +184,13 @@ __global__ void __launch_bounds__(256) k_mrc_freq_frames(const float2 *__restric
         float4 y[G];
         const float4 h = Hq[(long long)r * ld4];
 #pragma unroll
-        for (int g = 0; g < G; ++g) y[g] = nt_load4(Yq[g] + (long long)r * ld4);
+        for (int g = 0; g < G; ++g) y[g] = NT ? nt_load4(Yq[g] + (long long)r * ld4) : Yq[g][(long long)r * ld4];
         mac(h, y);
     }
     const int j0 = 2 * m - 1, j1 = 2 * m;  // subcarriers of bins 2m, 2m+1
+    // P is read only when dividing (mode 0): a numerator-only caller may pass none
     const float *Pf = P + f * p_fstride + p_jofs;
-    const float p0 = m > 0 ? Pf[j0] : 1.f, p1 = Pf[j1];
+    const float p0 = (mode == 0 && m > 0) ? Pf[j0] : 1.f, p1 = mode == 0 ? Pf[j1] : 1.f;
     const int o0 = mode == 0 ? out_pos(j0 < 0 ? 0 : j0, K) : j0, o1 = mode == 0 ? out_pos(j1, K) : j1;
 #pragma unroll
     for (int g = 0; g < G; ++g) {

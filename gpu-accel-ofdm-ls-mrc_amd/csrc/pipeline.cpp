@@ -174,16 +174,30 @@ int ofdm_pipeline_submit(ofdm_pipeline *p, long long nframes, ofdm_cf32 *out) {
     if (nframes < 0 || nframes > p->chunk) return err(OFDM_E_ARG, fn, "nframes out of [0, chunk_frames]");
     DeviceGuard dg(p->device);
     // any failure below releases the slot (its frames are not demodulated) so
-    // the pipeline stays usable: the next acquire hands out the same slot
+    // the pipeline stays usable: the next acquire hands out the same slot.
+    // Once anything may have been enqueued on the compute stream for this slot
+    // (from the wait on in_done on), the failure path still records
+    // comp_done / out_done and marks the slot used (best effort), so that the
+    // next acquire makes the copy-in wait for whatever kernel of this submit
+    // is still reading the slot's IQ.
     struct Release {
+        ofdm_pipeline *p;
         ofdm_pipeline::Slot &s;
-        bool ok = false;
+        bool ok = false, enqueued = false;
         ~Release() {
-            if (!ok) s.acquired = false;
+            if (ok) return;
+            if (enqueued) {
+                (void)hipEventRecord(s.comp_done, p->s_comp);
+                (void)hipStreamWaitEvent(p->s_out, s.comp_done, 0);
+                (void)hipEventRecord(s.out_done, p->s_out);
+                s.used = true;
+            }
+            s.acquired = false;
         }
-    } rel{s};
+    } rel{p, s};
     PL_TRY(dg.e, fn, "hipSetDevice");
     PL_TRY(hipEventRecord(s.in_done, p->s_in), fn, "hipEventRecord");
+    rel.enqueued = true;
     PL_TRY(hipStreamWaitEvent(p->s_comp, s.in_done, 0), fn, "hipStreamWaitEvent");
     if (s.used) PL_TRY(hipStreamWaitEvent(p->s_comp, s.out_done, 0), fn, "hipStreamWaitEvent");
     if (nframes > 0) {

@@ -71,20 +71,8 @@ __device__ __forceinline__ int lane_of(int b, int &k) {  // b < 1024
     k = (b >> 4) & 15;
     return 4 * q + (((c & 1) << 1) | (c >> 1));
 }
-// C = 4097: the C = 4096 wave-quad layout (frame_td4096r.hip): plane b & 3
-// of 1024 float2, register j of lane t at float4 (j >> 1) * 64 + t, where
-// (t, j) inverts rfft_bin (rfft1024.hpp) for b >> 2
-__device__ __forceinline__ int hc_pos_quad(int b) {
-    const int c = b & 3, bp = b >> 2;
-    const int k2 = bp & 15, khi = (bp >> 4) & 3, klo = bp >> 6;
-    const int j = (k2 & 3) | (khi << 2);
-    const int ca = klo >> 2, a = ((ca & 1) << 1) | (ca >> 1);
-    const int t = a | (((klo >> 1) & 1) << 2) | ((klo & 1) << 3) | (((k2 >> 2) & 1) << 4) | ((k2 >> 3) << 5);
-    return c * 1024 + 2 * ((j >> 1) * 64 + t) + (j & 1);
-}
 __device__ __forceinline__ int hc_pos(int b, int C) {  // C = 0: bin layout
     int k;
-    if (C == 4097) return hc_pos_quad(b);
     if (C == 1024) {  // float4 (k >> 1) * 64 + t holds bins (k & ~1, k | 1) of lane t
         const int t = lane_of(b, k);
         return 2 * ((k >> 1) * 64 + t) + (k & 1);
@@ -112,10 +100,10 @@ __global__ void __launch_bounds__(256) k_export_estimate(const float2 *__restric
     }
 }
 
-hipError_t launch_export_estimate(const float2 *Hc, const float *P, int R, int C, bool lane_order, bool quad4k,
+hipError_t launch_export_estimate(const float2 *Hc, const float *P, int R, int C, bool lane_order,
                                   float2 *Hconj, float *Hsqrd, hipStream_t s) {
     if (R > 65535) return hipErrorInvalidValue;
-    const int lay = !lane_order ? 0 : (C == 4096 && quad4k) ? 4097 : C;
+    const int lay = lane_order ? C : 0;
     hipLaunchKernelGGL(k_export_estimate, dim3((unsigned)((C - 1 + 255) / 256), (unsigned)R), dim3(256), 0, s,
                        Hc, P, R, C, lay, Hconj, Hsqrd);
     return hipGetLastError();

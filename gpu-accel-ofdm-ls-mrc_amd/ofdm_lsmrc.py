@@ -47,6 +47,7 @@ _SIGS = {
     "ofdm_shift_rows": (_I, [_P, _LL, _I, _P, _P]),
     "ofdm_dist_sqrd": (_I, [_P, _I, _I, _P, _P]),
     "ofdm_frame_workspace_bytes": (_c.c_size_t, [_LL, _I, _I, _I]),
+    "ofdm_workspace_release": (_I, [_P]),
     "ofdm_frame_demod": (_I, [_P, _LL, _I, _I, _I, _I, _P, _P, _c.c_size_t, _P, _P]),
     "ofdm_frame_estimate": (_I, [_P, _LL, _I, _I, _I, _I, _P, _P, _c.c_size_t, _P]),
     "ofdm_frame_combine": (_I, [_P, _LL, _I, _I, _I, _I, _P, _c.c_size_t, _P, _P]),
@@ -235,9 +236,21 @@ def workspace_bytes(nframes, S, R, C):
 
 
 def workspace(nframes, S, R, C, device="cuda"):
+    """A frame workspace.  When the tensor is collected its estimate tag is
+    dropped from the library's registry (ofdm_workspace_release), so that a
+    workspace the caching allocator later hands out at the same address is
+    refused by combine / mrc_partial / export until an estimate fills it."""
     import torch
-    return torch.empty(max(workspace_bytes(nframes, S, R, C), 256), dtype=torch.uint8,
-                       device=device)
+    import weakref
+    ws = torch.empty(max(workspace_bytes(nframes, S, R, C), 256), dtype=torch.uint8, device=device)
+    weakref.finalize(ws, lib().ofdm_workspace_release, _c.c_void_p(ws.data_ptr()))
+    return ws
+
+
+def workspace_release(ws):
+    """Forget the estimate held in `ws` (a tensor or a raw device address)."""
+    ptr = ws if isinstance(ws, int) else ws.data_ptr()
+    lib().ofdm_workspace_release(_c.c_void_p(ptr))
 
 
 def frame_demod(iq, X, prefix=0, ws=None, out=None, stream=None):

@@ -132,9 +132,20 @@ int ofdm_dist_sqrd(const ofdm_cf32 *d_H, int R, int K, float *d_Hsqrd, ofdm_stre
  * (no fused kernel), a frequency-domain staging buffer of at most 256 MiB.
  * A workspace carries the estimate of ONE geometry: the calls that consume it
  * (ofdm_frame_combine, ofdm_frame_mrc_partial, ofdm_frame_export_estimate)
- * must pass the nframes, S, R and C of the call that filled it, and return
- * OFDM_E_ARG otherwise (checked per process, on the host). */
+ * must pass the nframes, S, R, C and ws_bytes of the call that filled it, and
+ * return OFDM_E_ARG otherwise (checked per process, on the host, by a registry
+ * keyed on d_ws).  An estimate call clears the workspace's entry before it
+ * launches and records it only after every launch was enqueued, so a failed
+ * estimate leaves a workspace that the consumers refuse. */
 size_t ofdm_frame_workspace_bytes(long long nframes, int S, int R, int C);
+
+/* Drops what the registry above knows about d_ws.  Call it before the memory
+ * is freed (or handed to another user): a workspace later allocated at the
+ * same address then holds no estimate until an estimate call fills it, and
+ * the consumers return OFDM_E_ARG instead of dividing by a stale |H|^2.  The
+ * Python binding calls it from the workspace tensor's finaliser.  NULL or an
+ * unknown pointer is a no-op; always returns OFDM_OK. */
+int ofdm_workspace_release(const void *d_ws);
 
 /* Frame-batched receiver on time-domain IQ (what ShMemSymBuff delivers):
  * d_iq = nframes x S x R x (C + cp_len) samples; the cyclic prefix of every

@@ -115,6 +115,64 @@ void oracle_fft_row(oracle_cf32 *row, int C, int inverse) {
     if (C > 4096) { free(re); free(im); }
 }
 
+/* Single-precision variant, for the timed CPU baseline only (bench.py
+ * cpu_baseline): the reference calls FFTW's single-precision fftwf
+ * (cpuLS.hpp:157-159, 170-172), so the baseline should not pay for a float64
+ * transform.  Same radix-2 DIT structure, f32 arithmetic, f32 twiddle table
+ * (the reference re-plans per row; here the table is reused).
+ * Results agree with the float64 form to f32 rounding of the FFT (~1e-6
+ * relative), which is NOT the parity path: parity uses oracle_fft_row. */
+static float *g_tw32[ORACLE_MAX_LOG2 + 1];
+
+static const float *twiddles32(int log2c) {
+    float *t = __atomic_load_n(&g_tw32[log2c], __ATOMIC_ACQUIRE);
+    if (t) return t;
+    int C = 1 << log2c;
+    int h = C / 2 > 0 ? C / 2 : 1;
+    const double *td = twiddles(log2c);
+    float *nt = (float *)malloc((size_t)h * 2 * sizeof(float));
+    for (int k = 0; k < 2 * h; ++k) nt[k] = (float)td[k];
+    float *expected = NULL;
+    if (!__atomic_compare_exchange_n(&g_tw32[log2c], &expected, nt, 0,
+                                     __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) {
+        free(nt);
+        return expected;
+    }
+    return nt;
+}
+
+void oracle_fft_row_f32(oracle_cf32 *row, int C) {
+    float re[4096], im[4096];
+    if (C > 4096) { oracle_fft_row(row, C, 0); return; }
+    int log2c = 0;
+    while ((1 << log2c) < C) ++log2c;
+    for (int i = 0; i < C; ++i) { re[i] = row[i].re; im[i] = row[i].im; }
+    for (int i = 1, j = 0; i < C; ++i) {
+        int bit = C >> 1;
+        for (; j & bit; bit >>= 1) j ^= bit;
+        j ^= bit;
+        if (i < j) {
+            float t = re[i]; re[i] = re[j]; re[j] = t;
+            t = im[i]; im[i] = im[j]; im[j] = t;
+        }
+    }
+    const float *tw = twiddles32(log2c);
+    for (int len = 2; len <= C; len <<= 1) {
+        int half = len / 2, step = C / len;
+        for (int i = 0; i < C; i += len) {
+            for (int k = 0; k < half; ++k) {
+                float wr = tw[2 * k * step], wi = -tw[2 * k * step + 1];
+                int a = i + k, b = i + k + half;
+                float xr = re[b] * wr - im[b] * wi;
+                float xi = re[b] * wi + im[b] * wr;
+                re[b] = re[a] - xr; im[b] = im[a] - xi;
+                re[a] += xr;        im[a] += xi;
+            }
+        }
+    }
+    for (int i = 0; i < C; ++i) { row[i].re = re[i]; row[i].im = im[i]; }
+}
+
 /* ------------------------------------------------------------------------ */
 /* LS channel estimate (firstVector, cpuLS.hpp:290-311)                      */
 /* ------------------------------------------------------------------------ */
@@ -181,27 +239,42 @@ void oracle_mrc(const oracle_cf32 *Yfft, const oracle_cf32 *Hconj,
 /* Frames                                                                       */
 /* ------------------------------------------------------------------------ */
 static void load_symbol(const oracle_cf32 *sym, int R, int C, int prefix,
-                        oracle_cf32 *Y) {
+                        oracle_cf32 *Y, int fft32) {
     /* ShMemSymBuff.hpp:309-322: drop the prefix of each row */
     for (int r = 0; r < R; ++r)
         memcpy(&Y[(size_t)r * C], &sym[(size_t)r * (C + prefix) + prefix],
                (size_t)C * sizeof(*Y));
     /* fftOneRow per antenna row (cpuLS.hpp:278-281, 342-345) */
-    for (int r = 0; r < R; ++r) oracle_fft_row(&Y[(size_t)r * C], C, 0);
+    for (int r = 0; r < R; ++r) {
+        if (fft32)
+            oracle_fft_row_f32(&Y[(size_t)r * C], C);
+        else
+            oracle_fft_row(&Y[(size_t)r * C], C, 0);
+    }
 }
+
+static void frame_demod_ex(const oracle_cf32 *iq, int S, int R, int C, int prefix,
+                           const oracle_cf32 *X, oracle_cf32 *out,
+                           oracle_cf32 *Hconj, float *Hsqrd, int fft32);
 
 void oracle_frame_demod(const oracle_cf32 *iq, int S, int R, int C, int prefix,
                         const oracle_cf32 *X, oracle_cf32 *out,
                         oracle_cf32 *Hconj, float *Hsqrd) {
+    frame_demod_ex(iq, S, R, C, prefix, X, out, Hconj, Hsqrd, 0);
+}
+
+static void frame_demod_ex(const oracle_cf32 *iq, int S, int R, int C, int prefix,
+                           const oracle_cf32 *X, oracle_cf32 *out,
+                           oracle_cf32 *Hconj, float *Hsqrd, int fft32) {
     int K = C - 1;
     size_t sym_elems = (size_t)R * (C + prefix);
     oracle_cf32 *Y = (oracle_cf32 *)malloc((size_t)R * C * sizeof(*Y));
     oracle_cf32 *H = Hconj ? Hconj : (oracle_cf32 *)malloc((size_t)R * K * sizeof(*H));
     float *P = Hsqrd ? Hsqrd : (float *)malloc((size_t)K * sizeof(*P));
-    load_symbol(iq, R, C, prefix, Y);
+    load_symbol(iq, R, C, prefix, Y, fft32);
     oracle_ls(Y, X, R, C, H, P);
     for (int s = 1; s < S; ++s) {
-        load_symbol(iq + (size_t)s * sym_elems, R, C, prefix, Y);
+        load_symbol(iq + (size_t)s * sym_elems, R, C, prefix, Y, fft32);
         oracle_mrc(Y, H, P, R, C, out + (size_t)(s - 1) * K);
     }
     free(Y);
@@ -221,6 +294,21 @@ void oracle_frames_demod(const oracle_cf32 *iq, long long nframes, int S, int R,
     for (long long f = 0; f < nframes; ++f)
         oracle_frame_demod(iq + f * frame_elems, S, R, C, prefix, X,
                            out + f * out_elems, NULL, NULL);
+    (void)nthreads;
+}
+
+void oracle_frames_demod_fft32(const oracle_cf32 *iq, long long nframes, int S, int R,
+                               int C, int prefix, const oracle_cf32 *X,
+                               oracle_cf32 *out, int nthreads) {
+    size_t frame_elems = (size_t)S * R * (C + prefix);
+    size_t out_elems = (size_t)(S - 1) * (C - 1);
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads)
+#endif
+    for (long long f = 0; f < nframes; ++f)
+        frame_demod_ex(iq + f * frame_elems, S, R, C, prefix, X,
+                       out + f * out_elems, NULL, NULL, 1);
     (void)nthreads;
 }
 

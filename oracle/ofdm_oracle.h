@@ -76,6 +76,14 @@ void oracle_frames_demod(const oracle_cf32 *iq, long long nframes, int S, int R,
                          int C, int prefix, const oracle_cf32 *X,
                          oracle_cf32 *out, int nthreads);
 
+/* The same receiver with a single-precision radix-2 FFT (oracle_fft_row_f32,
+ * the precision of the reference's fftwf): the timed CPU baseline of
+ * bench.py.  Not a parity path (oracle_frames_demod is). */
+void oracle_fft_row_f32(oracle_cf32 *row, int C);
+void oracle_frames_demod_fft32(const oracle_cf32 *iq, long long nframes, int S, int R,
+                               int C, int prefix, const oracle_cf32 *X,
+                               oracle_cf32 *out, int nthreads);
+
 /* Frequency-domain frames (FFT already applied, no prefix): pilot + (S-1)
  * data symbols of R x C each.  OpenMP over frames. */
 void oracle_frames_demod_freq(const oracle_cf32 *yf, long long nframes, int S,

@@ -42,6 +42,9 @@ class Oracle:
                                          _P, _P, _P, _P]
         L.oracle_frames_demod.argtypes = [_P, _c.c_longlong, _c.c_int, _c.c_int,
                                           _c.c_int, _c.c_int, _P, _P, _c.c_int]
+        L.oracle_frames_demod_fft32.argtypes = [_P, _c.c_longlong, _c.c_int, _c.c_int,
+                                                _c.c_int, _c.c_int, _P, _P, _c.c_int]
+        L.oracle_fft_row_f32.argtypes = [_P, _c.c_int]
         L.oracle_frames_demod_freq.argtypes = [_P, _c.c_longlong, _c.c_int, _c.c_int,
                                                _c.c_int, _P, _P, _c.c_int]
         L.oracle_max_threads.restype = _c.c_int
@@ -159,6 +162,22 @@ class Oracle:
         self.lib.oracle_frames_demod(_ptr(iq), F, S, R, C, prefix, _ptr(X), _ptr(out),
                                      nthreads)
         return out
+
+    def frames_demod_fft32(self, iq, X, prefix=0, nthreads=0):
+        """frames_demod with the single-precision FFT (timed CPU baseline only)."""
+        iq, X = c64(iq), c64(X)
+        F, S, R, Cp = iq.shape
+        C = Cp - prefix
+        out = np.empty((F, S - 1, C - 1), np.complex64)
+        self.lib.oracle_frames_demod_fft32(_ptr(iq), F, S, R, C, prefix, _ptr(X), _ptr(out),
+                                           nthreads)
+        return out
+
+    def fft_rows_f32(self, rows):
+        rows = c64(rows).copy()
+        for r in rows.reshape(-1, rows.shape[-1]):
+            self.lib.oracle_fft_row_f32(_ptr(r), r.shape[-1])
+        return rows
 
     def frames_demod_freq(self, yf, X, nthreads=0):
         yf, X = c64(yf), c64(X)

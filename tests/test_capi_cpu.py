@@ -97,6 +97,41 @@ def test_zf_argument_validation_without_device(ofdm):
     assert L.ofdm_zf_detect(fake, None, 4, 8, 16, 3, fake, None) == -1
 
 
+def test_workspace_registry_without_device(ofdm):
+    """The consumers of a workspace refuse one that no estimate call filled
+    (host registry, checked before any launch); releasing an unknown or null
+    workspace is a no-op."""
+    L = ofdm.lib()
+    P = ctypes.c_void_p
+    fake, ws = P(4096), P(1 << 20)
+    need = L.ofdm_frame_workspace_bytes(2, 5, 8, 1024)
+    assert L.ofdm_workspace_release(ws) == 0
+    assert L.ofdm_workspace_release(None) == 0
+    assert L.ofdm_frame_combine(fake, 2, 5, 8, 1024, 0, ws, need, fake, None) == -1
+    assert b"holds no estimate" in L.ofdm_last_error()
+    assert L.ofdm_frame_mrc_partial(fake, 2, 5, 8, 1024, 0, ws, need, fake, None) == -1
+    assert L.ofdm_frame_combine_freq(fake, 2, 5, 8, 1024, ws, need, fake, None) == -1
+    assert L.ofdm_frame_export_estimate(ws, need, 2, 5, 8, 1024, 0, fake, None, None) == -1
+    assert b"holds no estimate" in L.ofdm_last_error()
+
+
+def test_product_library_dispatches_only_product_kernels(ofdm):
+    """Measured-and-dropped candidates live in scripts/experiments, not in the
+    shipped library: no wave-quad C = 4096 receiver and no register-FFT test
+    kernel."""
+    import subprocess
+    path = ofdm.LIB_PATH
+    if path.endswith("_ab.so"):
+        pytest.skip("OFDM_LSMRC_LIB=ab selects the A/B build")
+    syms = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True,
+                          check=True).stdout
+    for bad in ("td4096r", "rfft"):
+        assert bad not in syms, f"{bad} kernel in the product library"
+    mk = open(os.path.join(os.path.dirname(os.path.dirname(path)), "Makefile")).read()
+    srcs = [l for l in mk.splitlines() if l.startswith("SRCS_HIP")][0]
+    assert "td4096r" not in srcs and "rfft" not in srcs
+
+
 def test_workspace_sizes(ofdm):
     # fused C=1024: Hc [F][R][C] + P [F][C], no staging
     F, S, R, C = 100, 101, 16, 1024

@@ -351,8 +351,7 @@ def test_concurrent_host_threads_large_lds_kernels(ofdm, dev):
 def test_frame_export_estimate_vs_oracle(ofdm, oracle, dev, R, C, prefix):
     """ofdm_frame_export_estimate (gpuLS's Hconj / Hsqrd view of a frame's
     estimate) against the oracle's LS on the same pilot rows: every fused
-    kernel's lane order, incl. the C = 4096 wave-quad layout (even prefix)
-    and the wave-pair one (odd prefix)."""
+    kernel's lane order, even and odd cyclic prefixes."""
     F, S = 3, 3
     X = qpsk_pilots(C - 1, seed=C + R)
     iq = ofdm.synth_frames(F, S, R, C, to_dev(X, dev), prefix=prefix, seed=77, noise_std=0.02)
@@ -367,23 +366,52 @@ def test_frame_export_estimate_vs_oracle(ofdm, oracle, dev, R, C, prefix):
         parity(host(P), P_ref)
 
 
-def test_combine_across_c4096_alignments(ofdm, dev):
-    """A C = 4096 estimate made on 16-byte aligned rows (even prefix) and
-    combined on rows of the other alignment (odd prefix): the library either
-    refuses (the two alignments run kernels with different estimate layouts)
-    or returns what frame_demod returns for those frames (one layout)."""
-    F, S, R, C = 1, 3, 4, 4096
+def test_workspace_recycled_address_holds_no_estimate(ofdm, dev):
+    """A workspace freed and re-allocated at the same address (torch's
+    caching allocator hands the block straight back) is refused by combine,
+    mrc_partial and export with OFDM_E_ARG until an estimate fills it: the
+    tensor's finaliser drops the registry entry (ofdm_workspace_release)."""
+    import gc
+    import torch
+    F, S, R, C = 2, 5, 8, 1024
     X = to_dev(qpsk_pilots(C - 1), dev)
-    iq0 = ofdm.synth_frames(F, S, R, C, X, prefix=0, seed=3)
-    iq1 = ofdm.synth_frames(F, S, R, C, X, prefix=1, seed=3)
-    ws = ofdm.workspace(F, S, R, C, dev)
-    ofdm.frame_estimate(iq0, X, 0, ws)
+    iq = ofdm.synth_frames(F, S, R, C, X, seed=5, noise_std=0.02)
     out = ofdm.c64((F, S - 1, C - 1), dev)
-    try:
-        ofdm.frame_combine(iq1, 1, ws, out)
-    except ofdm.OfdmError:
-        return
-    # same channel and pilots (same seed), so the estimates agree: compare
-    # with the one-call receiver on iq1
-    ref = ofdm.frame_demod(iq1, X, prefix=1)
-    parity(host(out), host(ref))
+    ws = ofdm.workspace(F, S, R, C, dev)
+    ofdm.frame_estimate(iq, X, 0, ws)
+    ref = host(ofdm.frame_combine(iq, 0, ws, out))
+    addr = ws.data_ptr()
+    del ws
+    gc.collect()
+    ws2 = ofdm.workspace(F, S, R, C, dev)
+    if ws2.data_ptr() != addr:
+        pytest.skip("the allocator did not recycle the address")
+    for call in (lambda: ofdm.frame_combine(iq, 0, ws2, out),
+                 lambda: ofdm.frame_mrc_partial(iq, ws2, 0),
+                 lambda: ofdm.frame_export_estimate(ws2, F, S, R, C)):
+        with pytest.raises(ofdm.OfdmError, match=r"failed \(-1\).*holds no estimate"):
+            call()
+    ofdm.frame_estimate(iq, X, 0, ws2)
+    assert (host(ofdm.frame_combine(iq, 0, ws2, out)) == ref).all()
+    # explicit release of a live workspace, and a failed estimate leaves no tag
+    ofdm.workspace_release(ws2)
+    with pytest.raises(ofdm.OfdmError, match="holds no estimate"):
+        ofdm.frame_combine(iq, 0, ws2, out)
+    ofdm.frame_estimate(iq, X, 0, ws2)
+    with pytest.raises(ofdm.OfdmError):
+        ofdm.frame_estimate(iq, X, 0, ws2[:256])  # too small: refused before any launch
+    ofdm.frame_combine(iq, 0, ws2, out)  # the earlier estimate is untouched
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("C", [1024, 2048, 4096])
+def test_mrc_partial_refuses_frequency_domain_estimate(ofdm, dev, C):
+    """ofdm_frame_mrc_partial reads Hc in the fused kernels' lane order; an
+    estimate from ofdm_frame_estimate_freq (bin layout) is refused."""
+    F, S, R = 1, 3, 4
+    X = to_dev(qpsk_pilots(C - 1), dev)
+    Y = ofdm.synth_frames(F, S, R, C, X, seed=8, noise_std=0.05, freq_domain=True)
+    ws = ofdm.workspace(F, S, R, C, dev)
+    ofdm.frame_estimate_freq(Y, X, ws)
+    with pytest.raises(ofdm.OfdmError, match="frequency-domain estimate"):
+        ofdm.frame_mrc_partial(Y, ws, 0)

@@ -71,6 +71,24 @@ def test_oracle_fft_matches_numpy(oracle, C):
     assert np.max(np.abs(inv - refi)) <= 1e-6 * np.max(np.abs(refi))
 
 
+@pytest.mark.parametrize("C", [4, 64, 1024, 4096])
+def test_oracle_f32_fft_for_cpu_baseline(oracle, C):
+    """The single-precision FFT that bench.py's cpu_baseline times (the
+    precision class of the reference's fftwf) computes the same transform:
+    within f32 radix-2 rounding of the exact DFT, and the receiver built on it
+    within the north-star tolerance of the float64-FFT oracle."""
+    rng = np.random.default_rng(C + 1)
+    x = (rng.standard_normal((3, C)) + 1j * rng.standard_normal((3, C))).astype(np.complex64)
+    ref = np.fft.fft(x.astype(np.complex128), axis=-1)
+    got = oracle.fft_rows_f32(x)
+    assert np.max(np.abs(got - ref)) <= 2e-6 * np.log2(C) * np.max(np.abs(ref))
+    if C == 1024:
+        z = np.load(os.path.join(GOLDEN, "cfg1_r4_c1024_s10.npz"))
+        a = oracle.frames_demod(z["iq"], z["X"], int(z["prefix"]))
+        b = oracle.frames_demod_fft32(z["iq"], z["X"], int(z["prefix"]))
+        assert np.linalg.norm(b - a) <= 1e-5 * np.linalg.norm(a)
+
+
 @needs_ref
 @pytest.mark.parametrize("R,C", [(1, 4), (3, 64), (16, 1024), (64, 1024), (7, 2048)])
 def test_oracle_bitexact_vs_reference_build(oracle, R, C):
