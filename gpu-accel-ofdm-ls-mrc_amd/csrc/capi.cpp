@@ -529,6 +529,46 @@ int ofdm_frame_mrc_partial(const ofdm_cf32 *d_iq, long long nframes, int S, int 
     return td_staged(F2(d_iq), nframes, S, R, C, prefix, nullptr, w, F2(d_num), 1, s);
 }
 
+int ofdm_symbols_demod(const ofdm_cf32 *d_sym, long long nsym, int R, int C, int prefix, const void *d_ws,
+                       size_t ws_bytes_, long long frame, ofdm_cf32 *d_out, ofdm_stream_t stream) {
+    static const char *fn = "ofdm_symbols_demod";
+    if (nsym < 0 || nsym > 0x7ffffffell) return fail(OFDM_E_ARG, "%s: nsym=%lld out of range", fn, nsym);
+    if (nsym > 0 && (!d_sym || !d_out)) return fail(OFDM_E_ARG, "%s: null pointer", fn);
+    if (R < 1) return fail(OFDM_E_ARG, "%s: R=%d < 1", fn, R);
+    if (!fused_c(C))
+        return fail(OFDM_E_UNSUPPORTED, "%s: C=%d (the fused receivers cover C = 1024, 2048, 4096)", fn, C);
+    if (prefix < 0 || prefix > C) return fail(OFDM_E_ARG, "%s: prefix=%d out of [0, C]", fn, prefix);
+    if (!aligned(d_sym, 16)) return fail(OFDM_E_ARG, "%s: input must be 16-byte aligned", fn);
+    WsTag tag;
+    {
+        std::lock_guard<std::mutex> lock(g_ws_mu);
+        auto it = g_ws.find(d_ws);
+        if (it == g_ws.end())
+            return fail(OFDM_E_ARG, "%s: the workspace holds no estimate (run ofdm_frame_estimate on it first)", fn);
+        tag = it->second;
+    }
+    if (tag.R != R || tag.C != C || tag.bytes != ws_bytes_)
+        return fail(OFDM_E_ARG, "%s: the workspace estimate is for R=%d C=%d (%zu bytes), called with R=%d C=%d "
+                                "(%zu bytes)", fn, tag.R, tag.C, tag.bytes, R, C, ws_bytes_);
+    if (!tag.lane_order || tag.partial)
+        return fail(OFDM_E_ARG, "%s: the workspace holds a %s estimate, not ofdm_frame_estimate's", fn,
+                    tag.partial ? "partial (antenna-split)" : "frequency-domain");
+    if (frame < 0 || frame >= tag.F)
+        return fail(OFDM_E_ARG, "%s: frame %lld outside the workspace's [0, %lld)", fn, frame, tag.F);
+    if (nsym == 0) return OFDM_OK;
+    Workspace w;
+    int rc = carve(const_cast<void *>(d_ws), ws_bytes_, tag.F, tag.S, R, C, false, w);
+    if (rc) return rc;
+    // The fused MRC kernels read data symbols 1..S-1 of frame 0 at
+    // iq + s * R * (C + prefix) and never touch symbol 0 (the pilot, read by
+    // the LS kernels only): a "frame" whose symbol 1 is d_sym[0] is the run.
+    const long long row = (long long)R * (C + prefix);
+    const float2 *iq = reinterpret_cast<const float2 *>(reinterpret_cast<uintptr_t>(d_sym) - (uintptr_t)(row * 8));
+    return hip_check(mrc_fused(iq, 1, (int)(nsym + 1), R, C, prefix, w.Hc + frame * (long long)R * C,
+                               w.P + frame * C, F2(d_out), 0, hs(stream)),
+                     fn);
+}
+
 int ofdm_frame_export_estimate(const void *d_ws, size_t ws_bytes_, long long nframes, int S, int R, int C,
                                long long frame, ofdm_cf32 *d_Hconj, float *d_Hsqrd, ofdm_stream_t stream) {
     if (!d_Hconj) return fail(OFDM_E_ARG, "ofdm_frame_export_estimate: null d_Hconj");

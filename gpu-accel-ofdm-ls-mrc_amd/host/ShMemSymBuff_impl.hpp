@@ -192,6 +192,7 @@ class ShMemSymBuff {
             if (streams_[i]) (void)hipStreamDestroy(streams_[i]);
             if (events_[i]) (void)hipEventDestroy(events_[i]);
         }
+        if (io_stream_) (void)hipStreamDestroy(io_stream_);
         if (registered_) (void)hipHostUnregister(buff_);
 #endif
         if (!master_) ofdm_ring::store(&buff_->size, -1);  // tell the writer we left
@@ -274,7 +275,7 @@ class ShMemSymBuff {
     void readNextSymbolCUDA(T *dY, int it) {
         const int r = wait_readable();
         tic();
-        copy_to_device(dY, r, *createStream(it));
+        copy_to_device(dY, r, io_stream());
         toc(readT, it);
         advance_reader(r, /*last=*/false);
     }
@@ -283,7 +284,7 @@ class ShMemSymBuff {
     void readLastSymbolCUDA(T *dY) {
         const int r = wait_readable();
         tic();
-        copy_to_device(dY, r, *createStream(lenOfBuffer - 1));
+        copy_to_device(dY, r, io_stream());
         toc(readT, numberOfSymbolsToTest - 1);
         advance_reader(r, /*last=*/true);
     }
@@ -436,6 +437,14 @@ class ShMemSymBuff {
             hipStreamSynchronize(s) != hipSuccess)
             fail_copy();
     }
+    // The per-symbol readers copy on ONE stream of this object, created once
+    // (the reference creates a stream per symbol index and never destroys it,
+    // ShMemSymBuff_gpu.hpp:375-447; each creation costs far more than the
+    // 512 KiB copy).  createStream / destroyStream stay for callers.
+    hipStream_t io_stream() {
+        if (!io_stream_ && hipStreamCreateWithFlags(&io_stream_, hipStreamNonBlocking) != hipSuccess) fail_copy();
+        return io_stream_;
+    }
     // page-lock the ring once: true async DMA from shm
     void register_ring() {
         if (!registered_)
@@ -448,6 +457,7 @@ class ShMemSymBuff {
     }
     hipStream_t streams_[lenOfBuffer] = {};
     hipEvent_t events_[lenOfBuffer] = {};
+    hipStream_t io_stream_ = nullptr;
     bool registered_ = false;
 #endif
 

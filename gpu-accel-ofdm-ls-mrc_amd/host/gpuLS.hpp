@@ -140,13 +140,36 @@ class gpuLS {
     }
 
     // ---- per-symbol flow (gpuLS.cu:351-473) ------------------------------
-    // Pilot symbol from the ring into dY (host or device staging buffer),
-    // copied to Y (device, rows x cols), FFT'd in place; dH = conj(Y/X),
-    // Hsqrd = |H|^2.
+    // Pilot symbol from the ring into dY (host or device staging buffer);
+    // dH = conj(Y/X) (rows x (cols-1), device), Hsqrd = |H|^2 (cols-1).
+    // C in {1024, 2048, 4096}: ONE fused FFT + LS launch straight from the
+    // staging buffer (prefix skipped in the kernel) into this object's
+    // workspace, then its export into dH / Hsqrd, one sync; the workspace
+    // estimate is kept for demodOneSymbol.  Other C: FFT rows in Y, then LS.
     void firstVector(hipFloatComplex *dY, hipFloatComplex *Y, hipFloatComplex *dH,
                      hipFloatComplex *dX, float *Hsqrd, int rows, int cols, int it) {
-        read_symbol(dY, Y, rows, cols, it, false);
+        int pfx = 0;
+        const hipFloatComplex *src = read_symbol(dY, Y, rows, cols, it, false, fused(cols) ? &pfx : nullptr);
         clock_t t0 = clock();
+        est_H_ = nullptr;
+        est_P_ = nullptr;
+        if (fused(cols)) {
+            const size_t wsb = ofdm_frame_workspace_bytes(1, 2, rows, cols);
+            void *ws = ws1_.get(wsb);
+            ofdm::check(ofdm_frame_estimate(C(src), 1, 2, rows, cols, pfx, C(dX), ws, wsb, nullptr),
+                        "ofdm_frame_estimate");
+            ofdm::check(ofdm_frame_export_estimate(ws, wsb, 1, 2, rows, cols, 0, C(dH), Hsqrd, nullptr),
+                        "ofdm_frame_export_estimate");
+            sync();
+            buffPtr->setFft(0.f, it);  // fused into the LS kernel
+            buffPtr->setDecode(secs(t0), it);
+            est_H_ = dH;
+            est_P_ = Hsqrd;
+            est_rows_ = rows;
+            est_cols_ = cols;
+            est_wsb_ = wsb;
+            return;
+        }
         batchedFFT(Y, rows, cols, nullptr);
         sync();
         buffPtr->setFft(secs(t0), it);
@@ -156,17 +179,34 @@ class gpuLS {
         buffPtr->setDecode(secs(t0), it);
     }
     // Data symbol `it` from the ring; K rotated outputs land in dY[0..K)
-    // (host or device), as gpuLS_main.cu:112-117 expects.
+    // (host or device), as gpuLS_main.cu:112-117 expects.  When Hconj /
+    // Hsqrd are the buffers the last firstVector filled (the reference's
+    // call sequence, gpuLS_main.cu:107-112) and C is fused: ONE fused FFT +
+    // MRC + normalise + rotate launch (ofdm_symbols_demod) on the staging
+    // buffer against the kept estimate, one synchronising copy of the K
+    // outputs.  Otherwise FFT rows in Y, then MRC from Hconj / Hsqrd.
     void demodOneSymbol(hipFloatComplex *dY, hipFloatComplex *Y, hipFloatComplex *Hconj,
                         float *Hsqrd, int rows1, int cols1, int it) {
         const int K = cols1 - 1;
-        read_symbol(dY, Y, rows1, cols1, it, it == numberOfSymbolsToTest - 1);
+        const bool use_est = fused(cols1) && Hconj == est_H_ && Hsqrd == est_P_ && rows1 == est_rows_ &&
+                             cols1 == est_cols_;
+        int pfx = 0;
+        const hipFloatComplex *src = read_symbol(dY, Y, rows1, cols1, it, it == numberOfSymbolsToTest - 1,
+                                                 use_est ? &pfx : nullptr);
         clock_t t0 = clock();
+        auto *out = scratch_.get<ofdm_cf32>((size_t)K * 8);
+        if (use_est) {
+            ofdm::check(ofdm_symbols_demod(C(src), 1, rows1, cols1, pfx, ws1_.p, est_wsb_, 0, out, nullptr),
+                        "ofdm_symbols_demod");
+            ofdm::copy_any(dY, out, (size_t)K * 8);
+            buffPtr->setFft(0.f, it);  // fused into the MRC kernel
+            buffPtr->setDecode(secs(t0), it);
+            return;
+        }
         batchedFFT(Y, rows1, cols1, nullptr);
         sync();
         buffPtr->setFft(secs(t0), it);
         t0 = clock();
-        auto *out = scratch_.get<ofdm_cf32>((size_t)K * 8);
         ofdm::check(ofdm_mrc_demod(C(Y), 1, C(Hconj), Hsqrd, rows1, cols1, out, nullptr), "ofdm_mrc_demod");
         ofdm::copy_any(dY, out, (size_t)K * 8);
         buffPtr->setDecode(secs(t0), it);
@@ -281,16 +321,27 @@ class gpuLS {
     static float secs(clock_t t0) { return (float)(clock() - t0) / (float)CLOCKS_PER_SEC; }
     static void sync() { ofdm::hcheck(hipDeviceSynchronize(), "hipDeviceSynchronize"); }
 
+    static bool fused(int cols) { return cols == 1024 || cols == 2048 || cols == 4096; }
+
     // ring -> staging buffer dY (host: plain read; device: *CUDA read) -> Y;
-    // the cyclic prefix is dropped on the way
-    void read_symbol(hipFloatComplex *dY, hipFloatComplex *Y, int rows, int cols, int it, bool last) {
+    // the cyclic prefix is dropped on the way.  Returns the device symbol to
+    // compute on: with pfx non-null and a device dY, dY itself (no copy to Y;
+    // *pfx = prefix, skipped by the fused kernel), else Y (*pfx = 0).
+    const hipFloatComplex *read_symbol(hipFloatComplex *dY, hipFloatComplex *Y, int rows, int cols, int it,
+                                       bool last, int *pfx = nullptr) {
         const size_t bytes = (size_t)rows * cols * sizeof(hipFloatComplex);
         clock_t t0 = clock();
+        if (pfx) *pfx = 0;
         if (ofdm::is_device_ptr(dY)) {
             if (last)
                 buffPtr->readLastSymbolCUDA(dY);
             else
                 buffPtr->readNextSymbolCUDA(dY, it);
+            if (pfx) {
+                *pfx = prefix;
+                buffPtr->setReadT(secs(t0), it);
+                return dY;
+            }
             if (prefix > 0)
                 ofdm::hcheck(hipMemcpy2D(Y, (size_t)cols * 8, dY + prefix, (size_t)(cols + prefix) * 8,
                                          (size_t)cols * 8, rows, hipMemcpyDeviceToDevice),
@@ -305,9 +356,15 @@ class gpuLS {
             ofdm::copy_any(Y, dY, bytes);
         }
         buffPtr->setReadT(secs(t0), it);
+        return Y;
     }
 
-    ofdm::DevBuf scratch_, scratchP_, ws_;
+    ofdm::DevBuf scratch_, scratchP_, ws_, ws1_;
+    // the estimate firstVector keeps in ws1_ and the buffers it exported to
+    const hipFloatComplex *est_H_ = nullptr;
+    const float *est_P_ = nullptr;
+    int est_rows_ = 0, est_cols_ = 0;
+    size_t est_wsb_ = 0;
 };
 
 #endif  // OFDM_GPULS_HPP_

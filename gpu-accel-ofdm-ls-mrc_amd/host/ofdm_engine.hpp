@@ -35,13 +35,21 @@ struct DevBuf {
     DevBuf() = default;
     DevBuf(const DevBuf &) = delete;
     DevBuf &operator=(const DevBuf &) = delete;
+    // a buffer used as a frame workspace is dropped from the library's
+    // estimate registry before its memory goes back (ofdm_workspace_release)
     ~DevBuf() {
-        if (p) (void)hipFree(p);
+        if (p) {
+            (void)ofdm_workspace_release(p);
+            (void)hipFree(p);
+        }
     }
     template <typename T = void>
     T *get(size_t bytes) {
         if (bytes > n) {
-            if (p) hcheck(hipFree(p), "hipFree");
+            if (p) {
+                (void)ofdm_workspace_release(p);
+                hcheck(hipFree(p), "hipFree");
+            }
             hcheck(hipMalloc(&p, bytes), "hipMalloc");
             n = bytes;
         }

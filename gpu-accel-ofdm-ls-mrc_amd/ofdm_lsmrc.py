@@ -58,6 +58,7 @@ _SIGS = {
     "ofdm_frame_ls_partial": (_I, [_P, _LL, _I, _I, _I, _I, _P, _P, _c.c_size_t, _P, _P]),
     "ofdm_frame_mrc_partial": (_I, [_P, _LL, _I, _I, _I, _I, _P, _c.c_size_t, _P, _P]),
     "ofdm_frame_export_estimate": (_I, [_P, _c.c_size_t, _LL, _I, _I, _I, _LL, _P, _P, _P]),
+    "ofdm_symbols_demod": (_I, [_P, _LL, _I, _I, _I, _P, _c.c_size_t, _LL, _P, _P]),
     "ofdm_synth_frames": (_I, [_P, _LL, _I, _I, _I, _I, _P, _c.c_ulonglong, _LL, _c.c_float,
                                _I, _I, _P]),
     "ofdm_count_symbol_errors": (_I, [_P, _LL, _I, _I, _c.c_ulonglong, _LL, _P, _P]),
@@ -280,6 +281,18 @@ def frame_combine(iq, prefix, ws, out, stream=None):
     _check(lib().ofdm_frame_combine(_dptr(iq), F, S, R, Cp - prefix, prefix, _dptr(ws),
                                     ws.numel(), _dptr(out), _stream(stream)),
            "ofdm_frame_combine")
+    return out
+
+
+def symbols_demod(sym, ws, prefix=0, frame=0, out=None, stream=None):
+    """sym: (nsym, R, C+prefix) time-domain data symbols -> (nsym, K), against
+    frame `frame`'s estimate in ws (filled by frame_estimate)."""
+    n, R, Cp = sym.shape
+    C = Cp - prefix
+    if out is None:
+        out = c64((n, C - 1), sym.device)
+    _check(lib().ofdm_symbols_demod(_dptr(sym), n, R, C, prefix, _dptr(ws), ws.numel(), frame, _dptr(out),
+                                    _stream(stream)), "ofdm_symbols_demod")
     return out
 
 

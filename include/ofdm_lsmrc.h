@@ -183,6 +183,18 @@ int ofdm_frame_combine(const ofdm_cf32 *d_iq, long long nframes, int S, int R, i
 int ofdm_frame_export_estimate(const void *d_ws, size_t ws_bytes, long long nframes, int S, int R, int C,
                                long long frame, ofdm_cf32 *d_Hconj, float *d_Hsqrd, ofdm_stream_t stream);
 
+/* Per-symbol receiver (gpuLS::demodOneSymbol, gpuLS.cu:410-473, which runs
+ * cuFFT + multiplyWithChannelConj + combineForMRC + a CPU shift per symbol):
+ * nsym consecutive time-domain data symbols d_sym (nsym x R x (C + cp_len),
+ * each row's cyclic prefix skipped) demodulated against the LS estimate of
+ * frame `frame` of a workspace filled by ofdm_frame_estimate (any nframes and
+ * S; R, C and ws_bytes must match), in ONE fused launch (FFT + MRC +
+ * normalise + rotate, each row read once) -> d_out (nsym x K).  C in {1024,
+ * 2048, 4096} (else OFDM_E_UNSUPPORTED); a frequency-domain or partial
+ * estimate is refused with OFDM_E_ARG. */
+int ofdm_symbols_demod(const ofdm_cf32 *d_sym, long long nsym, int R, int C, int cp_len, const void *d_ws,
+                       size_t ws_bytes, long long frame, ofdm_cf32 *d_out, ofdm_stream_t stream);
+
 /* ofdm_frame_demod on frequency-domain symbols (FFT done upstream, no prefix):
  * d_Y = nframes x S x R x C.  The LS + MRC of the reference's GPU path on
  * its own (findHs + findDistSqrd, gpuLS.cu:158-209; multiplyWithChannelConj +
