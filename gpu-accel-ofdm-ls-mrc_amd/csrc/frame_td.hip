@@ -33,17 +33,24 @@ namespace ofdm {
 namespace td1024 {
 
 // ---------------------------------------------------------------------------
-// LS: one workgroup (4 waves) per frame; wave w takes antenna rows w, w+4, ...
-// and keeps a partial |H|^2 per bin; partials are added in wave order through
-// LDS (deterministic).  partial != 0: antenna-split mode (DC slot of P = 0).
-// P is written bin-indexed [F][C]; Hc lane-ordered [F][R][8][64] float4.
+// LS: one workgroup (NW waves) per frame; wave w takes antenna rows w, w+NW,
+// ... and keeps a partial |H|^2 per bin; partials are added in wave order
+// through LDS (deterministic; for R <= NW this is findDistSqrd's sequential
+// antenna order, cpuLS.hpp:211-228).  partial != 0: antenna-split mode (DC
+// slot of P = 0).  P is written bin-indexed [F][C]; Hc lane-ordered
+// [F][R][8][64] float4.  NW = 4 for large batches; NW = 16 (one antenna row
+// per wave up to R = 16, 148 KiB of LDS) when the batch has too few frames to
+// fill the GPU with 4-wave workgroups (BASELINE configs[1]: 100 frames x 16
+// antennas -- the frame's rows are transformed side by side instead of four
+// after one another).
 // ---------------------------------------------------------------------------
 constexpr int LS_WAVES = 4;
 
-__global__ void __launch_bounds__(256) k_ls_td1024(const float2 *__restrict__ iq, int S, int R,
-                                                   int prefix, const float2 *__restrict__ X,
-                                                   float2 *__restrict__ Hc, float *__restrict__ P,
-                                                   int partial) {
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) k_ls_td1024(const float2 *__restrict__ iq, int S, int R,
+                                                       int prefix, const float2 *__restrict__ X,
+                                                       float2 *__restrict__ Hc, float *__restrict__ P,
+                                                       int partial) {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     float2 *tw = lds;
     const int w = threadIdx.x >> 6;
@@ -66,7 +73,7 @@ __global__ void __launch_bounds__(256) k_ls_td1024(const float2 *__restrict__ iq
     float p[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) p[k] = 0.f;
-    for (int r = w; r < R; r += LS_WAVES) {
+    for (int r = w; r < R; r += NW) {
         float2 a[16], x[16];
         row_load(pilot + (long long)r * Cp, t, a);
         row_fft(a, t, T, tw, x);
@@ -80,14 +87,16 @@ __global__ void __launch_bounds__(256) k_ls_td1024(const float2 *__restrict__ iq
         hc_store(Hf + (long long)r * (C / 2), t, x);
     }
     __syncthreads();
-    float *pp = reinterpret_cast<float *>(lds + TWBUF);  // [LS_WAVES][C], reuses T
+    float *pp = reinterpret_cast<float *>(lds + TWBUF);  // [NW][C], reuses T
+    static_assert(NW * C * sizeof(float) <= NW * TBUF * sizeof(float2), "partials fit the transpose images");
 #pragma unroll
     for (int k = 0; k < 16; ++k) pp[w * C + b0 + 16 * k] = p[k];
     __syncthreads();
     float *Pf = P + f * C;
+    const int nw = R < NW ? R : NW;  // waves that hold rows
     for (int b = threadIdx.x; b < C; b += blockDim.x) {
         float sum = pp[b];
-        for (int i = 1; i < LS_WAVES; ++i) sum = sum + pp[i * C + b];
+        for (int i = 1; i < nw; ++i) sum = sum + pp[i * C + b];
         Pf[b] = b == 0 ? (partial ? 0.f : 1.f) : sum;
     }
 }
@@ -288,9 +297,20 @@ hipError_t launch_ls_td1024(const float2 *iq, long long nframes, int S, int R, i
     using namespace td1024;
     if (nframes <= 0) return hipSuccess;
     if (nframes > 0x7fffffffll) return hipErrorInvalidValue;
+    // 4-wave workgroups unless they leave the GPU under-filled: fewer than
+    // 2 waves per SIMD (2048 waves) with rows left to spread
+    if (nframes * LS_WAVES < 2048 && R > LS_WAVES) {
+        constexpr int NW = 16;
+        const size_t lds = (TWBUF + NW * TBUF) * sizeof(float2);
+        if (hipError_t e = opt_in_lds(reinterpret_cast<const void *>(k_ls_td1024<NW>), (int)lds); e != hipSuccess)
+            return e;
+        hipLaunchKernelGGL(k_ls_td1024<NW>, dim3((unsigned)nframes), dim3(64 * NW), lds, s, iq, S, R, prefix, X,
+                           Hc, P, partial);
+        return hipGetLastError();
+    }
     const size_t lds = (TWBUF + LS_WAVES * TBUF) * sizeof(float2);
-    hipLaunchKernelGGL(k_ls_td1024, dim3((unsigned)nframes), dim3(64 * LS_WAVES), lds, s, iq, S, R, prefix, X, Hc,
-                       P, partial);
+    hipLaunchKernelGGL(k_ls_td1024<LS_WAVES>, dim3((unsigned)nframes), dim3(64 * LS_WAVES), lds, s, iq, S, R,
+                       prefix, X, Hc, P, partial);
     return hipGetLastError();
 }
 

@@ -20,4 +20,5 @@ run bench && run bench_split --no-cpu --mode split --steps 10 && \
 run bench_cfg1 --no-cpu --no-mode-a --R 16 --frames 100 && \
 run bench_c4096 --no-cpu --steps 10 --R 32 --C 4096 --frames 400
 [ $? -eq 0 ] || exit 1
-timeout -k 10 300 bash scripts/ring_bench.sh 20 > $OUT/ring.log 2>&1; rc=$?; cat $OUT/ring.log | tail -5; exit $rc
+timeout -k 10 300 bash scripts/ring_bench.sh 20 > $OUT/ring.log 2>&1; rc=$?; tail -5 $OUT/ring.log; [ $rc -eq 0 ] || exit $rc
+if [ -x scripts/wrprobe ]; then timeout -k 10 120 scripts/wrprobe > $OUT/wrprobe.txt 2>&1; rc=$?; cat $OUT/wrprobe.txt; exit $rc; fi
