@@ -218,7 +218,7 @@ __device__ __forceinline__ void dma_hc_row(const float2 *g, unsigned lds) {
 // after this row's first barrier.  HP = 2 (A/B candidate): ONE Hc buffer,
 // refilled after a third barrier once every wave has read both planes of this
 // row (before its second FFT) and published at the next row's second barrier.
-template <int E, int PK, bool PREF, int DBG = 0, int TW = 3, int HP = 4>
+template <int E, int PK, bool PREF, int DBG = 0, int TW = 3, int HP = 4, int HE = 0>
 __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const float2 *__restrict__ hr,
                                       int t, float2 *T, const float2 *Tp, const float2 *tw1,
                                       const float2 *tw2, pk::v2f wb0, pk::v2f wb1, float2 (&a)[16],
@@ -289,14 +289,32 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
 #pragma unroll
     for (int m = 0; m < 16; ++m) z[m] = F(u[m]);
     hl::row_fft_a<PK, (TW & 1) != 0>(z, t, T, tw1);
+    if constexpr (HE == 1) {
+        // plane 0 of this row's Hc issued before the second FFT stage (all 8
+        // LDS reads in flight behind the transpose reads, landed by the MAC)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) h[k] = hr[k * 64 + t];
+        __builtin_amdgcn_sched_barrier(0);
+    }
     hl::row_fft_b<PK, (TW & 2) != 0>(t, T, tw2, x);
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (HE == 0) {
 #pragma unroll
-    for (int k = 0; k < 16; ++k) h[k] = hr[k * 64 + t];  // plane 0: bins 4 b + E, from LDS
+        for (int k = 0; k < 16; ++k) h[k] = hr[k * 64 + t];  // plane 0: bins 4 b + E, from LDS
 #pragma unroll
-    for (int k = 0; k < 16; ++k) h1[k] = hr[1024 + k * 64 + t];  // plane 1: bins 4 b + 2 + E
+        for (int k = 0; k < 16; ++k) h1[k] = hr[1024 + k * 64 + t];  // plane 1: bins 4 b + 2 + E
+    } else if constexpr (HE == 2) {
+        // plane 0 issued as one burst (no reuse of a read register), then the MAC
+#pragma unroll
+        for (int k = 0; k < 16; ++k) h[k] = hr[k * 64 + t];
+        __builtin_amdgcn_sched_barrier(0);
+    }
     mac(ae);
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (HE != 0) {  // plane 1 read after the first MAC, consumed after the second FFT
+#pragma unroll
+        for (int k = 0; k < 16; ++k) h1[k] = hr[1024 + k * 64 + t];
+    }
     if (HP != 4 && PREF) {  // every wave holds both planes of this row: refill the single buffer
         td1024::lds_barrier();
         if (!(DBG & 2) && hnext) dma_hc_row<2 * HP>(hnext, hb_next);
@@ -333,7 +351,7 @@ constexpr size_t H_LDS = h_lds(H_PAIRS);
 static_assert(H_LDS <= 160 * 1024, "one workgroup per CU");
 static_assert(2 * h_lds(2) <= 160 * 1024, "two 2-pair workgroups per CU");
 
-template <int E, int PK, int DBG = 0, int TW = 3, int HP = 4>
+template <int E, int PK, int DBG = 0, int TW = 3, int HP = 4, int HE = 0>
 __device__ __forceinline__ void h_rows(const float2 *sym, int Cp, int R, const float2 *Hg, float2 *HB, int t,
                                        float2 *T, const float2 *Tp, const float2 *tw1, const float2 *tw2,
                                        pk::v2f wb0, pk::v2f wb1, float2 (&ae)[16], float2 (&ao)[16]) {
@@ -360,16 +378,16 @@ __device__ __forceinline__ void h_rows(const float2 *sym, int Cp, int R, const f
     const unsigned hb0 = lds_addr(HB), hb1 = lds_addr(HB + C);
     constexpr int NB = HP == 4 ? 2 : 1;  // Hc buffers
     for (int r = 0; r + 1 < R; ++r)
-        x_row<E, PK, true, DBG, TW, HP>(sym + (long long)(r + 1) * Cp, HB + (NB == 2 ? (r & 1) * C : 0) + E * 2048,
+        x_row<E, PK, true, DBG, TW, HP, HE>(sym + (long long)(r + 1) * Cp, HB + (NB == 2 ? (r & 1) * C : 0) + E * 2048,
                                         t, T, Tp, tw1, tw2, wb0, wb1, a, b, ae, ao, Hg + (long long)(r + 1) * C,
                                         NB == 2 && !(r & 1) ? hb1 : hb0);
-    x_row<E, PK, false, DBG, TW, HP>(sym, HB + (NB == 2 ? ((R - 1) & 1) * C : 0) + E * 2048, t, T, Tp, tw1, tw2,
+    x_row<E, PK, false, DBG, TW, HP, HE>(sym, HB + (NB == 2 ? ((R - 1) & 1) * C : 0) + E * 2048, t, T, Tp, tw1, tw2,
                                      wb0, wb1, a, b, ae, ao, nullptr, 0);
 }
 
 constexpr int H_PK = 7;  // packed-f32 split, FFT halves and MAC (pk.hpp)
 
-template <int DBG = 0, int TW = 3, int HP = H_PAIRS>
+template <int DBG = 0, int TW = 3, int HP = H_PAIRS, int HE = 0>
 __global__ void __attribute__((amdgpu_flat_work_group_size(128 * HP, 128 * HP), amdgpu_waves_per_eu(2, 2)))
 k_mrc_td4096h(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
               const float *__restrict__ P, float2 *__restrict__ out, long long nframes, long long nblocks,
@@ -403,9 +421,9 @@ k_mrc_td4096h(const float2 *__restrict__ iq, int S, int R, int prefix, const flo
 #pragma unroll
     for (int k = 0; k < 16; ++k) ae[k] = ao[k] = float2{0.f, 0.f};
     if (e)
-        h_rows<1, H_PK, DBG, TW, HP>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
+        h_rows<1, H_PK, DBG, TW, HP, HE>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
     else
-        h_rows<0, H_PK, DBG, TW, HP>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
+        h_rows<0, H_PK, DBG, TW, HP, HE>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
     const long long q = f * nsym + j;
     const int b0 = lane_bin0(t);
     float2 *o = out + q * K;
@@ -520,6 +538,11 @@ hipError_t launch_mrc_td4096(const float2 *iq, long long nframes, int S, int R, 
         default: break;
     }
     if (ab_knob("MRC4K_TW", 3) == 0) kern = k_mrc_td4096h<0, 0>;  // table twiddles (round 1)
+    switch (ab_knob("MRC4K_HE", 0)) {  // when this row's Hc planes are read from LDS (x_row)
+        case 1: kern = k_mrc_td4096h<0, 3, H_PAIRS, 1>; break;
+        case 2: kern = k_mrc_td4096h<0, 3, H_PAIRS, 2>; break;
+        default: break;
+    }
     if (ab_knob("MRC4K_HP", 4) == 2) {  // two independent 2-pair workgroups per CU, single Hc buffer
         const long long bpf2 = ((S - 1) + 1) / 2, nb2 = nframes * bpf2, px2 = (nb2 + 7) / 8;
         if (px2 * 8 > 0x7fffffffll) return hipErrorInvalidValue;

@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
 # Round 3 GPU session: parity suite + smoke, then bench lines.
-# usage: bash scripts/gpu_r3.sh <tag> [bench-set]
+# usage: [AB="ab.py args"] bash scripts/gpu_r3.sh <tag> [bench-set]
 #   bench-set: "base" (default: headline + split + configs[1] + C=4096) or "none"
 set -o pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -21,4 +21,7 @@ run bench_cfg1 --no-cpu --no-mode-a --R 16 --frames 100 && \
 run bench_c4096 --no-cpu --steps 10 --R 32 --C 4096 --frames 400
 [ $? -eq 0 ] || exit 1
 timeout -k 10 300 bash scripts/ring_bench.sh 20 > $OUT/ring.log 2>&1; rc=$?; tail -5 $OUT/ring.log; [ $rc -eq 0 ] || exit $rc
-if [ -x scripts/wrprobe ]; then timeout -k 10 120 scripts/wrprobe > $OUT/wrprobe.txt 2>&1; rc=$?; cat $OUT/wrprobe.txt; exit $rc; fi
+if [ -x scripts/wrprobe ]; then timeout -k 10 120 scripts/wrprobe > $OUT/wrprobe.txt 2>&1 || exit 1; cat $OUT/wrprobe.txt; fi
+if [ -n "$AB" ]; then
+  timeout -k 10 400 python -u scripts/ab.py $AB > $OUT/ab.jsonl 2> $OUT/ab.err; rc=$?; cat $OUT/ab.jsonl; exit $rc
+fi

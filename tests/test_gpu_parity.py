@@ -421,9 +421,11 @@ def test_mrc_partial_refuses_frequency_domain_estimate(ofdm, dev, C):
 def test_symbols_demod_matches_frame_combine(ofdm, dev, C, prefix):
     """ofdm_symbols_demod (the fused per-symbol receiver behind
     gpuLS::demodOneSymbol): data symbols taken out of their frame and
-    demodulated against that frame's kept estimate equal ofdm_frame_combine's
-    output for them, bit for bit (same kernel, same estimate); a frame index
-    outside the workspace and a frequency-domain estimate are refused."""
+    demodulated against that frame's kept estimate match ofdm_frame_combine's
+    output for them (same kernels and estimate; within rounding, not bit for
+    bit: at C = 1024 a workgroup whose 8 symbols straddle two frames reads Hc
+    per wave from L2, a code path the compiler contracts differently); a frame
+    index outside the workspace and a frequency-domain estimate are refused."""
     F, S, R = 3, 6, 8
     X = to_dev(qpsk_pilots(C - 1), dev)
     iq = ofdm.synth_frames(F, S, R, C, X, prefix=prefix, seed=31, noise_std=0.02)
@@ -432,9 +434,9 @@ def test_symbols_demod_matches_frame_combine(ofdm, dev, C, prefix):
     ref = host(ofdm.frame_combine(iq, prefix, ws, ofdm.c64((F, S - 1, C - 1), dev)))
     for f in (0, F - 1):
         got = host(ofdm.symbols_demod(iq[f, 1:].contiguous(), ws, prefix, frame=f))
-        assert (got == ref[f]).all()
+        parity(got, ref[f], rtol=1e-6)
         one = host(ofdm.symbols_demod(iq[f, 2:3].contiguous(), ws, prefix, frame=f))
-        assert (one == ref[f, 1:2]).all()
+        parity(one, ref[f, 1:2], rtol=1e-6)
     with pytest.raises(ofdm.OfdmError, match="outside"):
         ofdm.symbols_demod(iq[0, 1:].contiguous(), ws, prefix, frame=F)
     Y = ofdm.synth_frames(1, S, R, C, X, seed=8, noise_std=0.05, freq_domain=True)
