@@ -220,9 +220,11 @@ def main():
 
     stream = torch.cuda.current_stream()
 
+    # Two HIP events per step on the launch stream: after the estimate (LS)
+    # and after the combine (MRC).  The LS of step i is timed from step i-1's
+    # end event (one event before the loop for i = 0), so no event sits
+    # between two steps' kernels beyond the one the MRC timing needs.
     def step(evs=None):
-        if evs:
-            evs[0].record(stream)
         if freq:
             ofdm.frame_estimate_freq(iq, X, ws, stream)
         else:
@@ -241,10 +243,14 @@ def main():
     torch.cuda.synchronize()
     errs = int(ofdm.count_symbol_errors(out, S, seed=args.seed, frame0=rank * F).item())
 
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    events = [[None] + [torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.steps)]
+    ev0 = torch.cuda.Event(enable_timing=True)
+    for i in range(args.steps):
+        events[i][0] = ev0 if i == 0 else events[i - 1][2]
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ev0.record(stream)
     for i in range(args.steps):
         step(events[i])
     torch.cuda.synchronize()

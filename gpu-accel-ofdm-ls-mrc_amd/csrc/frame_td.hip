@@ -46,7 +46,9 @@ namespace td1024 {
 // ---------------------------------------------------------------------------
 constexpr int LS_WAVES = 4;
 
-template <int NW>
+// DBG (A/B build only, wrong results by design): 1 return after the twiddle
+// fill, 2 no FFT (the loaded row is used as its transform), 4 no P combine.
+template <int NW, int DBG = 0>
 __global__ void __launch_bounds__(64 * NW) k_ls_td1024(const float2 *__restrict__ iq, int S, int R,
                                                        int prefix, const float2 *__restrict__ X,
                                                        float2 *__restrict__ Hc, float *__restrict__ P,
@@ -58,6 +60,7 @@ __global__ void __launch_bounds__(64 * NW) k_ls_td1024(const float2 *__restrict_
     float2 *T = lds + TWBUF + w * TBUF;
     fill_twiddles(tw);
     __syncthreads();
+    if constexpr ((DBG & 1) != 0) return;
 
     const long long f = blockIdx.x;
     const int Cp = C + prefix;
@@ -76,7 +79,12 @@ __global__ void __launch_bounds__(64 * NW) k_ls_td1024(const float2 *__restrict_
     for (int r = w; r < R; r += NW) {
         float2 a[16], x[16];
         row_load(pilot + (long long)r * Cp, t, a);
-        row_fft(a, t, T, tw, x);
+        if constexpr ((DBG & 2) != 0) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) x[k] = a[k];
+        } else {
+            row_fft(a, t, T, tw, x);
+        }
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             float2 h = ls_conj(x[k], xp[k]);
@@ -85,6 +93,13 @@ __global__ void __launch_bounds__(64 * NW) k_ls_td1024(const float2 *__restrict_
             p[k] = p[k] + (h.x * h.x) + (h.y * h.y);
         }
         hc_store(Hf + (long long)r * (C / 2), t, x);
+    }
+    if constexpr ((DBG & 4) != 0) {
+        if (w == 0) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) P[f * C + b0 + 16 * k] = p[k];
+        }
+        return;
     }
     __syncthreads();
     float *pp = reinterpret_cast<float *>(lds + TWBUF);  // [NW][C], reuses T
@@ -299,18 +314,32 @@ hipError_t launch_ls_td1024(const float2 *iq, long long nframes, int S, int R, i
     if (nframes > 0x7fffffffll) return hipErrorInvalidValue;
     // 4-wave workgroups unless they leave the GPU under-filled: fewer than
     // 2 waves per SIMD (2048 waves) with rows left to spread
-    if (nframes * LS_WAVES < 2048 && R > LS_WAVES) {
-        constexpr int NW = 16;
-        const size_t lds = (TWBUF + NW * TBUF) * sizeof(float2);
-        if (hipError_t e = opt_in_lds(reinterpret_cast<const void *>(k_ls_td1024<NW>), (int)lds); e != hipSuccess)
-            return e;
-        hipLaunchKernelGGL(k_ls_td1024<NW>, dim3((unsigned)nframes), dim3(64 * NW), lds, s, iq, S, R, prefix, X,
-                           Hc, P, partial);
+    int nw = (nframes * LS_WAVES < 2048 && R > LS_WAVES) ? 16 : LS_WAVES;
+    auto k16 = k_ls_td1024<16>;
+    auto k4 = k_ls_td1024<LS_WAVES>;
+    auto k8 = k16;  // 8-wave workgroups: A/B build only
+#ifdef OFDM_AB_KNOBS
+    k8 = k_ls_td1024<8>;
+    nw = ab_knob("LS1K_NW", nw);
+    switch (ab_knob("LS1K_DBG", 0)) {
+        case 1: k16 = k_ls_td1024<16, 1>; k8 = k_ls_td1024<8, 1>; k4 = k_ls_td1024<4, 1>; break;
+        case 2: k16 = k_ls_td1024<16, 2>; k8 = k_ls_td1024<8, 2>; k4 = k_ls_td1024<4, 2>; break;
+        case 4: k16 = k_ls_td1024<16, 4>; k8 = k_ls_td1024<8, 4>; k4 = k_ls_td1024<4, 4>; break;
+        case 6: k16 = k_ls_td1024<16, 6>; k8 = k_ls_td1024<8, 6>; k4 = k_ls_td1024<4, 6>; break;
+        default: break;
+    }
+#endif
+    if (nw == 16 || nw == 8) {
+        auto kern = nw == 16 ? k16 : k8;
+        const size_t lds = (TWBUF + nw * TBUF) * sizeof(float2);
+        if (hipError_t e = opt_in_lds(reinterpret_cast<const void *>(kern), (int)lds); e != hipSuccess) return e;
+        hipLaunchKernelGGL(kern, dim3((unsigned)nframes), dim3(64 * nw), lds, s, iq, S, R, prefix, X, Hc, P,
+                           partial);
         return hipGetLastError();
     }
     const size_t lds = (TWBUF + LS_WAVES * TBUF) * sizeof(float2);
-    hipLaunchKernelGGL(k_ls_td1024<LS_WAVES>, dim3((unsigned)nframes), dim3(64 * LS_WAVES), lds, s, iq, S, R,
-                       prefix, X, Hc, P, partial);
+    hipLaunchKernelGGL(k4, dim3((unsigned)nframes), dim3(64 * LS_WAVES), lds, s, iq, S, R, prefix, X, Hc, P,
+                       partial);
     return hipGetLastError();
 }
 
