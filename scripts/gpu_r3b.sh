@@ -9,4 +9,4 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$OUT/cfg1_trace" -o run \
   -- python3 "$ROOT/bench.py" --steps 10 --warmup 2 --no-cpu --no-mode-a --R 16 --frames 100 \
   > "$ROOT/$OUT/cfg1_trace.json" 2> "$ROOT/$OUT/cfg1_trace.err" || exit 1
-cd "$ROOT"; f=$(ls $OUT/cfg1_trace/*/run_kernel_stats.csv 2>/dev/null | head -1); [ -n "$f" ] && cut -d, -f1-8 "$f" | head -12
+echo "trace done"

@@ -54,6 +54,36 @@ __global__ void __launch_bounds__(256) k_flat(const float2 *__restrict__ in, flo
     }
 }
 
+// column pieces of 2 * 64 * WK subcarriers with 16-B stores (2 subcarriers per
+// lane): WK = 1: each wave a 1 KiB piece of a row, the 4 waves over the rows;
+// WK = 4: the 4 waves side by side, a 4 KiB piece per row, rows in sequence.
+// (Odd rows start 8 B off a 16-B boundary: those stores are misaligned.)
+template <int WK>
+__global__ void __launch_bounds__(256) k_col16(const float2 *__restrict__ in, float2 *__restrict__ out, int U, int R,
+                                               int K, long long nsym) {
+    constexpr int PK = 128 * WK;  // subcarriers per piece
+    const int nkb = (K + PK - 1) / PK;
+    const long long q = blockIdx.x / nkb;
+    const int kb = blockIdx.x % nkb, w = threadIdx.x >> 6, t = threadIdx.x & 63;
+    if (q >= nsym) return;
+    const int k = kb * PK + (WK == 4 ? 128 * w : 0) + 2 * t;
+    if (k >= K) return;
+    const float2 *x = in + q * (long long)U * K + k;
+    float2 *y = out + q * (long long)R * K + k;
+    const bool pair = k + 1 < K;
+    for (int r = (WK == 4 ? 0 : w); r < R; r += (WK == 4 ? 1 : 4)) {
+        const float2 *xr = x + (long long)(r % U) * K;
+        const float2 a = xr[0], b = pair ? xr[1] : float2{0.f, 0.f};
+        if (pair) {
+            f4v v = {a.x, a.y, b.x, b.y};
+            __builtin_nontemporal_store(v, reinterpret_cast<f4v *>(y + (long long)r * K));
+        } else {
+            __builtin_nontemporal_store(__builtin_bit_cast(unsigned long long, a),
+                                        reinterpret_cast<unsigned long long *>(y + (long long)r * K));
+        }
+    }
+}
+
 template <typename F>
 static double timed(F launch) {
     hipEvent_t a, b;
@@ -76,11 +106,15 @@ int main() {
     if (hipMalloc(&in, (size_t)nsym * 32 * 1024 * 8) != hipSuccess) return 1;
     if (hipMalloc(&out, (size_t)nsym * R * 1024 * 8) != hipSuccess) return 1;
     (void)hipMemset(in, 0, (size_t)nsym * 32 * 1024 * 8);
-    for (int U : {8, 16, 32}) {
+    for (int U : {8, 16}) {  // k_col keeps U <= 16 rows in registers
         double ms = timed([&] { k_col<1023><<<(unsigned)(nsym * 16), 256>>>(in, out, U, R, nsym); });
         printf("U=%2d col stripes K=1023: %.3f ms %6.0f GB/s\n", U, ms, (double)(U + R) * 1023 * 8 * nsym / (ms * 1e-3) / 1e9);
         ms = timed([&] { k_col<1024><<<(unsigned)(nsym * 16), 256>>>(in, out, U, R, nsym); });
         printf("U=%2d col stripes K=1024: %.3f ms %6.0f GB/s\n", U, ms, (double)(U + R) * 1024 * 8 * nsym / (ms * 1e-3) / 1e9);
+        ms = timed([&] { k_col16<1><<<(unsigned)(nsym * 8), 256>>>(in, out, U, R, 1023, nsym); });
+        printf("U=%2d col 1 KiB 16B K=1023: %.3f ms %6.0f GB/s\n", U, ms, (double)(U + R) * 1023 * 8 * nsym / (ms * 1e-3) / 1e9);
+        ms = timed([&] { k_col16<4><<<(unsigned)(nsym * 2), 256>>>(in, out, U, R, 1023, nsym); });
+        printf("U=%2d col 4 KiB 16B K=1023: %.3f ms %6.0f GB/s\n", U, ms, (double)(U + R) * 1023 * 8 * nsym / (ms * 1e-3) / 1e9);
         ms = timed([&] { k_flat<<<(unsigned)(nsym * 8), 256>>>(in, out, U, R, 1023, nsym); });
         printf("U=%2d flat 16B     K=1023: %.3f ms %6.0f GB/s\n", U, ms, (double)(U + R) * 1023 * 8 * nsym / (ms * 1e-3) / 1e9);
     }
