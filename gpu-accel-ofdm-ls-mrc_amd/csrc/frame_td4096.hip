@@ -196,6 +196,37 @@ __device__ __forceinline__ void dma_hc_row(const float2 *g, unsigned lds) {
     for (int j = 0; j < 32 / NW; ++j) dma16(src + j * NW * 1024, lds + j * NW * 1024 + w * 1024);
 }
 
+// The two FFT1024 stages of hlds::row_fft_a / row_fft_b (PK = 3, TW = 3:
+// packed butterflies, twiddles by recurrence) split at the transpose, so that
+// x_row's IL variant can put one transform's compute between the other's
+// LDS write and read (A/B build only).
+// w1 = W1024^t (tw1[t]) and gw = g(a) W64^a (tw2[4 + a]) are per-lane row
+// invariants, read from LDS once per kernel: an LDS read inside the pipeline
+// would make every later wait on it a wait for the whole transpose in flight.
+__device__ __forceinline__ void fa_compute(pk::v2f (&v)[16], pk::v2f w1) {
+    pk::fft_reg<16>(v);
+    hl::tw_powers(v, w1, w1);
+}
+__device__ __forceinline__ void fa_write(const pk::v2f (&v)[16], int t, float2 *T) {
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2) T[hl::swz(k2, t)] = pk::F(v[k2]);
+}
+__device__ __forceinline__ void fb_read(int t, const float2 *T, pk::v2f (&v)[16]) {
+    const int q = t >> 2, qa = t & 3;
+#pragma unroll
+    for (int l = 0; l < 16; ++l) v[l] = pk::V(T[hl::swz(q, qa + 4 * l)]);
+}
+__device__ __forceinline__ void fb_compute(pk::v2f (&v)[16], pk::v2f gw, int t, float2 (&x)[16]) {
+    const int qa = t & 3;
+    const float g = td1024::quad_g(qa);
+    pk::fft_reg<16>(v);
+    v[0] = pk::scale(v[0], g);
+    hl::tw_powers(v, pk::scale(gw, g), gw);
+#pragma unroll
+    for (int m = 0; m < 16; ++m) x[m] = pk::F(v[m]);
+    td1024::quad_dft(x, qa);
+}
+
 // One antenna row for wave E of the pair.  On entry a/b hold the row's
 // quarters E and E + 2; with PREF the next row's quarters are loaded into
 // them after the first FFT and stay in flight through the second FFT and
@@ -218,12 +249,12 @@ __device__ __forceinline__ void dma_hc_row(const float2 *g, unsigned lds) {
 // after this row's first barrier.  HP = 2 (A/B candidate): ONE Hc buffer,
 // refilled after a third barrier once every wave has read both planes of this
 // row (before its second FFT) and published at the next row's second barrier.
-template <int E, int PK, bool PREF, int DBG = 0, int TW = 3, int HP = 4, int HE = 0>
+template <int E, int PK, bool PREF, int DBG = 0, int TW = 3, int HP = 4, int HE = 0, int IL = 0>
 __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const float2 *__restrict__ hr,
                                       int t, float2 *T, const float2 *Tp, const float2 *tw1,
                                       const float2 *tw2, pk::v2f wb0, pk::v2f wb1, float2 (&a)[16],
                                       float2 (&b)[16], float2 (&ae)[16], float2 (&ao)[16],
-                                      const float2 *hnext, unsigned hb_next) {
+                                      const float2 *hnext, unsigned hb_next, pk::v2f w1 = {}, pk::v2f gw = {}) {
     using namespace pk;
     v2f u[16], v[16];
 #pragma unroll
@@ -272,6 +303,50 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
     OFDM_TWM(14) OFDM_TWM(15)
 #undef OFDM_TWM
     float2 z[16], x[16];
+    if constexpr (IL != 0) {
+        static_assert(PK == 7 && TW == 3 && HP == 4, "the interleaved row uses the packed, recurrence-twiddle FFT");
+        // Both FFT1024s of the row software-pipelined through the one
+        // transpose image: A(u) -> write(u) -> read(u) issued -> A(v) computed
+        // while u's transpose is in flight -> write(v), read(v) issued (LDS
+        // ops of a wave complete in order, so v's writes follow u's reads) ->
+        // B(u) and MAC(u) while v's transpose is in flight -> next row's
+        // loads -> B(v), MAC(v).
+        v2f xu[16];
+        fa_compute(u, w1);
+        fa_write(u, t, T);
+        fb_read(t, T, xu);
+        fa_compute(v, w1);
+        fa_write(v, t, T);
+        fb_read(t, T, u);  // u's registers are free: v's transpose lands in them
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) h[k] = hr[k * 64 + t];  // plane 0, lands during B(u)
+        __builtin_amdgcn_sched_barrier(0);
+        fb_compute(xu, gw, t, x);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {  // matrixMultThenSum (cpuLS.hpp:191-206), packed as the default path
+            v2f a0 = V(ae[k]);
+            pk::mac(a0, V(x[k]), V(h[k]));
+            ae[k] = F(a0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) h[k] = hr[1024 + k * 64 + t];  // plane 1, lands during B(v)
+        __builtin_amdgcn_sched_barrier(0);
+        if (PREF && !(DBG & 64)) {
+            row_load<true>(next + 1024 * E, t, a);
+            row_load<true>(next + 1024 * (E + 2), t, b);
+        }
+        fb_compute(u, gw, t, x);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            v2f a0 = V(ao[k]);
+            pk::mac(a0, V(x[k]), V(h[k]));
+            ao[k] = F(a0);
+        }
+        (void)h1;
+        return;
+    }
     // matrixMultThenSum (cpuLS.hpp:203-204), antennas in order, per bin set
     auto mac = [&](float2 (&acc)[16]) {
 #pragma unroll
@@ -351,7 +426,7 @@ constexpr size_t H_LDS = h_lds(H_PAIRS);
 static_assert(H_LDS <= 160 * 1024, "one workgroup per CU");
 static_assert(2 * h_lds(2) <= 160 * 1024, "two 2-pair workgroups per CU");
 
-template <int E, int PK, int DBG = 0, int TW = 3, int HP = 4, int HE = 0>
+template <int E, int PK, int DBG = 0, int TW = 3, int HP = 4, int HE = 0, int IL = 0>
 __device__ __forceinline__ void h_rows(const float2 *sym, int Cp, int R, const float2 *Hg, float2 *HB, int t,
                                        float2 *T, const float2 *Tp, const float2 *tw1, const float2 *tw2,
                                        pk::v2f wb0, pk::v2f wb1, float2 (&ae)[16], float2 (&ao)[16]) {
@@ -377,17 +452,22 @@ __device__ __forceinline__ void h_rows(const float2 *sym, int Cp, int R, const f
     }
     const unsigned hb0 = lds_addr(HB), hb1 = lds_addr(HB + C);
     constexpr int NB = HP == 4 ? 2 : 1;  // Hc buffers
+    pk::v2f w1 = {}, gw = {};
+    if constexpr (IL != 0) {  // the FFT twiddle bases, loop-invariant (see fa_compute)
+        w1 = pk::V(tw1[t]);
+        gw = pk::V(tw2[4 + (t & 3)]);
+    }
     for (int r = 0; r + 1 < R; ++r)
-        x_row<E, PK, true, DBG, TW, HP, HE>(sym + (long long)(r + 1) * Cp, HB + (NB == 2 ? (r & 1) * C : 0) + E * 2048,
+        x_row<E, PK, true, DBG, TW, HP, HE, IL>(sym + (long long)(r + 1) * Cp, HB + (NB == 2 ? (r & 1) * C : 0) + E * 2048,
                                         t, T, Tp, tw1, tw2, wb0, wb1, a, b, ae, ao, Hg + (long long)(r + 1) * C,
-                                        NB == 2 && !(r & 1) ? hb1 : hb0);
-    x_row<E, PK, false, DBG, TW, HP, HE>(sym, HB + (NB == 2 ? ((R - 1) & 1) * C : 0) + E * 2048, t, T, Tp, tw1, tw2,
-                                     wb0, wb1, a, b, ae, ao, nullptr, 0);
+                                        NB == 2 && !(r & 1) ? hb1 : hb0, w1, gw);
+    x_row<E, PK, false, DBG, TW, HP, HE, IL>(sym, HB + (NB == 2 ? ((R - 1) & 1) * C : 0) + E * 2048, t, T, Tp, tw1, tw2,
+                                     wb0, wb1, a, b, ae, ao, nullptr, 0, w1, gw);
 }
 
 constexpr int H_PK = 7;  // packed-f32 split, FFT halves and MAC (pk.hpp)
 
-template <int DBG = 0, int TW = 3, int HP = H_PAIRS, int HE = 0>
+template <int DBG = 0, int TW = 3, int HP = H_PAIRS, int HE = 0, int IL = 0>
 __global__ void __attribute__((amdgpu_flat_work_group_size(128 * HP, 128 * HP), amdgpu_waves_per_eu(2, 2)))
 k_mrc_td4096h(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
               const float *__restrict__ P, float2 *__restrict__ out, long long nframes, long long nblocks,
@@ -421,9 +501,9 @@ k_mrc_td4096h(const float2 *__restrict__ iq, int S, int R, int prefix, const flo
 #pragma unroll
     for (int k = 0; k < 16; ++k) ae[k] = ao[k] = float2{0.f, 0.f};
     if (e)
-        h_rows<1, H_PK, DBG, TW, HP, HE>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
+        h_rows<1, H_PK, DBG, TW, HP, HE, IL>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
     else
-        h_rows<0, H_PK, DBG, TW, HP, HE>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
+        h_rows<0, H_PK, DBG, TW, HP, HE, IL>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
     const long long q = f * nsym + j;
     const int b0 = lane_bin0(t);
     float2 *o = out + q * K;
@@ -543,6 +623,8 @@ hipError_t launch_mrc_td4096(const float2 *iq, long long nframes, int S, int R, 
         case 2: kern = k_mrc_td4096h<0, 3, H_PAIRS, 2>; break;
         default: break;
     }
+    if (ab_knob("MRC4K_IL", 0) == 1) kern = k_mrc_td4096h<0, 3, H_PAIRS, 0, 1>;  // FFTs software-pipelined
+    if (ab_knob("MRC4K_IL", 0) == 65) kern = k_mrc_td4096h<64, 3, H_PAIRS, 0, 1>;  // + compute only (diag)
     if (ab_knob("MRC4K_HP", 4) == 2) {  // two independent 2-pair workgroups per CU, single Hc buffer
         const long long bpf2 = ((S - 1) + 1) / 2, nb2 = nframes * bpf2, px2 = (nb2 + 7) / 8;
         if (px2 * 8 > 0x7fffffffll) return hipErrorInvalidValue;
