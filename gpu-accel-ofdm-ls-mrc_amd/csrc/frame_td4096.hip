@@ -312,6 +312,9 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
         // B(u) and MAC(u) while v's transpose is in flight -> next row's
         // loads -> B(v), MAC(v).
         v2f xu[16];
+        if constexpr (IL == 3) {  // first quarter of the next row in flight through both transforms
+            if (PREF && !(DBG & 64)) row_load<true>(next + 1024 * E, t, a);
+        }
         fa_compute(u, w1);
         fa_write(u, t, T);
         fb_read(t, T, xu);
@@ -334,7 +337,7 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
         for (int k = 0; k < 16; ++k) h[k] = hr[1024 + k * 64 + t];  // plane 1, lands during B(v)
         __builtin_amdgcn_sched_barrier(0);
         if (PREF && !(DBG & 64)) {
-            row_load<true>(next + 1024 * E, t, a);
+            if (IL == 1) row_load<true>(next + 1024 * E, t, a);
             row_load<true>(next + 1024 * (E + 2), t, b);
         }
         fb_compute(u, gw, t, x);
@@ -624,6 +627,7 @@ hipError_t launch_mrc_td4096(const float2 *iq, long long nframes, int S, int R, 
         default: break;
     }
     if (ab_knob("MRC4K_IL", 0) == 1) kern = k_mrc_td4096h<0, 3, H_PAIRS, 0, 1>;  // FFTs software-pipelined
+    if (ab_knob("MRC4K_IL", 0) == 3) kern = k_mrc_td4096h<0, 3, H_PAIRS, 0, 3>;  // + a quarter at row start
     if (ab_knob("MRC4K_IL", 0) == 65) kern = k_mrc_td4096h<64, 3, H_PAIRS, 0, 1>;  // + compute only (diag)
     if (ab_knob("MRC4K_HP", 4) == 2) {  // two independent 2-pair workgroups per CU, single Hc buffer
         const long long bpf2 = ((S - 1) + 1) / 2, nb2 = nframes * bpf2, px2 = (nb2 + 7) / 8;
