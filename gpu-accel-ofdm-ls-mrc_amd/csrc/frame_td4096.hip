@@ -312,7 +312,7 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
         // B(u) and MAC(u) while v's transpose is in flight -> next row's
         // loads -> B(v), MAC(v).
         v2f xu[16];
-        if constexpr (IL == 3) {  // first quarter of the next row in flight through both transforms
+        if constexpr (IL >= 3) {  // first quarter of the next row in flight through both transforms
             if (PREF && !(DBG & 64)) row_load<true>(next + 1024 * E, t, a);
         }
         fa_compute(u, w1);
@@ -606,8 +606,13 @@ hipError_t launch_mrc_td4096(const float2 *iq, long long nframes, int S, int R, 
     if (nq <= 0) return hipSuccess;
     const long long bpf = ((S - 1) + H_PAIRS - 1) / H_PAIRS, nb = nframes * bpf, pxcd = (nb + 7) / 8;
     if (pxcd * 8 > 0x7fffffffll) return hipErrorInvalidValue;
-    auto kern = k_mrc_td4096h<0>;
+    // IL = 3: the row's two FFT1024s software-pipelined through the transpose
+    // image and the first quarter of the next row issued at the row start
+    // (same-process A/B, R=32 x 300 frames: 6.81 vs 7.53 ms, bit-identical;
+    // profiles/r3/r3_ab_il*_c4096.jsonl)
+    auto kern = k_mrc_td4096h<0, 3, H_PAIRS, 0, 3>;
 #ifdef OFDM_AB_KNOBS
+    if (ab_knob("MRC4K_IL", 3) == 0) kern = k_mrc_td4096h<0>;  // round 2's row (FFTs one after the other)
     switch (ab_knob("MRC4K_DBG", 0)) {
         case 1: kern = k_mrc_td4096h<1>; break;
         case 2: kern = k_mrc_td4096h<2>; break;
@@ -628,6 +633,7 @@ hipError_t launch_mrc_td4096(const float2 *iq, long long nframes, int S, int R, 
     }
     if (ab_knob("MRC4K_IL", 0) == 1) kern = k_mrc_td4096h<0, 3, H_PAIRS, 0, 1>;  // FFTs software-pipelined
     if (ab_knob("MRC4K_IL", 0) == 3) kern = k_mrc_td4096h<0, 3, H_PAIRS, 0, 3>;  // + a quarter at row start
+    if (ab_knob("MRC4K_IL", 0) == 67) kern = k_mrc_td4096h<64, 3, H_PAIRS, 0, 3>;  // IL=3 compute only (diag)
     if (ab_knob("MRC4K_IL", 0) == 65) kern = k_mrc_td4096h<64, 3, H_PAIRS, 0, 1>;  // + compute only (diag)
     if (ab_knob("MRC4K_HP", 4) == 2) {  // two independent 2-pair workgroups per CU, single Hc buffer
         const long long bpf2 = ((S - 1) + 1) / 2, nb2 = nframes * bpf2, px2 = (nb2 + 7) / 8;
