@@ -141,7 +141,58 @@ constexpr int MRC_WAVES = 4;
 // PK: packed-f32 arithmetic (pk.hpp) -- bit 1 the first half of each
 // 1024-point FFT (row_fft_a), bit 2 the second (row_fft_b), bit 4 the MAC.
 // Default 6: 3-3.5 % faster than none under the ILP scheduler.
-template <int DBG = 0, int PK = 6>
+// IL (A/B): the row's two FFT1024s software-pipelined through the transpose
+// image as in k_mrc_td4096h (hlds::fa_* / fb_*, packed butterflies,
+// recurrence twiddles, the MAC packed): A(u) -> write(u) -> read(u) -> A(v)
+// while u's transpose is in flight -> write(v), read(v) -> the row's Hc
+// loads -> B(u), B(v) -> MAC.  IL = 2: also the lower half of the next row
+// issued right after this row's DIF split (in flight through both FFTs).
+template <int IL>
+__device__ __forceinline__ void il_row(const float2 *__restrict__ src, const float2 *__restrict__ next,
+                                       const float4 *__restrict__ hr, int t, float2 *T, const float2 *twv,
+                                       pk::v2f w1, pk::v2f gw, float2 (&lo)[16], float2 (&ae)[16],
+                                       float2 (&ao)[16]) {
+    using namespace pk;
+    float2 hi[16];
+    if (IL == 1) row_load<true>(src, t, lo);  // IL >= 2: lo was loaded during the previous row
+    row_load<true>(src + HALF, t, hi);
+    v2f u[16], v[16], xu[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        const v2f d = sub(V(lo[m]), V(hi[m]));
+        u[m] = add(V(lo[m]), V(hi[m]));
+        v[m] = cmul(d, V(twv[m * 64 + t]));
+    }
+    if (IL >= 2 && next) row_load<true>(next, t, lo);
+    hl::fa_compute(u, w1);
+    hl::fa_write(u, t, T);
+    hl::fb_read(t, T, xu);
+    hl::fa_compute(v, w1);
+    hl::fa_write(v, t, T);
+    hl::fb_read(t, T, u);
+    __builtin_amdgcn_sched_barrier(0);
+    float4 h[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) h[k] = hr[k * 64 + t];
+    __builtin_amdgcn_sched_barrier(0);
+    float2 x[16];
+    hl::fb_compute(xu, gw, t, x);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {  // matrixMultThenSum (cpuLS.hpp:191-206), packed as the default kernel
+        v2f a0 = V(ae[k]);
+        pk::mac(a0, V(x[k]), (v2f){h[k].x, h[k].y});
+        ae[k] = F(a0);
+    }
+    hl::fb_compute(u, gw, t, x);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        v2f a0 = V(ao[k]);
+        pk::mac(a0, V(x[k]), (v2f){h[k].z, h[k].w});
+        ao[k] = F(a0);
+    }
+}
+
+template <int DBG = 0, int PK = 6, int IL = 0>
 __global__ void __attribute__((amdgpu_flat_work_group_size(256, 256), amdgpu_waves_per_eu(2, 2)))
 k_mrc_td2048(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
              const float *__restrict__ P, float2 *__restrict__ out, long long nq, long long nblocks,
@@ -167,8 +218,17 @@ k_mrc_td2048(const float2 *__restrict__ iq, int S, int R, int prefix, const floa
     float2 ae[16], ao[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) ae[k] = ao[k] = float2{0.f, 0.f};
+    if constexpr (IL != 0) {
+        const float2 *twv = lds + hl::TW1S + hl::TW2S;
+        const pk::v2f w1 = pk::V(lds[t]), gw = pk::V(lds[hl::TW1S + 4 + (t & 3)]);  // row invariants
+        float2 lo[16];
+        if (IL >= 2) row_load<true>(sym, t, lo);
+        for (int r = 0; r < R; ++r)
+            il_row<IL>(sym + (long long)r * Cp, r + 1 < R ? sym + (long long)(r + 1) * Cp : nullptr,
+                       Hf + (long long)r * (C / 2), t, T, twv, w1, gw, lo, ae, ao);
+    }
     float2 xe[16], xo[16];
-    for (int r = 0; r < R; ++r) {
+    for (int r = 0; r < (IL != 0 ? 0 : R); ++r) {
         if ((DBG & 64) && r > 0)
             row_fft2048<true, false>(sym, t, T, lds, xe, xo);
         else
@@ -295,6 +355,8 @@ hipError_t launch_mrc_td2048(const float2 *iq, long long nframes, int S, int R, 
         case 64: kern = k_mrc_td2048<64>; break;
         default: break;
     }
+    if (ab_knob("MRC2K_IL", 0) == 1) kern = k_mrc_td2048<0, 6, 1>;  // FFTs software-pipelined
+    if (ab_knob("MRC2K_IL", 0) == 2) kern = k_mrc_td2048<0, 6, 2>;  // + next row's lower half early
     switch (ab_knob("MRC2K_PK", -1)) {  // packed-f32 parts other than the default 6
         case 0: kern = k_mrc_td2048<0, 0>; break;
         case 1: kern = k_mrc_td2048<0, 1>; break;

@@ -196,37 +196,6 @@ __device__ __forceinline__ void dma_hc_row(const float2 *g, unsigned lds) {
     for (int j = 0; j < 32 / NW; ++j) dma16(src + j * NW * 1024, lds + j * NW * 1024 + w * 1024);
 }
 
-// The two FFT1024 stages of hlds::row_fft_a / row_fft_b (PK = 3, TW = 3:
-// packed butterflies, twiddles by recurrence) split at the transpose, so that
-// x_row's IL variant can put one transform's compute between the other's
-// LDS write and read (A/B build only).
-// w1 = W1024^t (tw1[t]) and gw = g(a) W64^a (tw2[4 + a]) are per-lane row
-// invariants, read from LDS once per kernel: an LDS read inside the pipeline
-// would make every later wait on it a wait for the whole transpose in flight.
-__device__ __forceinline__ void fa_compute(pk::v2f (&v)[16], pk::v2f w1) {
-    pk::fft_reg<16>(v);
-    hl::tw_powers(v, w1, w1);
-}
-__device__ __forceinline__ void fa_write(const pk::v2f (&v)[16], int t, float2 *T) {
-#pragma unroll
-    for (int k2 = 0; k2 < 16; ++k2) T[hl::swz(k2, t)] = pk::F(v[k2]);
-}
-__device__ __forceinline__ void fb_read(int t, const float2 *T, pk::v2f (&v)[16]) {
-    const int q = t >> 2, qa = t & 3;
-#pragma unroll
-    for (int l = 0; l < 16; ++l) v[l] = pk::V(T[hl::swz(q, qa + 4 * l)]);
-}
-__device__ __forceinline__ void fb_compute(pk::v2f (&v)[16], pk::v2f gw, int t, float2 (&x)[16]) {
-    const int qa = t & 3;
-    const float g = td1024::quad_g(qa);
-    pk::fft_reg<16>(v);
-    v[0] = pk::scale(v[0], g);
-    hl::tw_powers(v, pk::scale(gw, g), gw);
-#pragma unroll
-    for (int m = 0; m < 16; ++m) x[m] = pk::F(v[m]);
-    td1024::quad_dft(x, qa);
-}
-
 // One antenna row for wave E of the pair.  On entry a/b hold the row's
 // quarters E and E + 2; with PREF the next row's quarters are loaded into
 // them after the first FFT and stay in flight through the second FFT and
@@ -315,17 +284,17 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
         if constexpr (IL >= 3) {  // first quarter of the next row in flight through both transforms
             if (PREF && !(DBG & 64)) row_load<true>(next + 1024 * E, t, a);
         }
-        fa_compute(u, w1);
-        fa_write(u, t, T);
-        fb_read(t, T, xu);
-        fa_compute(v, w1);
-        fa_write(v, t, T);
-        fb_read(t, T, u);  // u's registers are free: v's transpose lands in them
+        hl::fa_compute(u, w1);
+        hl::fa_write(u, t, T);
+        hl::fb_read(t, T, xu);
+        hl::fa_compute(v, w1);
+        hl::fa_write(v, t, T);
+        hl::fb_read(t, T, u);  // u's registers are free: v's transpose lands in them
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int k = 0; k < 16; ++k) h[k] = hr[k * 64 + t];  // plane 0, lands during B(u)
         __builtin_amdgcn_sched_barrier(0);
-        fb_compute(xu, gw, t, x);
+        hl::fb_compute(xu, gw, t, x);
 #pragma unroll
         for (int k = 0; k < 16; ++k) {  // matrixMultThenSum (cpuLS.hpp:191-206), packed as the default path
             v2f a0 = V(ae[k]);
@@ -340,7 +309,7 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
             if (IL == 1) row_load<true>(next + 1024 * E, t, a);
             row_load<true>(next + 1024 * (E + 2), t, b);
         }
-        fb_compute(u, gw, t, x);
+        hl::fb_compute(u, gw, t, x);
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             v2f a0 = V(ao[k]);
@@ -456,7 +425,7 @@ __device__ __forceinline__ void h_rows(const float2 *sym, int Cp, int R, const f
     const unsigned hb0 = lds_addr(HB), hb1 = lds_addr(HB + C);
     constexpr int NB = HP == 4 ? 2 : 1;  // Hc buffers
     pk::v2f w1 = {}, gw = {};
-    if constexpr (IL != 0) {  // the FFT twiddle bases, loop-invariant (see fa_compute)
+    if constexpr (IL != 0) {  // the FFT twiddle bases, loop-invariant (see hlds::fa_compute)
         w1 = pk::V(tw1[t]);
         gw = pk::V(tw2[4 + (t & 3)]);
     }

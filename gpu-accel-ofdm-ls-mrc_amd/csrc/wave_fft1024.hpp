@@ -347,6 +347,37 @@ __device__ __forceinline__ void row_fft_b(int t, float2 *T, const float2 *tw2, f
     }
     quad_dft(x, qa);
 }
+// The two FFT1024 stages of hlds::row_fft_a / row_fft_b (PK = 3, TW = 3:
+// packed butterflies, twiddles by recurrence) split at the transpose, so that
+// the IL variants of the C = 2048 / 4096 rows can put one transform's compute between the other's
+// LDS write and read (A/B build only).
+// w1 = W1024^t (tw1[t]) and gw = g(a) W64^a (tw2[4 + a]) are per-lane row
+// invariants, read from LDS once per kernel: an LDS read inside the pipeline
+// would make every later wait on it a wait for the whole transpose in flight.
+__device__ __forceinline__ void fa_compute(pk::v2f (&v)[16], pk::v2f w1) {
+    pk::fft_reg<16>(v);
+    tw_powers(v, w1, w1);
+}
+__device__ __forceinline__ void fa_write(const pk::v2f (&v)[16], int t, float2 *T) {
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2) T[swz(k2, t)] = pk::F(v[k2]);
+}
+__device__ __forceinline__ void fb_read(int t, const float2 *T, pk::v2f (&v)[16]) {
+    const int q = t >> 2, qa = t & 3;
+#pragma unroll
+    for (int l = 0; l < 16; ++l) v[l] = pk::V(T[swz(q, qa + 4 * l)]);
+}
+__device__ __forceinline__ void fb_compute(pk::v2f (&v)[16], pk::v2f gw, int t, float2 (&x)[16]) {
+    const int qa = t & 3;
+    const float g = quad_g(qa);
+    pk::fft_reg<16>(v);
+    v[0] = pk::scale(v[0], g);
+    tw_powers(v, pk::scale(gw, g), gw);
+#pragma unroll
+    for (int m = 0; m < 16; ++m) x[m] = pk::F(v[m]);
+    quad_dft(x, qa);
+}
+
 }  // namespace hlds
 
 }  // namespace td1024
