@@ -141,20 +141,22 @@ constexpr int MRC_WAVES = 4;
 // PK: packed-f32 arithmetic (pk.hpp) -- bit 1 the first half of each
 // 1024-point FFT (row_fft_a), bit 2 the second (row_fft_b), bit 4 the MAC.
 // Default 6: 3-3.5 % faster than none under the ILP scheduler.
-// IL (A/B): the row's two FFT1024s software-pipelined through the transpose
-// image as in k_mrc_td4096h (hlds::fa_* / fb_*, packed butterflies,
-// recurrence twiddles, the MAC packed): A(u) -> write(u) -> read(u) -> A(v)
-// while u's transpose is in flight -> write(v), read(v) -> the row's Hc
-// loads -> B(u), B(v) -> MAC.  IL = 2: also the lower half of the next row
-// issued right after this row's DIF split (in flight through both FFTs).
+// IL = 1 (the default since round 3): the row's two FFT1024s
+// software-pipelined through the transpose image as in k_mrc_td4096h
+// (hlds::fa_* / fb_*, packed butterflies, recurrence twiddles, the MAC
+// packed): A(u) -> write(u) -> read(u) -> A(v) while u's transpose is in
+// flight -> write(v), read(v) -> the row's Hc loads -> B(u), B(v) -> MAC.
+// Same-process A/B, R=64 x 200 frames: 4.06 vs 4.29 ms, outputs within
+// 7.8e-7 of the round-2 row (profiles/r3/r3_ab_il_c2048.jsonl).  The next
+// row's lower half issued after the DIF split (measured: 47 spilled VGPRs,
+// 6.87 ms) was dropped.
 template <int IL>
-__device__ __forceinline__ void il_row(const float2 *__restrict__ src, const float2 *__restrict__ next,
-                                       const float4 *__restrict__ hr, int t, float2 *T, const float2 *twv,
+__device__ __forceinline__ void il_row(const float2 *__restrict__ src, const float4 *__restrict__ hr, int t, float2 *T, const float2 *twv,
                                        pk::v2f w1, pk::v2f gw, float2 (&lo)[16], float2 (&ae)[16],
                                        float2 (&ao)[16]) {
     using namespace pk;
     float2 hi[16];
-    if (IL == 1) row_load<true>(src, t, lo);  // IL >= 2: lo was loaded during the previous row
+    row_load<true>(src, t, lo);
     row_load<true>(src + HALF, t, hi);
     v2f u[16], v[16], xu[16];
 #pragma unroll
@@ -163,7 +165,6 @@ __device__ __forceinline__ void il_row(const float2 *__restrict__ src, const flo
         u[m] = add(V(lo[m]), V(hi[m]));
         v[m] = cmul(d, V(twv[m * 64 + t]));
     }
-    if (IL >= 2 && next) row_load<true>(next, t, lo);
     hl::fa_compute(u, w1);
     hl::fa_write(u, t, T);
     hl::fb_read(t, T, xu);
@@ -192,7 +193,7 @@ __device__ __forceinline__ void il_row(const float2 *__restrict__ src, const flo
     }
 }
 
-template <int DBG = 0, int PK = 6, int IL = 0>
+template <int DBG = 0, int PK = 6, int IL = 1>
 __global__ void __attribute__((amdgpu_flat_work_group_size(256, 256), amdgpu_waves_per_eu(2, 2)))
 k_mrc_td2048(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
              const float *__restrict__ P, float2 *__restrict__ out, long long nq, long long nblocks,
@@ -222,10 +223,8 @@ k_mrc_td2048(const float2 *__restrict__ iq, int S, int R, int prefix, const floa
         const float2 *twv = lds + hl::TW1S + hl::TW2S;
         const pk::v2f w1 = pk::V(lds[t]), gw = pk::V(lds[hl::TW1S + 4 + (t & 3)]);  // row invariants
         float2 lo[16];
-        if (IL >= 2) row_load<true>(sym, t, lo);
         for (int r = 0; r < R; ++r)
-            il_row<IL>(sym + (long long)r * Cp, r + 1 < R ? sym + (long long)(r + 1) * Cp : nullptr,
-                       Hf + (long long)r * (C / 2), t, T, twv, w1, gw, lo, ae, ao);
+            il_row<IL>(sym + (long long)r * Cp, Hf + (long long)r * (C / 2), t, T, twv, w1, gw, lo, ae, ao);
     }
     float2 xe[16], xo[16];
     for (int r = 0; r < (IL != 0 ? 0 : R); ++r) {
@@ -347,22 +346,21 @@ hipError_t launch_mrc_td2048(const float2 *iq, long long nframes, int S, int R, 
     if (grid > 0x7fffffffll) return hipErrorInvalidValue;
     auto kern = k_mrc_td2048<0>;
 #ifdef OFDM_AB_KNOBS
+    if (ab_knob("MRC2K_IL", 1) == 0) kern = k_mrc_td2048<0, 6, 0>;  // round 2's row (FFTs one after the other)
     switch (ab_knob("MRC2K_DBG", 0)) {
-        case 2: kern = k_mrc_td2048<2>; break;
-        case 4: kern = k_mrc_td2048<4>; break;
-        case 6: kern = k_mrc_td2048<6>; break;
-        case 8: kern = k_mrc_td2048<8>; break;
-        case 64: kern = k_mrc_td2048<64>; break;
+        case 2: kern = k_mrc_td2048<2, 6, 0>; break;  // round-2 row
+        case 4: kern = k_mrc_td2048<4, 6, 0>; break;  // round-2 row
+        case 6: kern = k_mrc_td2048<6, 6, 0>; break;  // round-2 row
+        case 8: kern = k_mrc_td2048<8, 6, 0>; break;  // round-2 row
+        case 64: kern = k_mrc_td2048<64, 6, 0>; break;  // round-2 row
         default: break;
     }
-    if (ab_knob("MRC2K_IL", 0) == 1) kern = k_mrc_td2048<0, 6, 1>;  // FFTs software-pipelined
-    if (ab_knob("MRC2K_IL", 0) == 2) kern = k_mrc_td2048<0, 6, 2>;  // + next row's lower half early
     switch (ab_knob("MRC2K_PK", -1)) {  // packed-f32 parts other than the default 6
-        case 0: kern = k_mrc_td2048<0, 0>; break;
-        case 1: kern = k_mrc_td2048<0, 1>; break;
-        case 2: kern = k_mrc_td2048<0, 2>; break;
-        case 3: kern = k_mrc_td2048<0, 3>; break;
-        case 7: kern = k_mrc_td2048<0, 7>; break;
+        case 0: kern = k_mrc_td2048<0, 0, 0>; break;
+        case 1: kern = k_mrc_td2048<0, 1, 0>; break;
+        case 2: kern = k_mrc_td2048<0, 2, 0>; break;
+        case 3: kern = k_mrc_td2048<0, 3, 0>; break;
+        case 7: kern = k_mrc_td2048<0, 7, 0>; break;
         default: break;
     }
 #endif
