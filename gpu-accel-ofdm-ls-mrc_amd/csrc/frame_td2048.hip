@@ -152,7 +152,7 @@ constexpr int MRC_WAVES = 4;
 // 6.87 ms) was dropped.
 template <int IL>
 __device__ __forceinline__ void il_row(const float2 *__restrict__ src, const float4 *__restrict__ hr, int t, float2 *T, const float2 *twv,
-                                       pk::v2f w1, pk::v2f gw, float2 (&lo)[16], float2 (&ae)[16],
+                                       const hl::TwAnchors &ca, const hl::TwAnchors &cb, float2 (&lo)[16], float2 (&ae)[16],
                                        float2 (&ao)[16]) {
     using namespace pk;
     float2 hi[16];
@@ -165,10 +165,10 @@ __device__ __forceinline__ void il_row(const float2 *__restrict__ src, const flo
         u[m] = add(V(lo[m]), V(hi[m]));
         v[m] = cmul(d, V(twv[m * 64 + t]));
     }
-    hl::fa_compute(u, w1);
+    hl::fa_compute(u, ca);
     hl::fa_write(u, t, T);
     hl::fb_read(t, T, xu);
-    hl::fa_compute(v, w1);
+    hl::fa_compute(v, ca);
     hl::fa_write(v, t, T);
     hl::fb_read(t, T, u);
     __builtin_amdgcn_sched_barrier(0);
@@ -177,14 +177,14 @@ __device__ __forceinline__ void il_row(const float2 *__restrict__ src, const flo
     for (int k = 0; k < 16; ++k) h[k] = hr[k * 64 + t];
     __builtin_amdgcn_sched_barrier(0);
     float2 x[16];
-    hl::fb_compute(xu, gw, t, x);
+    hl::fb_compute(xu, cb, t, x);
 #pragma unroll
     for (int k = 0; k < 16; ++k) {  // matrixMultThenSum (cpuLS.hpp:191-206), packed as the default kernel
         v2f a0 = V(ae[k]);
         pk::mac(a0, V(x[k]), (v2f){h[k].x, h[k].y});
         ae[k] = F(a0);
     }
-    hl::fb_compute(u, gw, t, x);
+    hl::fb_compute(u, cb, t, x);
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
         v2f a0 = V(ao[k]);
@@ -221,10 +221,10 @@ k_mrc_td2048(const float2 *__restrict__ iq, int S, int R, int prefix, const floa
     for (int k = 0; k < 16; ++k) ae[k] = ao[k] = float2{0.f, 0.f};
     if constexpr (IL != 0) {
         const float2 *twv = lds + hl::TW1S + hl::TW2S;
-        const pk::v2f w1 = pk::V(lds[t]), gw = pk::V(lds[hl::TW1S + 4 + (t & 3)]);  // row invariants
+        const hl::TwAnchors ca = hl::anchors_a(lds, t), cb = hl::anchors_b(lds + hl::TW1S, t);  // row invariants
         float2 lo[16];
         for (int r = 0; r < R; ++r)
-            il_row<IL>(sym + (long long)r * Cp, Hf + (long long)r * (C / 2), t, T, twv, w1, gw, lo, ae, ao);
+            il_row<IL>(sym + (long long)r * Cp, Hf + (long long)r * (C / 2), t, T, twv, ca, cb, lo, ae, ao);
     }
     float2 xe[16], xo[16];
     for (int r = 0; r < (IL != 0 ? 0 : R); ++r) {

@@ -223,7 +223,8 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
                                       int t, float2 *T, const float2 *Tp, const float2 *tw1,
                                       const float2 *tw2, pk::v2f wb0, pk::v2f wb1, float2 (&a)[16],
                                       float2 (&b)[16], float2 (&ae)[16], float2 (&ao)[16],
-                                      const float2 *hnext, unsigned hb_next, pk::v2f w1 = {}, pk::v2f gw = {}) {
+                                      const float2 *hnext, unsigned hb_next, const hl::TwAnchors &ca = {},
+                                      const hl::TwAnchors &cb = {}) {
     using namespace pk;
     v2f u[16], v[16];
 #pragma unroll
@@ -284,17 +285,25 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
         if constexpr (IL >= 3) {  // first quarter of the next row in flight through both transforms
             if (PREF && !(DBG & 64)) row_load<true>(next + 1024 * E, t, a);
         }
-        hl::fa_compute(u, w1);
+        // twiddle anchors read just in time, not held across the row
+        // (hlds::tw_anchored; as row invariants they cost 37 spilled VGPRs):
+        // stage A's with the LDS queue empty, stage B's behind v's transpose
+        // reads, consumed after B's radix-16
+        (void)ca;
+        (void)cb;
+        const hl::TwAnchors a_tw = hl::anchors_a(tw1, t);
+        hl::fa_compute(u, a_tw);
         hl::fa_write(u, t, T);
         hl::fb_read(t, T, xu);
-        hl::fa_compute(v, w1);
+        hl::fa_compute(v, a_tw);
         hl::fa_write(v, t, T);
         hl::fb_read(t, T, u);  // u's registers are free: v's transpose lands in them
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int k = 0; k < 16; ++k) h[k] = hr[k * 64 + t];  // plane 0, lands during B(u)
+        hl::TwAnchors b_tw = hl::anchors_b(tw2, t);
         __builtin_amdgcn_sched_barrier(0);
-        hl::fb_compute(xu, gw, t, x);
+        hl::fb_compute(xu, b_tw, t, x);
 #pragma unroll
         for (int k = 0; k < 16; ++k) {  // matrixMultThenSum (cpuLS.hpp:191-206), packed as the default path
             v2f a0 = V(ae[k]);
@@ -309,7 +318,8 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
             if (IL == 1) row_load<true>(next + 1024 * E, t, a);
             row_load<true>(next + 1024 * (E + 2), t, b);
         }
-        hl::fb_compute(u, gw, t, x);
+        b_tw = hl::anchors_b(tw2, t);
+        hl::fb_compute(u, b_tw, t, x);
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             v2f a0 = V(ao[k]);
@@ -424,17 +434,13 @@ __device__ __forceinline__ void h_rows(const float2 *sym, int Cp, int R, const f
     }
     const unsigned hb0 = lds_addr(HB), hb1 = lds_addr(HB + C);
     constexpr int NB = HP == 4 ? 2 : 1;  // Hc buffers
-    pk::v2f w1 = {}, gw = {};
-    if constexpr (IL != 0) {  // the FFT twiddle bases, loop-invariant (see hlds::fa_compute)
-        w1 = pk::V(tw1[t]);
-        gw = pk::V(tw2[4 + (t & 3)]);
-    }
+    const hl::TwAnchors ca = {}, cb = {};  // (read per row inside x_row)
     for (int r = 0; r + 1 < R; ++r)
         x_row<E, PK, true, DBG, TW, HP, HE, IL>(sym + (long long)(r + 1) * Cp, HB + (NB == 2 ? (r & 1) * C : 0) + E * 2048,
                                         t, T, Tp, tw1, tw2, wb0, wb1, a, b, ae, ao, Hg + (long long)(r + 1) * C,
-                                        NB == 2 && !(r & 1) ? hb1 : hb0, w1, gw);
+                                        NB == 2 && !(r & 1) ? hb1 : hb0, ca, cb);
     x_row<E, PK, false, DBG, TW, HP, HE, IL>(sym, HB + (NB == 2 ? ((R - 1) & 1) * C : 0) + E * 2048, t, T, Tp, tw1, tw2,
-                                     wb0, wb1, a, b, ae, ao, nullptr, 0, w1, gw);
+                                     wb0, wb1, a, b, ae, ao, nullptr, 0, ca, cb);
 }
 
 constexpr int H_PK = 7;  // packed-f32 split, FFT halves and MAC (pk.hpp)

@@ -354,9 +354,48 @@ __device__ __forceinline__ void row_fft_b(int t, float2 *T, const float2 *tw2, f
 // w1 = W1024^t (tw1[t]) and gw = g(a) W64^a (tw2[4 + a]) are per-lane row
 // invariants, read from LDS once per kernel: an LDS read inside the pipeline
 // would make every later wait on it a wait for the whole transpose in flight.
+// Twiddles s W^k, k = 1..15, from exact table anchors A_k = s W^k for
+// k = 1, 4, 8, 12 and the base W: every other power is one anchor times W,
+// W^2 or W^3 (recursion depth <= 3 instead of tw_powers' 7, so the error
+// stays within a few ulp -- tw_powers' up to 8e-7 pushed single-antenna
+// (R = 1) outputs past the 1e-5 element-wise parity bound).
+struct TwAnchors {
+    pk::v2f w, a1, a4, a8, a12;
+};
+__device__ __forceinline__ void tw_anchored(pk::v2f (&v)[16], const TwAnchors &c) {
+    const pk::v2f w2 = pk::cmul(c.w, c.w), w3 = pk::cmul(w2, c.w);
+    v[1] = pk::cmul(v[1], c.a1);
+    v[2] = pk::cmul(v[2], pk::cmul(c.a1, c.w));
+    v[3] = pk::cmul(v[3], pk::cmul(c.a1, w2));
+#pragma unroll
+    for (int j = 1; j < 4; ++j) {
+        const pk::v2f a = j == 1 ? c.a4 : j == 2 ? c.a8 : c.a12;
+        v[4 * j] = pk::cmul(v[4 * j], a);
+        v[4 * j + 1] = pk::cmul(v[4 * j + 1], pk::cmul(a, c.w));
+        v[4 * j + 2] = pk::cmul(v[4 * j + 2], pk::cmul(a, w2));
+        v[4 * j + 3] = pk::cmul(v[4 * j + 3], pk::cmul(a, w3));
+    }
+}
+// The anchors of the two FFT1024 stages for lane t, from the hlds tables:
+// stage A: W1024^(t k) = tw1[(k - 1) * 64 + t]; stage B: g(a) W64^(a k) =
+// tw2[k * 4 + a] (g = +-1, so W = g * tw2[4 + a] is exact).
+__device__ __forceinline__ TwAnchors anchors_a(const float2 *tw1, int t) {
+    const pk::v2f w = pk::V(tw1[t]);
+    return TwAnchors{w, w, pk::V(tw1[3 * 64 + t]), pk::V(tw1[7 * 64 + t]), pk::V(tw1[11 * 64 + t])};
+}
+__device__ __forceinline__ TwAnchors anchors_b(const float2 *tw2, int t) {
+    const int qa = t & 3;
+    const pk::v2f gw = pk::V(tw2[4 + qa]);
+    return TwAnchors{pk::scale(gw, quad_g(qa)), gw, pk::V(tw2[16 + qa]), pk::V(tw2[32 + qa]), pk::V(tw2[48 + qa])};
+}
+
 __device__ __forceinline__ void fa_compute(pk::v2f (&v)[16], pk::v2f w1) {
     pk::fft_reg<16>(v);
     tw_powers(v, w1, w1);
+}
+__device__ __forceinline__ void fa_compute(pk::v2f (&v)[16], const TwAnchors &c) {
+    pk::fft_reg<16>(v);
+    tw_anchored(v, c);
 }
 __device__ __forceinline__ void fa_write(const pk::v2f (&v)[16], int t, float2 *T) {
 #pragma unroll
@@ -373,6 +412,15 @@ __device__ __forceinline__ void fb_compute(pk::v2f (&v)[16], pk::v2f gw, int t, 
     pk::fft_reg<16>(v);
     v[0] = pk::scale(v[0], g);
     tw_powers(v, pk::scale(gw, g), gw);
+#pragma unroll
+    for (int m = 0; m < 16; ++m) x[m] = pk::F(v[m]);
+    quad_dft(x, qa);
+}
+__device__ __forceinline__ void fb_compute(pk::v2f (&v)[16], const TwAnchors &c, int t, float2 (&x)[16]) {
+    const int qa = t & 3;
+    pk::fft_reg<16>(v);
+    v[0] = pk::scale(v[0], quad_g(qa));
+    tw_anchored(v, c);
 #pragma unroll
     for (int m = 0; m < 16; ++m) x[m] = pk::F(v[m]);
     quad_dft(x, qa);
