@@ -1320,6 +1320,134 @@ k_zf_wstat(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__rest
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// k_zf_apply16: the apply (multiplyWithChannelInv, cpuLS.hpp:449-463; Y = W X
+// per subcarrier) with TWO subcarriers per lane, so every operand load and
+// every output store is 16 B per lane (1 KiB per wave instruction).  The
+// round-3 store-stream probes (scripts/zfprobe2.hip) put the
+// apply's bytes at 35-40 % less time with 16-B than with 8-B stores, and row
+// contiguity beyond a 1 KiB piece at nothing.  Workgroup = 4 waves over a
+// tile of 128 subcarriers x 2 MT rows, stepping through 2 ST symbols at a
+// time in its symbol chunk; wave (mg, sg) owns MT rows x ST symbols x 2
+// subcarriers (MT ST complex pairs of accumulators).  Per input n the tile's
+// 2 MT W rows and 2 ST input rows (1 KiB each) are staged once in LDS
+// (double buffer, the next n's loads in flight during this n's MACs, one
+// barrier per n) and every wave reads its 16-B operands from there.  Sums
+// over n in the reference's order (n = 0 .. N-1, one complex MAC each as
+// k_zf_gemm_lds).  K odd: the lane pair (K-1, K) stores one value.
+// ---------------------------------------------------------------------------
+template <int MT, int ST>
+__global__ void __attribute__((amdgpu_flat_work_group_size(256, 256), amdgpu_waves_per_eu(2)))
+k_zf_apply16(const float2 *__restrict__ Wt, const float2 *__restrict__ X, int U, int R, int K, long long nsym,
+             float2 *__restrict__ Y, int ntile, int tpx, int nkb, long long chunk_steps) {
+    constexpr int MB = 2 * MT, SB = 2 * ST, ROWS = MB + SB;  // staged 1 KiB rows per n
+    constexpr int RPT = ROWS / 4;                            // staged rows per wave
+    static_assert(ROWS % 4 == 0, "staged rows split over the 4 waves");
+    __shared__ float4 sm[2][ROWS * 64];
+    const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
+    const int tile = xcd + 8 * (j % tpx);
+    if (tile >= ntile) return;  // whole workgroup
+    const long long chunk = j / tpx;
+    const int kb = tile % nkb, rb = tile / nkb;
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int mg = w & 1, sg = w >> 1;
+    const int k = kb * 128 + 2 * lane;                 // this lane's subcarriers k, k + 1
+    const int kc = k + 1 < K ? k : (K >= 2 ? K - 2 : 0);  // loads stay in range (K >= 2 here)
+    const int r0 = rb * MB;
+    const long long nsteps_total = (nsym + SB - 1) / SB;
+    const long long step0 = chunk * chunk_steps, step1 = min(step0 + chunk_steps, nsteps_total);
+    if (step1 <= step0) return;  // whole workgroup
+    const int nst = (int)(step1 - step0);
+
+    // staged row i of wave w: row = w + 4 i; rows < MB are W(r0 + row, n),
+    // the others input rows (symbol s0 + row - MB, n)
+    float4 stg[RPT];
+    auto load = [&](int cs, int n) {
+        const long long s0 = (step0 + cs) * SB;
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) {
+            const int row = w + 4 * i;
+            const float2 *p;
+            if (row < MB) {
+                const int r = min(r0 + row, R - 1);
+                p = Wt + ((long long)n * R + r) * K + kc;
+            } else {
+                const long long sy = min(s0 + (row - MB), nsym - 1);
+                p = X + (sy * U + n) * (long long)K + kc;
+            }
+            stg[i] = *reinterpret_cast<const float4 *>(p);  // 8-byte aligned on odd rows: unaligned dwordx4
+        }
+    };
+    auto put = [&](int buf) {
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) sm[buf][(w + 4 * i) * 64 + lane] = stg[i];
+    };
+    float2 acc[MT][ST][2];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int jj = 0; jj < ST; ++jj) acc[i][jj][0] = acc[i][jj][1] = float2{0.f, 0.f};
+    load(0, 0);
+    put(0);
+    __syncthreads();
+    int cs = 0, n = 0, buf = 0;
+    for (;;) {
+        const int nn = n + 1 == U ? 0 : n + 1, ncs = n + 1 == U ? cs + 1 : cs;
+        const bool more = ncs < nst;
+        if (more) load(ncs, nn);  // in flight during this n's MACs
+        const float4 *sa = sm[buf] + (mg * MT) * 64 + lane;
+        const float4 *sx = sm[buf] + (MB + sg * ST) * 64 + lane;
+        float4 a[MT], x[ST];
+#pragma unroll
+        for (int i = 0; i < MT; ++i) a[i] = sa[i * 64];
+#pragma unroll
+        for (int jj = 0; jj < ST; ++jj) x[jj] = sx[jj * 64];
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+#pragma unroll
+            for (int jj = 0; jj < ST; ++jj) {  // W(r, n) X(s, n) for both subcarriers
+                acc[i][jj][0].x = fmaf(a[i].x, x[jj].x, fmaf(-a[i].y, x[jj].y, acc[i][jj][0].x));
+                acc[i][jj][0].y = fmaf(a[i].x, x[jj].y, fmaf(a[i].y, x[jj].x, acc[i][jj][0].y));
+                acc[i][jj][1].x = fmaf(a[i].z, x[jj].z, fmaf(-a[i].w, x[jj].w, acc[i][jj][1].x));
+                acc[i][jj][1].y = fmaf(a[i].z, x[jj].w, fmaf(a[i].w, x[jj].z, acc[i][jj][1].y));
+            }
+        }
+        if (n == U - 1) {  // the symbol step's last input: store, reset
+            const long long s0 = (step0 + cs) * SB + sg * ST;
+            const int m0 = r0 + mg * MT;
+            if (k < K) {
+                float2 *o = Y + (s0 * R + m0) * (long long)K + k;
+                const bool pair = k + 1 < K;
+#pragma unroll
+                for (int jj = 0; jj < ST; ++jj) {
+                    if (s0 + jj >= nsym) break;
+#pragma unroll
+                    for (int i = 0; i < MT; ++i) {
+                        if (m0 + i >= R) break;
+                        float2 *q = o + (long long)(jj * R + i) * K;
+                        if (pair)
+                            *reinterpret_cast<float4 *>(q) =
+                                float4{acc[i][jj][0].x, acc[i][jj][0].y, acc[i][jj][1].x, acc[i][jj][1].y};
+                        else
+                            *q = acc[i][jj][0];
+                    }
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int jj = 0; jj < ST; ++jj) acc[i][jj][0] = acc[i][jj][1] = float2{0.f, 0.f};
+        }
+        if (!more) break;
+        buf ^= 1;
+        put(buf);  // that buffer was last read in the previous n
+        cs = ncs;
+        n = nn;
+        __syncthreads();
+    }
+}
 }  // namespace zf
 
 size_t zf_precoder_lds_bytes(int U, int R) {
@@ -1414,6 +1542,26 @@ hipError_t gemm_lds_launch(const float2 *Wt, int a_m, int a_n, const float2 *in,
 #endif
     hipLaunchKernelGGL((zf::k_zf_gemm_lds<MG, CONJ>), dim3((unsigned)blocks), dim3(256), 0, s, Wt, a_m,
                        a_n, in, N, M, K, nsym, out, ntile, tpx, nkb, chunk_steps);
+    return hipGetLastError();
+}
+
+
+// k_zf_apply16 (16-B lanes); MT x ST register tiles per wave
+template <int MT, int ST>
+hipError_t apply16_launch(const float2 *Wt, const float2 *X, int U, int R, int K, long long nsym, float2 *Y,
+                          hipStream_t s) {
+    constexpr int MB = 2 * MT, SB = 2 * ST;
+    const int nkb = (K + 127) / 128, nrb = (R + MB - 1) / MB;
+    const int ntile = nkb * nrb, tpx = (ntile + 7) / 8;
+    const long long nsteps = (nsym + SB - 1) / SB;
+    long long nchunk = (2048 + 8LL * tpx - 1) / (8LL * tpx);
+    long long chunk_steps = (nsteps + nchunk - 1) / nchunk;
+    if (chunk_steps < 4) chunk_steps = 4;
+    nchunk = (nsteps + chunk_steps - 1) / chunk_steps;
+    const long long blocks = 8LL * tpx * nchunk;
+    if (blocks > 0x7fffffffll) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((zf::k_zf_apply16<MT, ST>), dim3((unsigned)blocks), dim3(256), 0, s, Wt, X, U, R, K, nsym, Y,
+                       ntile, tpx, nkb, chunk_steps);
     return hipGetLastError();
 }
 
@@ -1599,6 +1747,14 @@ hipError_t gemm_dispatch(const float2 *Wt, int a_m, int a_n, const float2 *in, i
 hipError_t launch_zf_apply(const float2 *Wt, const float2 *X, int U, int R, int K, long long nsym,
                            float2 *Y, hipStream_t s) {
     if (K == 0 || nsym == 0) return hipSuccess;
+#ifdef OFDM_AB_KNOBS
+    switch (ab_knob("ZF_A16", 0)) {  // 16-B lane apply candidates (MT x ST tiles)
+        case 1: if (K >= 2) return apply16_launch<8, 4>(Wt, X, U, R, K, nsym, Y, s); break;
+        case 2: if (K >= 2) return apply16_launch<4, 8>(Wt, X, U, R, K, nsym, Y, s); break;
+        case 3: if (K >= 2) return apply16_launch<4, 4>(Wt, X, U, R, K, nsym, Y, s); break;
+        default: break;
+    }
+#endif
     return gemm_dispatch<false>(Wt, 1, R, X, U, R, K, nsym, Y, s);
 }
 
