@@ -24,6 +24,11 @@ for C in (2048, 4096):
     iq = ofdm.synth_frames(F, S, R, C, X, prefix=prefix, seed=99 + C, noise_std=0.05)
     ref = o.frames_demod(iq.cpu().numpy(), Xh, prefix, nthreads=8).astype(np.complex128).ravel()
     rms = np.sqrt(np.mean(np.abs(ref) ** 2))
+    # what an f32 FFT (FFTW single precision in cpuLS) scores against the same f64 oracle
+    r32 = o.frames_demod_fft32(iq.cpu().numpy(), Xh, prefix, nthreads=8).astype(np.complex128).ravel()
+    e32 = np.abs(r32 - ref) / np.maximum(np.abs(ref), rms)
+    print(f"C={C} {'oracle-f32':14s} norm-rel {np.linalg.norm(r32 - ref) / np.linalg.norm(ref):.3e} "
+          f"elem-rel max {e32.max():.3e} 2nd {np.sort(e32)[-2]:.3e} p99 {np.percentile(e32, 99):.3e}", flush=True)
     for v in ["default"] + sys.argv[1:]:
         for kv in (v.split(",") if v != "default" else []):
             k, val = kv.split("=")
