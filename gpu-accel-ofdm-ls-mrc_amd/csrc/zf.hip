@@ -34,6 +34,7 @@
 #include <hip/hip_runtime.h>
 
 #include "launch.hpp"
+#include "pk.hpp"
 
 namespace ofdm {
 namespace zf {
@@ -1322,130 +1323,118 @@ k_zf_wstat(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__rest
 
 
 // ---------------------------------------------------------------------------
-// k_zf_apply16: the apply (multiplyWithChannelInv, cpuLS.hpp:449-463; Y = W X
-// per subcarrier) with TWO subcarriers per lane, so every operand load and
-// every output store is 16 B per lane (1 KiB per wave instruction).  The
-// round-3 store-stream probes (scripts/zfprobe2.hip) put the
-// apply's bytes at 35-40 % less time with 16-B than with 8-B stores, and row
-// contiguity beyond a 1 KiB piece at nothing.  Workgroup = 4 waves over a
-// tile of 128 subcarriers x 2 MT rows, stepping through 2 ST symbols at a
-// time in its symbol chunk; wave (mg, sg) owns MT rows x ST symbols x 2
-// subcarriers (MT ST complex pairs of accumulators).  Per input n the tile's
-// 2 MT W rows and 2 ST input rows (1 KiB each) are staged once in LDS
-// (double buffer, the next n's loads in flight during this n's MACs, one
-// barrier per n) and every wave reads its 16-B operands from there.  Sums
-// over n in the reference's order (n = 0 .. N-1, one complex MAC each as
-// k_zf_gemm_lds).  K odd: the lane pair (K-1, K) stores one value.
+// k_zf_apply_ws16: the apply (multiplyWithChannelInv, cpuLS.hpp:449-463;
+// Y[s][r][k] = sum_u W(r, u) X[s][u][k]) with TWO subcarriers per lane, so
+// every input load and output store is 16 B per lane (a 1 KiB piece of a row
+// per wave instruction).  The round-3 store-stream probes (scripts/
+// zfprobe2.hip) put the apply's bytes at 35-40 % less time with
+// 16-B than with 8-B stores.
+// W-stationary: a workgroup owns a tile of 128 subcarriers x MB = 8 RG output
+// rows, loads its W tile (U x MB x 1 KiB, 128 KiB at U = 16) into LDS once,
+// then its 8 waves stream their own symbols of one symbol chunk: wave (rg, sg)
+// computes rows 8 rg .. 8 rg + 7 for ST = 4 symbols at a time, reading the
+// symbols' input pieces straight from memory (prefetched one u ahead) and W
+// from LDS.  The nrb row blocks of one (chunk, subcarrier block) run on one
+// XCD, adjacent in dispatch order, so each input piece comes from HBM once and
+// from that XCD's L2 for the other row blocks.  Sum over u in the reference's
+// order, one complex MAC per u (packed: (acc + x.re w) + (-x.im) w~, which
+// matches within the parity tolerance, not bit for bit).  K odd: the last
+// lane covers subcarriers (K-2, K-1) with W(K-2) zeroed and stores only K-1.
 // ---------------------------------------------------------------------------
-template <int MT, int ST>
-__global__ void __attribute__((amdgpu_flat_work_group_size(256, 256), amdgpu_waves_per_eu(2)))
-k_zf_apply16(const float2 *__restrict__ Wt, const float2 *__restrict__ X, int U, int R, int K, long long nsym,
-             float2 *__restrict__ Y, int ntile, int tpx, int nkb, long long chunk_steps) {
-    constexpr int MB = 2 * MT, SB = 2 * ST, ROWS = MB + SB;  // staged 1 KiB rows per n
-    constexpr int RPT = ROWS / 4;                            // staged rows per wave
-    static_assert(ROWS % 4 == 0, "staged rows split over the 4 waves");
-    __shared__ float4 sm[2][ROWS * 64];
+template <int RG>
+__global__ void __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(2, 2)))
+k_zf_apply_ws16(const float2 *__restrict__ Wt, const float2 *__restrict__ X, int U, int R, int K, long long nsym,
+                float2 *__restrict__ Y, int nkb, int nrb, int ngroups, long long chunk_syms) {
+    constexpr int MT = 8, ST = 4, SGN = 8 / RG, MB = MT * RG;
+    extern __shared__ __attribute__((aligned(16))) float4 smw[];  // [U][MB][64]
     const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
-    const int tile = xcd + 8 * (j % tpx);
-    if (tile >= ntile) return;  // whole workgroup
-    const long long chunk = j / tpx;
-    const int kb = tile % nkb, rb = tile / nkb;
+    const int group = xcd + 8 * (j / nrb), rb = j % nrb;
+    if (group >= ngroups) return;  // whole workgroup
+    const int kb = group % nkb;
+    const long long chunk = group / nkb;
+    const long long sbeg = chunk * chunk_syms, send = min(sbeg + chunk_syms, nsym);
+    if (sbeg >= send) return;  // whole workgroup
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int mg = w & 1, sg = w >> 1;
-    const int k = kb * 128 + 2 * lane;                 // this lane's subcarriers k, k + 1
-    const int kc = k + 1 < K ? k : (K >= 2 ? K - 2 : 0);  // loads stay in range (K >= 2 here)
+    const int rg = w % RG, sg = w / RG;
+    const int k = kb * 128 + 2 * lane;
+    const bool pair = k + 1 < K, last = k == K - 1;  // last: K odd, this lane stores K-1 only
+    const int kc = pair ? k : (K >= 2 ? K - 2 : 0);  // every 16-B load in range
     const int r0 = rb * MB;
-    const long long nsteps_total = (nsym + SB - 1) / SB;
-    const long long step0 = chunk * chunk_steps, step1 = min(step0 + chunk_steps, nsteps_total);
-    if (step1 <= step0) return;  // whole workgroup
-    const int nst = (int)(step1 - step0);
 
-    // staged row i of wave w: row = w + 4 i; rows < MB are W(r0 + row, n),
-    // the others input rows (symbol s0 + row - MB, n)
-    float4 stg[RPT];
-    auto load = [&](int cs, int n) {
-        const long long s0 = (step0 + cs) * SB;
-#pragma unroll
-        for (int i = 0; i < RPT; ++i) {
-            const int row = w + 4 * i;
-            const float2 *p;
-            if (row < MB) {
-                const int r = min(r0 + row, R - 1);
-                p = Wt + ((long long)n * R + r) * K + kc;
-            } else {
-                const long long sy = min(s0 + (row - MB), nsym - 1);
-                p = X + (sy * U + n) * (long long)K + kc;
+    // W tile -> LDS; element (u, m) of this lane = W(r0 + m, u) at subcarriers (kc, kc + 1)
+    for (int e = w; e < U * MB; e += 8) {
+        const int u = e / MB, m = e % MB, r = r0 + m;
+        float4 v = float4{0.f, 0.f, 0.f, 0.f};
+        if (r < R) {
+            const float2 *p = Wt + ((long long)u * R + r) * K + kc;
+            if (pair) {
+                v = *reinterpret_cast<const float4 *>(p);  // 8-B aligned on odd rows: unaligned dwordx4
+            } else if (last) {
+                const float2 h = p[1];
+                v = float4{0.f, 0.f, h.x, h.y};
             }
-            stg[i] = *reinterpret_cast<const float4 *>(p);  // 8-byte aligned on odd rows: unaligned dwordx4
         }
-    };
-    auto put = [&](int buf) {
-#pragma unroll
-        for (int i = 0; i < RPT; ++i) sm[buf][(w + 4 * i) * 64 + lane] = stg[i];
-    };
-    float2 acc[MT][ST][2];
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int jj = 0; jj < ST; ++jj) acc[i][jj][0] = acc[i][jj][1] = float2{0.f, 0.f};
-    load(0, 0);
-    put(0);
+        smw[e * 64 + lane] = v;
+    }
     __syncthreads();
-    int cs = 0, n = 0, buf = 0;
-    for (;;) {
-        const int nn = n + 1 == U ? 0 : n + 1, ncs = n + 1 == U ? cs + 1 : cs;
-        const bool more = ncs < nst;
-        if (more) load(ncs, nn);  // in flight during this n's MACs
-        const float4 *sa = sm[buf] + (mg * MT) * 64 + lane;
-        const float4 *sx = sm[buf] + (MB + sg * ST) * 64 + lane;
-        float4 a[MT], x[ST];
+
+    const float4 *wl = smw + (rg * MT) * 64 + lane;  // + (u * MB + i) * 64
+    const int m0 = r0 + rg * MT;
+    const long long UK = (long long)U * K;
+    for (long long s0 = sbeg + (long long)sg * ST; s0 < send; s0 += (long long)SGN * ST) {
+        const float2 *xs[ST];
 #pragma unroll
-        for (int i = 0; i < MT; ++i) a[i] = sa[i * 64];
+        for (int q = 0; q < ST; ++q) xs[q] = X + min(s0 + q, send - 1) * UK + kc;
+        pk::v2f acc[MT][ST][2];
 #pragma unroll
-        for (int jj = 0; jj < ST; ++jj) x[jj] = sx[jj * 64];
+        for (int i = 0; i < MT; ++i)
 #pragma unroll
-        for (int i = 0; i < MT; ++i) {
+            for (int q = 0; q < ST; ++q) acc[i][q][0] = acc[i][q][1] = (pk::v2f){0.f, 0.f};
+        float4 xa[ST], xb[ST];
 #pragma unroll
-            for (int jj = 0; jj < ST; ++jj) {  // W(r, n) X(s, n) for both subcarriers
-                acc[i][jj][0].x = fmaf(a[i].x, x[jj].x, fmaf(-a[i].y, x[jj].y, acc[i][jj][0].x));
-                acc[i][jj][0].y = fmaf(a[i].x, x[jj].y, fmaf(a[i].y, x[jj].x, acc[i][jj][0].y));
-                acc[i][jj][1].x = fmaf(a[i].z, x[jj].z, fmaf(-a[i].w, x[jj].w, acc[i][jj][1].x));
-                acc[i][jj][1].y = fmaf(a[i].z, x[jj].w, fmaf(a[i].w, x[jj].z, acc[i][jj][1].y));
-            }
-        }
-        if (n == U - 1) {  // the symbol step's last input: store, reset
-            const long long s0 = (step0 + cs) * SB + sg * ST;
-            const int m0 = r0 + mg * MT;
-            if (k < K) {
-                float2 *o = Y + (s0 * R + m0) * (long long)K + k;
-                const bool pair = k + 1 < K;
+        for (int q = 0; q < ST; ++q) xa[q] = *reinterpret_cast<const float4 *>(xs[q]);
+        auto step = [&](int u, const float4 (&x)[ST]) {
 #pragma unroll
-                for (int jj = 0; jj < ST; ++jj) {
-                    if (s0 + jj >= nsym) break;
+            for (int i = 0; i < MT; ++i) {
+                const float4 wv = wl[(u * MB + i) * 64];
 #pragma unroll
-                    for (int i = 0; i < MT; ++i) {
-                        if (m0 + i >= R) break;
-                        float2 *q = o + (long long)(jj * R + i) * K;
-                        if (pair)
-                            *reinterpret_cast<float4 *>(q) =
-                                float4{acc[i][jj][0].x, acc[i][jj][0].y, acc[i][jj][1].x, acc[i][jj][1].y};
-                        else
-                            *q = acc[i][jj][0];
-                    }
+                for (int q = 0; q < ST; ++q) {
+                    pk::mac(acc[i][q][0], (pk::v2f){x[q].x, x[q].y}, (pk::v2f){wv.x, wv.y});
+                    pk::mac(acc[i][q][1], (pk::v2f){x[q].z, x[q].w}, (pk::v2f){wv.z, wv.w});
                 }
             }
+        };
+        int u = 0;
+        for (; u + 1 < U; u += 2) {
 #pragma unroll
-            for (int i = 0; i < MT; ++i)
+            for (int q = 0; q < ST; ++q) xb[q] = *reinterpret_cast<const float4 *>(xs[q] + (long long)(u + 1) * K);
+            step(u, xa);
+            if (u + 2 < U) {
 #pragma unroll
-                for (int jj = 0; jj < ST; ++jj) acc[i][jj][0] = acc[i][jj][1] = float2{0.f, 0.f};
+                for (int q = 0; q < ST; ++q) xa[q] = *reinterpret_cast<const float4 *>(xs[q] + (long long)(u + 2) * K);
+            }
+            step(u + 1, xb);
         }
-        if (!more) break;
-        buf ^= 1;
-        put(buf);  // that buffer was last read in the previous n
-        cs = ncs;
-        n = nn;
-        __syncthreads();
+        if (u < U) step(u, xa);  // U odd: xa holds u = U - 1
+        if (pair || last) {
+#pragma unroll
+            for (int q = 0; q < ST; ++q) {
+                if (s0 + q >= send) break;
+                float2 *o = Y + ((s0 + q) * R + m0) * (long long)K + kc;
+#pragma unroll
+                for (int i = 0; i < MT; ++i) {
+                    if (m0 + i >= R) break;
+                    float2 *y = o + (long long)i * K;
+                    const float2 lo = pk::F(acc[i][q][0]), hi = pk::F(acc[i][q][1]);
+                    if (pair)
+                        __builtin_nontemporal_store(mf4{lo.x, lo.y, hi.x, hi.y}, reinterpret_cast<mf4 *>(y));
+                    else
+                        __builtin_nontemporal_store(__builtin_bit_cast(unsigned long long, hi),
+                                                    reinterpret_cast<unsigned long long *>(y + 1));
+                }
+            }
+        }
     }
 }
 }  // namespace zf
@@ -1546,22 +1535,26 @@ hipError_t gemm_lds_launch(const float2 *Wt, int a_m, int a_n, const float2 *in,
 }
 
 
-// k_zf_apply16 (16-B lanes); MT x ST register tiles per wave
-template <int MT, int ST>
-hipError_t apply16_launch(const float2 *Wt, const float2 *X, int U, int R, int K, long long nsym, float2 *Y,
-                          hipStream_t s) {
-    constexpr int MB = 2 * MT, SB = 2 * ST;
+// k_zf_apply_ws16 (16-B lanes, W-stationary): RG row groups of 8 per tile
+template <int RG>
+hipError_t apply_ws16_launch(const float2 *Wt, const float2 *X, int U, int R, int K, long long nsym, float2 *Y,
+                             int target_groups, hipStream_t s) {
+    constexpr int MB = 8 * RG;
+    const size_t lds = (size_t)U * MB * 64 * sizeof(float4);
+    if (lds > 160 * 1024 || K < 2) return hipErrorInvalidValue;
     const int nkb = (K + 127) / 128, nrb = (R + MB - 1) / MB;
-    const int ntile = nkb * nrb, tpx = (ntile + 7) / 8;
-    const long long nsteps = (nsym + SB - 1) / SB;
-    long long nchunk = (2048 + 8LL * tpx - 1) / (8LL * tpx);
-    long long chunk_steps = (nsteps + nchunk - 1) / nchunk;
-    if (chunk_steps < 4) chunk_steps = 4;
-    nchunk = (nsteps + chunk_steps - 1) / chunk_steps;
-    const long long blocks = 8LL * tpx * nchunk;
+    long long nch = (target_groups + nkb - 1) / nkb;
+    if (nch < 1) nch = 1;
+    long long chunk_syms = (nsym + nch - 1) / nch;
+    chunk_syms = (chunk_syms + 31) / 32 * 32;  // whole 4-symbol steps of every wave
+    nch = (nsym + chunk_syms - 1) / chunk_syms;
+    const long long ngroups = nch * nkb;
+    const long long blocks = 8LL * ((ngroups + 7) / 8) * nrb;
     if (blocks > 0x7fffffffll) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((zf::k_zf_apply16<MT, ST>), dim3((unsigned)blocks), dim3(256), 0, s, Wt, X, U, R, K, nsym, Y,
-                       ntile, tpx, nkb, chunk_steps);
+    auto kern = zf::k_zf_apply_ws16<RG>;
+    if (hipError_t e = opt_in_lds(reinterpret_cast<const void *>(kern), (int)lds); e != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(512), lds, s, Wt, X, U, R, K, nsym, Y, nkb, nrb,
+                       (int)ngroups, chunk_syms);
     return hipGetLastError();
 }
 
@@ -1748,10 +1741,11 @@ hipError_t launch_zf_apply(const float2 *Wt, const float2 *X, int U, int R, int 
                            float2 *Y, hipStream_t s) {
     if (K == 0 || nsym == 0) return hipSuccess;
 #ifdef OFDM_AB_KNOBS
-    switch (ab_knob("ZF_A16", 0)) {  // 16-B lane apply candidates (MT x ST tiles)
-        case 1: if (K >= 2) return apply16_launch<8, 4>(Wt, X, U, R, K, nsym, Y, s); break;
-        case 2: if (K >= 2) return apply16_launch<4, 8>(Wt, X, U, R, K, nsym, Y, s); break;
-        case 3: if (K >= 2) return apply16_launch<4, 4>(Wt, X, U, R, K, nsym, Y, s); break;
+    switch (ab_knob("ZF_A16", 0)) {  // 16-B lane W-stationary apply: row groups x target (chunk, block) groups
+        case 1: if (K >= 2 && U <= 20) return apply_ws16_launch<1>(Wt, X, U, R, K, nsym, Y, 64, s); break;
+        case 2: if (K >= 2 && U <= 20) return apply_ws16_launch<1>(Wt, X, U, R, K, nsym, Y, 128, s); break;
+        case 3: if (K >= 2 && U <= 20) return apply_ws16_launch<1>(Wt, X, U, R, K, nsym, Y, 32, s); break;
+        case 4: if (K >= 2 && U <= 10) return apply_ws16_launch<2>(Wt, X, U, R, K, nsym, Y, 64, s); break;
         default: break;
     }
 #endif

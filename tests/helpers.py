@@ -14,7 +14,7 @@ GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 RTOL = 1e-5
 
 
-def parity(got, ref, rtol=RTOL):
+def parity(got, ref, rtol=RTOL, erel_tol=None):
     got = np.asarray(got, np.complex128).ravel()
     ref = np.asarray(ref, np.complex128).ravel()
     assert got.shape == ref.shape, (got.shape, ref.shape)
@@ -25,7 +25,8 @@ def parity(got, ref, rtol=RTOL):
     rms = np.sqrt(np.mean(np.abs(ref) ** 2))
     erel = np.max(np.abs(got - ref) / np.maximum(np.abs(ref), rms))
     assert nrel <= rtol, f"norm-relative error {nrel:.3e} > {rtol:g}"
-    assert erel <= rtol, f"element-wise relative error {erel:.3e} > {rtol:g}"
+    etol = rtol if erel_tol is None else erel_tol
+    assert erel <= etol, f"element-wise relative error {erel:.3e} > {etol:g}"
     return nrel, erel
 
 
