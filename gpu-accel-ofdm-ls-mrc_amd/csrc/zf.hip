@@ -1341,11 +1341,11 @@ k_zf_wstat(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__rest
 // matches within the parity tolerance, not bit for bit).  K odd: the last
 // lane covers subcarriers (K-2, K-1) with W(K-2) zeroed and stores only K-1.
 // ---------------------------------------------------------------------------
-template <int RG>
-__global__ void __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(2, 2)))
+template <int MT, int RG, int ST, int NW>
+__global__ void __attribute__((amdgpu_flat_work_group_size(64 * NW, 64 * NW), amdgpu_waves_per_eu(NW / 4, NW / 4)))
 k_zf_apply_ws16(const float2 *__restrict__ Wt, const float2 *__restrict__ X, int U, int R, int K, long long nsym,
                 float2 *__restrict__ Y, int nkb, int nrb, int ngroups, long long chunk_syms) {
-    constexpr int MT = 8, ST = 4, SGN = 8 / RG, MB = MT * RG;
+    constexpr int SGN = NW / RG, MB = MT * RG;
     extern __shared__ __attribute__((aligned(16))) float4 smw[];  // [U][MB][64]
     const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
     const int group = xcd + 8 * (j / nrb), rb = j % nrb;
@@ -1363,7 +1363,7 @@ k_zf_apply_ws16(const float2 *__restrict__ Wt, const float2 *__restrict__ X, int
     const int r0 = rb * MB;
 
     // W tile -> LDS; element (u, m) of this lane = W(r0 + m, u) at subcarriers (kc, kc + 1)
-    for (int e = w; e < U * MB; e += 8) {
+    for (int e = w; e < U * MB; e += NW) {
         const int u = e / MB, m = e % MB, r = r0 + m;
         float4 v = float4{0.f, 0.f, 0.f, 0.f};
         if (r < R) {
@@ -1535,25 +1535,26 @@ hipError_t gemm_lds_launch(const float2 *Wt, int a_m, int a_n, const float2 *in,
 }
 
 
-// k_zf_apply_ws16 (16-B lanes, W-stationary): RG row groups of 8 per tile
-template <int RG>
+// k_zf_apply_ws16 (16-B lanes, W-stationary): NW waves, RG row groups of MT
+// rows per tile, ST symbols per wave step
+template <int MT, int RG, int ST, int NW>
 hipError_t apply_ws16_launch(const float2 *Wt, const float2 *X, int U, int R, int K, long long nsym, float2 *Y,
                              int target_groups, hipStream_t s) {
-    constexpr int MB = 8 * RG;
+    constexpr int MB = MT * RG, WSTEP = NW / RG * ST;
     const size_t lds = (size_t)U * MB * 64 * sizeof(float4);
     if (lds > 160 * 1024 || K < 2) return hipErrorInvalidValue;
     const int nkb = (K + 127) / 128, nrb = (R + MB - 1) / MB;
     long long nch = (target_groups + nkb - 1) / nkb;
     if (nch < 1) nch = 1;
     long long chunk_syms = (nsym + nch - 1) / nch;
-    chunk_syms = (chunk_syms + 31) / 32 * 32;  // whole 4-symbol steps of every wave
+    chunk_syms = (chunk_syms + WSTEP - 1) / WSTEP * WSTEP;  // whole steps of every wave
     nch = (nsym + chunk_syms - 1) / chunk_syms;
     const long long ngroups = nch * nkb;
     const long long blocks = 8LL * ((ngroups + 7) / 8) * nrb;
     if (blocks > 0x7fffffffll) return hipErrorInvalidValue;
-    auto kern = zf::k_zf_apply_ws16<RG>;
+    auto kern = zf::k_zf_apply_ws16<MT, RG, ST, NW>;
     if (hipError_t e = opt_in_lds(reinterpret_cast<const void *>(kern), (int)lds); e != hipSuccess) return e;
-    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(512), lds, s, Wt, X, U, R, K, nsym, Y, nkb, nrb,
+    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(64 * NW), lds, s, Wt, X, U, R, K, nsym, Y, nkb, nrb,
                        (int)ngroups, chunk_syms);
     return hipGetLastError();
 }
@@ -1741,14 +1742,24 @@ hipError_t launch_zf_apply(const float2 *Wt, const float2 *X, int U, int R, int 
                            float2 *Y, hipStream_t s) {
     if (K == 0 || nsym == 0) return hipSuccess;
 #ifdef OFDM_AB_KNOBS
-    switch (ab_knob("ZF_A16", 0)) {  // 16-B lane W-stationary apply: row groups x target (chunk, block) groups
-        case 1: if (K >= 2 && U <= 20) return apply_ws16_launch<1>(Wt, X, U, R, K, nsym, Y, 64, s); break;
-        case 2: if (K >= 2 && U <= 20) return apply_ws16_launch<1>(Wt, X, U, R, K, nsym, Y, 128, s); break;
-        case 3: if (K >= 2 && U <= 20) return apply_ws16_launch<1>(Wt, X, U, R, K, nsym, Y, 32, s); break;
-        case 4: if (K >= 2 && U <= 10) return apply_ws16_launch<2>(Wt, X, U, R, K, nsym, Y, 64, s); break;
+    switch (ab_knob("ZF_A16", 0)) {  // W-stationary 16-B lane tiles <MT, RG, ST, NW>, target groups; -1: round-2 kernels
+        case -1: return gemm_dispatch<false>(Wt, 1, R, X, U, R, K, nsym, Y, s);
+        case 3: if (K >= 2 && U <= 20) return apply_ws16_launch<8, 1, 4, 8>(Wt, X, U, R, K, nsym, Y, 32, s); break;
+        case 5: if (K >= 2 && U <= 20) return apply_ws16_launch<8, 1, 2, 16>(Wt, X, U, R, K, nsym, Y, 32, s); break;
+        case 6: if (K >= 2 && U <= 20) return apply_ws16_launch<8, 1, 2, 16>(Wt, X, U, R, K, nsym, Y, 64, s); break;
+        case 7: if (K >= 2 && U <= 10) return apply_ws16_launch<8, 2, 2, 16>(Wt, X, U, R, K, nsym, Y, 64, s); break;
+        case 9: if (K >= 2 && U <= 40) return apply_ws16_launch<4, 1, 4, 16>(Wt, X, U, R, K, nsym, Y, 32, s); break;
         default: break;
     }
 #endif
+    // 16-B lanes, W-stationary (k_zf_apply_ws16): 8-row tiles up to U = 20
+    // (W tile U x 8 KiB of LDS), 4-row tiles with 8-symbol steps up to U = 40;
+    // same-process A/B at R = 64, K = 1023, 10 000 symbols:
+    // U = 4 / 8 / 16 / 24 / 32: 1.82 / 1.96 / 2.38 / 3.16 / 4.42 ms -> 1.50 /
+    // 1.53 / 1.94-1.96 / 2.93 / 3.58 ms.  Fewer than 8 antenna rows fill less
+    // than one 8-row tile: the register-tiled kernels below.
+    if (K >= 2 && R >= 8 && U <= 20) return apply_ws16_launch<8, 1, 4, 8>(Wt, X, U, R, K, nsym, Y, 64, s);
+    if (K >= 2 && R >= 8 && U <= 40) return apply_ws16_launch<4, 1, 8, 8>(Wt, X, U, R, K, nsym, Y, 32, s);
     return gemm_dispatch<false>(Wt, 1, R, X, U, R, K, nsym, Y, s);
 }
 

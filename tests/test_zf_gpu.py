@@ -51,8 +51,9 @@ def test_zf_precoder_single_output(ofdm, dev):
 # The shapes select every kernel of the shape-based dispatch (zf.hip
 # gemm_dispatch): detect -- register tiles (U <= 8 or R < 8), W-stationary
 # MFMA (U > 8, R <= 72), 8-wave MFMA (U > 16, R > 72), 128-subcarrier MFMA
-# (8 < U <= 16, R > 72); apply -- register tiles (U < 8 or R <= 4), LDS tiles,
-# W-stationary MFMA (32 <= U <= 72).
+# (8 < U <= 16, R > 72); apply -- 16-B-lane W-stationary tiles (R >= 8 and
+# K >= 2: 8-row tiles for U <= 20, 4-row tiles for U <= 40; K odd exercises the
+# lane that stores subcarrier K-1 alone), register tiles (R < 8 or K < 2).
 @pytest.mark.parametrize("U,R,K,n", [(1, 1, 5, 1), (2, 4, 1023, 7), (3, 5, 64, 9), (4, 16, 1023, 33),
                                      (5, 12, 130, 17), (8, 64, 1023, 40), (12, 40, 200, 16),
                                      (16, 64, 1023, 100), (17, 64, 65, 3), (32, 64, 255, 25),
