@@ -1341,17 +1341,29 @@ k_zf_wstat(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__rest
 // matches within the parity tolerance, not bit for bit).  K odd: the last
 // lane covers subcarriers (K-2, K-1) with W(K-2) zeroed and stores only K-1.
 // ---------------------------------------------------------------------------
-template <int MT, int RG, int ST, int NW>
+template <int MT, int RG, int ST, int NW, int XM = 0>
 __global__ void __attribute__((amdgpu_flat_work_group_size(64 * NW, 64 * NW), amdgpu_waves_per_eu(NW / 4, NW / 4)))
 k_zf_apply_ws16(const float2 *__restrict__ Wt, const float2 *__restrict__ X, int U, int R, int K, long long nsym,
                 float2 *__restrict__ Y, int nkb, int nrb, int ngroups, long long chunk_syms) {
     constexpr int SGN = NW / RG, MB = MT * RG;
     extern __shared__ __attribute__((aligned(16))) float4 smw[];  // [U][MB][64]
     const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
-    const int group = xcd + 8 * (j / nrb), rb = j % nrb;
-    if (group >= ngroups) return;  // whole workgroup
-    const int kb = group % nkb;
-    const long long chunk = group / nkb;
+    int kb, rb;
+    long long chunk;
+    if constexpr (XM == 0) {  // (chunk, subcarrier block) groups round-robin over the XCDs
+        const int group = xcd + 8 * (j / nrb);
+        rb = j % nrb;
+        if (group >= ngroups) return;  // whole workgroup
+        kb = group % nkb;
+        chunk = group / nkb;
+    } else {  // A/B: every block of a chunk on one XCD (XM 1: row blocks adjacent, 2: subcarrier blocks adjacent)
+        const int per = nkb * nrb;
+        chunk = xcd + 8LL * (j / per);
+        const int jj = j % per;
+        rb = XM == 1 ? jj % nrb : jj / nkb;
+        kb = XM == 1 ? jj / nrb : jj % nkb;
+        if (chunk * nkb >= ngroups) return;  // whole workgroup
+    }
     const long long sbeg = chunk * chunk_syms, send = min(sbeg + chunk_syms, nsym);
     if (sbeg >= send) return;  // whole workgroup
     const int lane = threadIdx.x & 63;
@@ -1537,7 +1549,7 @@ hipError_t gemm_lds_launch(const float2 *Wt, int a_m, int a_n, const float2 *in,
 
 // k_zf_apply_ws16 (16-B lanes, W-stationary): NW waves, RG row groups of MT
 // rows per tile, ST symbols per wave step
-template <int MT, int RG, int ST, int NW>
+template <int MT, int RG, int ST, int NW, int XM = 0>
 hipError_t apply_ws16_launch(const float2 *Wt, const float2 *X, int U, int R, int K, long long nsym, float2 *Y,
                              int target_groups, hipStream_t s) {
     constexpr int MB = MT * RG, WSTEP = NW / RG * ST;
@@ -1550,9 +1562,9 @@ hipError_t apply_ws16_launch(const float2 *Wt, const float2 *X, int U, int R, in
     chunk_syms = (chunk_syms + WSTEP - 1) / WSTEP * WSTEP;  // whole steps of every wave
     nch = (nsym + chunk_syms - 1) / chunk_syms;
     const long long ngroups = nch * nkb;
-    const long long blocks = 8LL * ((ngroups + 7) / 8) * nrb;
+    const long long blocks = XM == 0 ? 8LL * ((ngroups + 7) / 8) * nrb : 8LL * ((nch + 7) / 8) * nkb * nrb;
     if (blocks > 0x7fffffffll) return hipErrorInvalidValue;
-    auto kern = zf::k_zf_apply_ws16<MT, RG, ST, NW>;
+    auto kern = zf::k_zf_apply_ws16<MT, RG, ST, NW, XM>;
     if (hipError_t e = opt_in_lds(reinterpret_cast<const void *>(kern), (int)lds); e != hipSuccess) return e;
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(64 * NW), lds, s, Wt, X, U, R, K, nsym, Y, nkb, nrb,
                        (int)ngroups, chunk_syms);
@@ -1748,6 +1760,9 @@ hipError_t launch_zf_apply(const float2 *Wt, const float2 *X, int U, int R, int 
         case 5: if (K >= 2 && U <= 20) return apply_ws16_launch<8, 1, 2, 16>(Wt, X, U, R, K, nsym, Y, 32, s); break;
         case 6: if (K >= 2 && U <= 20) return apply_ws16_launch<8, 1, 2, 16>(Wt, X, U, R, K, nsym, Y, 64, s); break;
         case 7: if (K >= 2 && U <= 10) return apply_ws16_launch<8, 2, 2, 16>(Wt, X, U, R, K, nsym, Y, 64, s); break;
+        case 10: if (K >= 2 && U <= 20) return apply_ws16_launch<8, 1, 4, 8, 1>(Wt, X, U, R, K, nsym, Y, 64, s); break;
+        case 11: if (K >= 2 && U <= 20) return apply_ws16_launch<8, 1, 4, 8, 2>(Wt, X, U, R, K, nsym, Y, 64, s); break;
+        case 12: if (K >= 2 && U <= 20) return apply_ws16_launch<8, 1, 4, 8, 1>(Wt, X, U, R, K, nsym, Y, 128, s); break;
         case 9: if (K >= 2 && U <= 40) return apply_ws16_launch<4, 1, 4, 16>(Wt, X, U, R, K, nsym, Y, 32, s); break;
         default: break;
     }
