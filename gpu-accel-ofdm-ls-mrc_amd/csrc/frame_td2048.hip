@@ -293,12 +293,20 @@ k_mrc_td2048(const float2 *__restrict__ iq, int S, int R, int prefix, const floa
     // contiguous 512-B nontemporal wave stores (instead of 32 scattered ones)
     if ((mode & 1) == 0) {
         const float *Pf = P + f * C;
+        // all 16 |H|^2 pairs in flight before the first divide (left to
+        // itself the compiler issues each load just before its use, behind a
+        // vmcnt(0) wait: 16 serial L2 round trips per symbol)
+        float2 pv[16];
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             const int be = 2 * (b0 + 16 * k);
-            const float pe = Pf[be], po = Pf[be + 1];  // Pf[0] = 1: the DC slot
-            ae[k] = float2{ae[k].x / pe, ae[k].y / pe};
-            ao[k] = float2{ao[k].x / po, ao[k].y / po};
+            pv[k] = *reinterpret_cast<const float2 *>(Pf + be);  // Pf[0] = 1: the DC slot
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            ae[k] = float2{ae[k].x / pv[k].x, ae[k].y / pv[k].x};
+            ao[k] = float2{ao[k].x / pv[k].y, ao[k].y / pv[k].y};
         }
     }
 #pragma unroll
