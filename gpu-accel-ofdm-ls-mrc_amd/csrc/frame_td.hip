@@ -210,6 +210,61 @@ __device__ __forceinline__ void hlds_rows(const float2 *sym, int Cp, int R, cons
     }
 }
 
+// Epilogue of one symbol (mode 0: normalise by P): stage the K outputs in
+// this wave's transpose image (free after the last row; its padding tails
+// still hold other waves' Hc words, so index it as [16][TP]) at their final
+// positions, then store them as 16 contiguous 512-B nontemporal wave stores
+// instead of 4 scattered 128-B runs per instruction.
+template <int DBG = 0>
+__device__ __forceinline__ void hlds_epilogue(const float2 (&acc)[16], const float *P, long long f, long long q,
+                                              int t, float2 *T, float2 *__restrict__ out, int mode) {
+    if (DBG & 4) {  // diagnostic: no output stores (keep the sums live)
+        float sacc = 0.f;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) sacc += acc[k].x * acc[k].y;
+        if (sacc == 1234.5f) out[q] = float2{sacc, 0.f};
+        return;
+    }
+    const int b0 = lane_bin0(t);
+    float2 *o = out + q * K;
+    const float *Pf = P + f * C + b0;
+    // all 16 |H|^2 loads issued before the first use (under the DC-bin
+    // condition the compiler issued them one at a time, each behind a
+    // vmcnt(0) wait; neutral at 4 waves/SIMD)
+    float pv[16];
+    if ((mode & 1) == 0 && !(DBG & 16)) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) pv[k] = Pf[16 * k];
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int b = b0 + 16 * k;
+        float2 v = acc[k];
+        int j = b - 1;
+        if ((mode & 1) == 0) {
+            if (!(DBG & 16)) v = float2{acc[k].x / pv[k], acc[k].y / pv[k]};
+            j = out_pos(b > 0 ? b - 1 : 0, K);
+        }
+        if (b > 0) T[(j >> 6) * hlds::TP + (j & 63)] = v;
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        const int j = t + 64 * m;
+        if (j < K) {
+            const float2 v = T[m * hlds::TP + t];
+            if (DBG & 8) {  // diagnostic: the epilogue without its global stores
+                if (v.x == 1234.5f) o[j] = v;
+            } else if (DBG & 32) {  // A/B: plain stores
+                o[j] = v;
+            } else {  // nontemporal (streaming) stores: 2-3 % faster than plain ones
+                __builtin_nontemporal_store(__builtin_bit_cast(unsigned long long, v),
+                                            reinterpret_cast<unsigned long long *>(o + j));
+            }
+        }
+    }
+}
+
 // 8 waves = 8 consecutive data symbols per workgroup, XCD-grouped block order
 // (blocks b and b+8 share an XCD under round-robin dispatch, so a frame's
 // workgroups share its Hc rows in one L2; speed only, never correctness).
@@ -256,52 +311,7 @@ k_mrc_td1024_hlds(const float2 *__restrict__ iq, int S, int R, int prefix, const
         hlds_rows<false>(sym, Cp, R, reinterpret_cast<const float4 *>(Hc + f * (long long)R * C), t, T, tw1,
                          tw2, T0, hfree, acc);
     if (!store) return;
-    if (DBG & 4) {  // diagnostic: no output stores (keep the sums live)
-        float sacc = 0.f;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) sacc += acc[k].x * acc[k].y;
-        if (sacc == 1234.5f) out[q] = float2{sacc, 0.f};
-        return;
-    }
-    // Stage the K outputs in this wave's transpose image (free after the last
-    // row; its padding tails still hold other waves' Hc words, so index it as
-    // [16][TP]) at their final positions, then store them as 16 contiguous
-    // 512-B nontemporal wave stores instead of 4 scattered 128-B runs per
-    // instruction.
-    const int b0 = lane_bin0(t);
-    float2 *o = out + q * K;
-    const float *Pf = P + f * C + b0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const int b = b0 + 16 * k;
-        if (b == 0) continue;
-        float2 v = acc[k];
-        int j = b - 1;
-        if ((mode & 1) == 0) {
-            if (!(DBG & 16)) {
-                const float pv = Pf[16 * k];
-                v = float2{acc[k].x / pv, acc[k].y / pv};
-            }
-            j = out_pos(b - 1, K);
-        }
-        T[(j >> 6) * hlds::TP + (j & 63)] = v;
-    }
-    wave_lds_sync();
-#pragma unroll
-    for (int m = 0; m < 16; ++m) {
-        const int j = t + 64 * m;
-        if (j < K) {
-            const float2 v = T[m * hlds::TP + t];
-            if (DBG & 8) {  // diagnostic: the epilogue without its global stores
-                if (v.x == 1234.5f) o[j] = v;
-            } else if (DBG & 32) {  // A/B: plain stores
-                o[j] = v;
-            } else {  // nontemporal (streaming) stores: 2-3 % faster than plain ones
-                __builtin_nontemporal_store(__builtin_bit_cast(unsigned long long, v),
-                                            reinterpret_cast<unsigned long long *>(o + j));
-            }
-        }
-    }
+    hlds_epilogue<DBG>(acc, P, f, q, t, T, out, mode);
 }
 
 
