@@ -7,13 +7,16 @@ sharded by symbol index (no RCCL), per-GPU hipStreams"): each GPU holds
 `--frames` frames (default 1250) of S = 101 symbols (1 pilot + 100 data,
 lenOfBuffer of ShMemSymBuff_gpu.hpp:74) x R = 64 antennas x C = 1024
 time-domain IQ samples, synthetic, resident in HBM (66 GB per GPU).  One step =
-ofdm_frame_estimate (pilot FFT + LS) + ofdm_frame_combine (FFT + MRC +
-normalise + rotate) over the whole batch: 125,000 data symbols per GPU, 1M at
-8 GPUs (weak scaling, frame-sharded, no collective on the data path).
+ofdm_frame_demod over the whole batch (pilot FFT + LS, FFT + MRC + normalise +
+rotate): 125,000 data symbols per GPU, 1M at 8 GPUs (weak scaling,
+frame-sharded, no collective on the data path).  At C = 1024 that is ONE
+launch (k_demod_td1024: estimator and MRC workgroups in one grid); --flow two
+runs and times ofdm_frame_estimate + ofdm_frame_combine separately.
 
 value = data symbols demodulated per second, whole job (all ranks).
-roofline: dominant kernel (MRC), algorithmic bytes per data symbol
-  B_sym = R*C*8 (IQ read once) + K*8 (output written once)  
+roofline: dominant kernel, algorithmic bytes per data symbol
+  B_sym = R*C*8 (IQ read once) + K*8 (output written once), for the
+  one-launch kernel + R*C*8 + K*8 per frame (pilot symbol, pilot vector),
   divided by its HIP-event-measured average launch time, vs 8 TB/s HBM3E.
 cpu_baseline: the oracle's C restatement of cpuLS.hpp (oracle/) with its
   single-precision radix-2 FFT (the reference's fftwf precision; the parity
@@ -60,6 +63,10 @@ def parse():
     ap.add_argument("--chunk", type=int, default=None,
                     help="frames per pipelined chunk (split: 50, pcie: 4)")
     ap.add_argument("--prefix", type=int, default=0)
+    ap.add_argument("--flow", choices=["auto", "one", "two"], default="auto",
+                    help="frames mode: 'one' = ofdm_frame_demod (LS and MRC in one launch, C = 1024), "
+                         "'two' = ofdm_frame_estimate + ofdm_frame_combine timed separately; auto: one at "
+                         "C = 1024 in the time domain, else two")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--noise", type=float, default=0.01)
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
@@ -144,7 +151,9 @@ def pmc_traffic(path, cfg):
     """Corrected PMC HBM bytes per MRC launch for this exact config: `path`
     (profiles/pmc_traffic.json, the default shape) or else the latest-tagged
     profiles/r*_traffic.json written by scripts/pmc_summary.py for it."""
-    cands = [path] + sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")), reverse=True)
+    cands = [path] + sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")) +
+                            glob.glob(os.path.join(ROOT, "profiles", "r*", "r*_traffic.json")),
+                            key=os.path.basename, reverse=True)
     for p in cands:
         try:
             with open(p) as fp:
@@ -153,7 +162,8 @@ def pmc_traffic(path, cfg):
             continue
         dc = d.get("config", {})
         if all(dc.get(k) == cfg[k] for k in ("R", "C", "S", "frames_per_gpu", "prefix")) and \
-                dc.get("domain", "time") == cfg["domain"]:
+                dc.get("domain", "time") == cfg["domain"] and \
+                dc.get("flow", "two-launch") == cfg.get("flow", "two-launch"):
             return d.get("mrc_hbm_bytes_per_launch"), os.path.relpath(p, ROOT)
     return None, None
 
@@ -219,12 +229,22 @@ def main():
     log(f"[rank {rank}] synthesised {iq.numel() * 8 / 1e9:.1f} GB in {time.perf_counter() - t:.1f} s")
 
     stream = torch.cuda.current_stream()
+    one = args.flow == "one" or (args.flow == "auto" and not freq and C == 1024)
+    if one and (freq or C != 1024):
+        raise SystemExit("--flow one: C = 1024, time domain only")
 
     # Two HIP events per step on the launch stream: after the estimate (LS)
     # and after the combine (MRC).  The LS of step i is timed from step i-1's
     # end event (one event before the loop for i = 0), so no event sits
     # between two steps' kernels beyond the one the MRC timing needs.
+    # One-launch flow: the step is ofdm_frame_demod (k_demod_td1024, LS and
+    # MRC in one grid), timed from the previous step's end event.
     def step(evs=None):
+        if one:
+            ofdm.frame_demod(iq, X, prefix, ws=ws, out=out, stream=stream)
+            if evs:
+                evs[2].record(stream)
+            return
         if freq:
             ofdm.frame_estimate_freq(iq, X, ws, stream)
         else:
@@ -257,8 +277,8 @@ def main():
     elapsed = time.perf_counter() - t0
     barrier()
 
-    ls_ms = sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
-    mrc_all = sorted(e[1].elapsed_time(e[2]) for e in events)
+    ls_ms = None if one else sum(e[0].elapsed_time(e[1]) for e in events) / args.steps
+    mrc_all = sorted(e[0 if one else 1].elapsed_time(e[2]) for e in events)
     mrc_ms = sum(mrc_all) / args.steps
     mrc_median = mrc_all[len(mrc_all) // 2]
     stats = torch.tensor([elapsed, float(errs)], dtype=torch.float64, device=dev)
@@ -275,13 +295,18 @@ def main():
            "domain": "freq" if freq else "time",
            "R": R, "C": C, "S": S, "prefix": prefix, "frames_per_gpu": F,
            "data_symbols_per_gpu": Q, "global_data_symbols": Q * world,
+           "flow": "one-launch" if one else "two-launch",
            "parallelism": f"frame-sharded x{world}, no collective"}
     b_sym = R * C * 8 + K * 8
     kern = {1024: "k_mrc_td1024_hlds", 2048: "k_mrc_td2048", 4096: "k_mrc_td4096h"}.get(C)
     mrc_name = f"{kern} (FFT+MRC+normalise+rotate)" if kern else "k_fft_rows + k_mrc_freq (staged)"
     if freq:
         mrc_name = "k_mrc_freq_frames (MRC+normalise+rotate)" if C >= 512 else "k_mrc_freq (MRC+normalise+rotate)"
-    achieved = Q * b_sym / (mrc_ms * 1e-3) / 1e9
+    bytes_launch = Q * b_sym
+    if one:  # + the pilot symbol and pilot vector per frame
+        mrc_name = "k_demod_td1024 (LS + FFT+MRC+normalise+rotate, one launch)"
+        bytes_launch += F * (R * C * 8 + K * 8)
+    achieved = bytes_launch / (mrc_ms * 1e-3) / 1e9
     traffic, tsrc = pmc_traffic(args.pmc, cfg)
     step_bytes = F * S * R * C * 8 + Q * K * 8
     result = {
@@ -302,9 +327,9 @@ def main():
                      "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                      "traffic_source": tsrc,
-                     "bytes_per_launch": Q * b_sym, "avg_launch_ms": mrc_ms,
+                     "bytes_per_launch": bytes_launch, "avg_launch_ms": mrc_ms,
                      "median_launch_ms": mrc_median},
-        "stages_ms": {"estimate_ls": ls_ms, "combine_mrc": mrc_ms},
+        "stages_ms": {"demod_one_launch": mrc_ms} if one else {"estimate_ls": ls_ms, "combine_mrc": mrc_ms},
         "step_algorithmic_GBps": step_bytes / (elapsed / args.steps) / 1e9,
         "check": {"qpsk_symbol_errors": errs},
         "cpu_baseline": None,

@@ -2,11 +2,13 @@
 // reporting, workspace carving and kernel dispatch.  Compiled by hipcc as HIP.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <random>
 #include <string>
 
 #include "../../include/ofdm_lsmrc.h"
@@ -58,6 +60,29 @@ hipError_t mrc_fused(const float2 *iq, long long F, int S, int R, int C, int pre
     return ofdm::launch_mrc_td4096(iq, F, S, R, prefix, Hc, P, out, mode, s);
 }
 
+// ofdm_frame_demod at C = 1024 runs LS and MRC as ONE launch
+// (k_demod_td1024) unless the stream is being captured into a graph: its
+// per-launch flag epoch would be frozen in the graph, and a replay would
+// find every flag already set.
+bool one_launch_demod(int C, hipStream_t s) {
+    if (C != 1024 || !ofdm::ab_knob("DEMOD1K_FUSED", 1)) return false;
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &st) != hipSuccess) return false;
+    return st == hipStreamCaptureStatusNone;
+}
+
+// Per-launch flag values of the one-launch demod: 64 bits, never 0 and never
+// repeated in this process; the high half is drawn once per process so that
+// flags left in recycled memory by another process do not match either.
+unsigned long long next_epoch() {
+    static std::atomic<unsigned long long> ctr{0};
+    static const unsigned long long salt = [] {
+        std::random_device rd;
+        return ((unsigned long long)rd() << 32) | 0x80000000ull;
+    }();
+    return salt + (ctr.fetch_add(1) & 0x7fffffffull) + 1;
+}
+
 long long staging_frames(long long nframes, int S, int R, int C) {
     const long long per = (long long)S * R * C * (long long)sizeof(float2);
     long long n = (256ll << 20) / (per > 0 ? per : 1);
@@ -66,14 +91,16 @@ long long staging_frames(long long nframes, int S, int R, int C) {
 }
 
 struct Workspace {
-    float2 *Hc;       // [F][R][C] bin layout
-    float *P;         // [F][C]   bin layout
-    float2 *staging;  // [chunk][S][R][C] (non-fused C only)
+    float2 *Hc;                 // [F][R][C] bin layout
+    float *P;                   // [F][C]   bin layout
+    unsigned long long *flags;  // [F] per-frame estimate flags of the one-launch demod
+    float2 *staging;            // [chunk][S][R][C] (non-fused C only)
     long long chunk;
 };
 
 size_t ws_bytes(long long F, int S, int R, int C, bool need_staging) {
-    size_t b = up256((size_t)F * R * C * sizeof(float2)) + up256((size_t)F * C * sizeof(float));
+    size_t b = up256((size_t)F * R * C * sizeof(float2)) + up256((size_t)F * C * sizeof(float)) +
+               up256((size_t)F * sizeof(unsigned long long));
     if (need_staging) b += up256((size_t)staging_frames(F, S, R, C) * S * R * C * sizeof(float2));
     return b;
 }
@@ -89,6 +116,8 @@ int carve(void *d_ws, size_t bytes, long long F, int S, int R, int C, bool need_
     p += up256((size_t)F * R * C * sizeof(float2));
     w.P = reinterpret_cast<float *>(p);
     p += up256((size_t)F * C * sizeof(float));
+    w.flags = reinterpret_cast<unsigned long long *>(p);
+    p += up256((size_t)F * sizeof(unsigned long long));
     w.staging = need_staging ? reinterpret_cast<float2 *>(p) : nullptr;
     w.chunk = need_staging ? staging_frames(F, S, R, C) : F;
     return OFDM_OK;
@@ -401,6 +430,13 @@ int ofdm_frame_demod(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int
     if ((rc = carve(d_ws, ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
     hipStream_t s = hs(stream);
     ws_forget(d_ws);
+    if (one_launch_demod(C, s)) {
+        rc = hip_check(ofdm::launch_demod_td1024(F2(d_iq), nframes, S, R, prefix, F2(d_X), w.Hc, w.P, F2(d_out),
+                                                 w.flags, next_epoch(), s),
+                       "launch_demod_td1024");
+        if (rc == OFDM_OK) ws_record(d_ws, ws_bytes_, nframes, S, R, C, true, false);
+        return rc;
+    }
     if (fused_c(C)) {
         rc = hip_check(ls_fused(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w.Hc, w.P, 0, s),
                        "ls_fused");

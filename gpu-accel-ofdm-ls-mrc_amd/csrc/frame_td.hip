@@ -315,6 +315,195 @@ k_mrc_td1024_hlds(const float2 *__restrict__ iq, int S, int R, int prefix, const
 }
 
 
+// ---------------------------------------------------------------------------
+// One-launch frame demodulation (ofdm_frame_demod at C = 1024): the reference
+// runs demodOneFrameCUDA as dependent launches (gpuLS.cu:575-675); here the
+// LS of every frame and the MRC of every data symbol share ONE grid.
+// Workgroups 0 .. nls-1 (nls = nframes rounded up to 8, so the MRC blocks
+// keep their XCD grouping) each estimate one frame -- FFT of its R pilot
+// rows, Hc = conj(Y/X) into the workspace in lane order, P = sum_r |Hc|^2 --
+// and publish it with an agent-scope release and a 64-bit flag (cdna_hip_
+// programming.md Guideline 16, R1: plain stores, every storing wave's
+// vmcnt(0), barrier, one lane's release fence + vmcnt(0) + relaxed agent
+// flag store).  The MRC workgroups behind them poll the flags of the (one or
+// two) frames they read with one lane, relaxed, then ONE agent acquire, a
+// vmcnt(0) and a barrier before any Hc / P load.  Flags hold a per-launch
+// 64-bit epoch (never reused; a workspace's flags need no reset).  The wait
+// is bounded: a workgroup that has not seen its flag after SPIN_TICKS of
+// the 100 MHz wall clock estimates the frame itself (the same bytes) and
+// goes on, so no dispatch-order or residency assumption is needed for a
+// correct result -- in-order dispatch only makes the wait short.
+// ---------------------------------------------------------------------------
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+constexpr long long SPIN_TICKS = 200000;  // 2 ms at 100 MHz (A/B build: OFDM_AB_DEMOD1K_SPIN)
+
+// LS of frame f by one 8-wave workgroup in the HLDS LDS layout (tables
+// filled): wave w takes rows w, w + 8, ...; partial |H|^2 added in wave
+// order through the transpose images (the k_ls_td1024<8> order).
+template <bool WT>
+__device__ __forceinline__ void hlds_ls_frame(const float2 *__restrict__ iq, int S, int R, int prefix,
+                                              const float2 *__restrict__ X, float2 *Hc, float *P, long long f,
+                                              int w, int t, float2 *T, float2 *T0, const float2 *tw1,
+                                              const float2 *tw2) {
+    using namespace hlds;
+    const int Cp = C + prefix;
+    const float2 *pilot = iq + f * (long long)S * R * Cp + prefix;
+    float4 *Hf = reinterpret_cast<float4 *>(Hc + f * (long long)R * C);
+    const int b0 = lane_bin0(t);
+    float2 xp[16];  // rotated pilots of this lane's subcarriers
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int b = b0 + 16 * k;
+        xp[k] = b > 0 ? X[b - 1] : float2{1.f, 0.f};
+    }
+    float p[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) p[k] = 0.f;
+    for (int r = w; r < R; r += WAVES) {
+        float2 a[16], x[16];
+        row_load<true>(pilot + (long long)r * Cp, t, a);
+        row_fft_a(a, t, T, tw1);
+        row_fft_b(t, T, tw2, x);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            float2 h = ls_conj(x[k], xp[k]);  // divideOneRow + conj (cpuLS.hpp:233-244)
+            if (b0 + 16 * k == 0) h = float2{0.f, 0.f};
+            x[k] = h;
+            p[k] = p[k] + (h.x * h.x) + (h.y * h.y);
+        }
+        if constexpr (WT) {  // write-through (sc1, aux 16): visible at agent scope once vmcnt drains
+            // (a buffer store, not inline asm: the compiler must see the
+            // store-data VGPRs to resolve the VALU-write hazard in front of it)
+            typedef int v4i __attribute__((ext_vector_type(4)));
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(Hf, (short)0, R * C * 8, 0x00020000);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const v4i v = {__builtin_bit_cast(int, x[2 * i].x), __builtin_bit_cast(int, x[2 * i].y),
+                               __builtin_bit_cast(int, x[2 * i + 1].x), __builtin_bit_cast(int, x[2 * i + 1].y)};
+                __builtin_amdgcn_raw_buffer_store_b128(v, rs, (r * (C / 2) + i * 64 + t) * 16, 0, 16);
+            }
+        } else {
+            hc_store(Hf + (long long)r * (C / 2), t, x);
+        }
+    }
+    __syncthreads();  // every wave is done with its transpose image
+    float *pp = reinterpret_cast<float *>(T0);  // [WAVES][C], over the images
+#pragma unroll
+    for (int k = 0; k < 16; ++k) pp[w * C + b0 + 16 * k] = p[k];
+    __syncthreads();
+    float *Pf = P + f * C;
+    const int nw = R < WAVES ? R : WAVES;
+    for (int b = threadIdx.x; b < C; b += blockDim.x) {
+        float sum = pp[b];
+        for (int i = 1; i < nw; ++i) sum = sum + pp[i * C + b];
+        const float v = b == 0 ? 1.f : sum;
+        if constexpr (WT)
+            __hip_atomic_store((__attribute__((address_space(1))) unsigned *)(Pf + b), __builtin_bit_cast(unsigned, v),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else
+            Pf[b] = v;
+    }
+    __syncthreads();  // pp (the transpose images) read before they are reused
+}
+
+__device__ __forceinline__ bool wait_flag(unsigned long long *flag, unsigned long long epoch, long long ticks) {
+    const long long t0 = wall_clock64();
+    while (__hip_atomic_load((gu64 *)(flag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+        if (wall_clock64() - t0 >= ticks) return false;
+        __builtin_amdgcn_s_sleep(2);
+    }
+    return true;
+}
+
+// WT: the estimate is stored write-through (sc1: 16-B Hc stores, 4-B agent
+// atomic P stores) and published without the release fence, whose L2
+// write-back would also flush the output lines the MRC workgroups of the
+// same XCD left dirty (Guideline 16, R1 write-through form); else plain
+// stores + release fence.
+template <int DBG = 0, bool WT = true>
+__global__ void __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 4)))
+k_demod_td1024(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ X, float2 *Hc,
+               float *P, float2 *__restrict__ out, long long nq, long long nblocks, long long per_xcd,
+               unsigned long long *flags, unsigned long long epoch, int nls, long long nframes,
+               long long spin_ticks) {
+    using namespace hlds;
+    constexpr int HW = WAVES;
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    float2 *tw1 = lds, *tw2 = lds + TW1S;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), t = threadIdx.x & 63;
+    float2 *T = lds + TW1S + TW2S + w * TS;
+    float2 *T0 = lds + TW1S + TW2S;
+    float4 *hfree = reinterpret_cast<float4 *>(T0 + HW * TS);
+
+    if ((int)blockIdx.x < nls) {  // estimator workgroup
+        const long long f = blockIdx.x;
+        if (f >= nframes) return;
+        fill(tw1, tw2);
+        __syncthreads();
+        hlds_ls_frame<WT>(iq, S, R, prefix, X, Hc, P, f, w, t, T, T0, tw1, tw2);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's Hc and P stores
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            if constexpr (!WT) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store((gu64 *)(flags + f), epoch, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
+    }
+    const long long pb = blockIdx.x - nls;
+    const long long lb = (pb & 7) * per_xcd + (pb >> 3);  // XCD-grouped logical block
+    if (lb >= nblocks) return;
+    fill(tw1, tw2);
+
+    const int nsym = S - 1;
+    const long long qw = lb * HW + w;
+    const bool store = qw < nq;
+    const long long q = store ? qw : nq - 1;
+    const long long f = q / nsym;
+    const long long f0 = (lb * HW) / nsym;
+    const long long fl = ((lb * HW + HW - 1 < nq ? lb * HW + HW - 1 : nq - 1)) / nsym;
+    const int s = 1 + (int)(q % nsym);
+    const int Cp = C + prefix;
+    const float2 *sym = iq + (f * S + s) * (long long)R * Cp + prefix;
+
+    // wait for the estimates of frames f0 .. fl (one lane polls; hfree, not
+    // used before the rows, carries the outcome to the other waves)
+    int *seen = reinterpret_cast<int *>(hfree);
+    if (threadIdx.x == 0) {
+        const bool ok = wait_flag(flags + f0, epoch, spin_ticks) &&
+                        (fl == f0 || wait_flag(flags + fl, epoch, spin_ticks));
+        *seen = ok ? 1 : 0;
+        if (ok) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();  // tables filled; the acquire has completed
+    if (!*seen) {
+        // not published in time: estimate here (identical bytes), then read
+        // them back behind an acquire of our own
+        __syncthreads();  // every wave has read the word
+        for (long long ff = f0; ff <= fl; ++ff)
+            hlds_ls_frame<WT>(iq, S, R, prefix, X, Hc, P, ff, w, t, T, T0, tw1, tw2);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+    }
+
+    float2 acc[16];
+    if (f0 == fl)
+        hlds_rows<true, DBG>(sym, Cp, R, reinterpret_cast<const float4 *>(Hc + f0 * (long long)R * C), t, T, tw1,
+                             tw2, T0, hfree, acc);
+    else
+        hlds_rows<false>(sym, Cp, R, reinterpret_cast<const float4 *>(Hc + f * (long long)R * C), t, T, tw1, tw2,
+                         T0, hfree, acc);
+    if (!store) return;
+    hlds_epilogue<DBG>(acc, P, f, q, t, T, out, 0);
+}
+
 }  // namespace td1024
 
 hipError_t launch_ls_td1024(const float2 *iq, long long nframes, int S, int R, int prefix,
@@ -378,6 +567,28 @@ hipError_t launch_mrc_td1024(const float2 *iq, long long nframes, int S, int R, 
 #endif
     hipLaunchKernelGGL(kern, dim3((unsigned)(pxcd * 8)), dim3(64 * hlds::WAVES), hlds::LDS_BYTES, s, iq, S, R,
                        prefix, Hc, P, out, nq, nb, pxcd, mode);
+    return hipGetLastError();
+}
+
+// One-launch LS + MRC (ofdm_frame_demod, mode 0).  flags: nframes 64-bit
+// words of the workspace; epoch: a value none of them holds (per launch).
+hipError_t launch_demod_td1024(const float2 *iq, long long nframes, int S, int R, int prefix, const float2 *X,
+                               float2 *Hc, float *P, float2 *out, unsigned long long *flags,
+                               unsigned long long epoch, hipStream_t s) {
+    using namespace td1024;
+    const long long nq = nframes * (S - 1);
+    if (nq <= 0) return hipSuccess;
+    const long long nb = (nq + hlds::WAVES - 1) / hlds::WAVES;
+    const long long pxcd = (nb + 7) / 8;
+    const long long nls = (nframes + 7) / 8 * 8;
+    if (pxcd * 8 + nls > 0x7fffffffll) return hipErrorInvalidValue;
+    auto kern = k_demod_td1024<0, true>;
+#ifdef OFDM_AB_KNOBS
+    if (!ab_knob("DEMOD1K_WT", 1)) kern = k_demod_td1024<0, false>;  // plain stores + release fence
+#endif
+    hipLaunchKernelGGL(kern, dim3((unsigned)(nls + pxcd * 8)), dim3(64 * hlds::WAVES), hlds::LDS_BYTES, s, iq, S,
+                       R, prefix, X, Hc, P, out, nq, nb, pxcd, flags, epoch, (int)nls, nframes,
+                       (long long)ab_knob("DEMOD1K_SPIN", (int)SPIN_TICKS));
     return hipGetLastError();
 }
 

@@ -92,6 +92,13 @@ hipError_t launch_ls_td1024(const float2 *iq, long long nframes, int S, int R, i
 hipError_t launch_mrc_td1024(const float2 *iq, long long nframes, int S, int R, int prefix,
                              const float2 *Hc, const float *P, float2 *out, int mode,
                              hipStream_t s);
+// Both in one grid (frame_td.hip k_demod_td1024): estimator workgroups
+// publish each frame's estimate through flags[f] = epoch (agent scope), the
+// MRC workgroups wait for it.  flags: nframes words in the workspace; epoch:
+// a per-launch value no flag holds.  mode 0 (full demod) only.
+hipError_t launch_demod_td1024(const float2 *iq, long long nframes, int S, int R, int prefix, const float2 *X,
+                               float2 *Hc, float *P, float2 *out, unsigned long long *flags,
+                               unsigned long long epoch, hipStream_t s);
 
 // Stage-wise operations of the reference's per-stage gpuLS methods (stages.hip).
 // fused time-domain receiver, C = 2048 (frame_td2048.hip); same contracts

@@ -128,7 +128,9 @@ int ofdm_dist_sqrd(const ofdm_cf32 *d_H, int R, int K, float *d_Hsqrd, ofdm_stre
 
 /* Workspace for ofdm_frame_demod / ofdm_frame_demod_freq and the two-stage
  * and antenna-split calls (bytes, 256-aligned pieces): per-frame channel
- * estimates [F][R][C], |H|^2 [F][C] and, for C outside {1024, 2048, 4096}
+ * estimates [F][R][C], |H|^2 [F][C], one 64-bit word per frame (the
+ * estimate flags of the one-launch C = 1024 demod below) and, for C outside
+ * {1024, 2048, 4096}
  * (no fused kernel), a frequency-domain staging buffer of at most 256 MiB.
  * A workspace carries the estimate of ONE geometry: the calls that consume it
  * (ofdm_frame_combine, ofdm_frame_mrc_partial, ofdm_frame_export_estimate)
@@ -154,9 +156,12 @@ int ofdm_workspace_release(const void *d_ws);
  * d_out = nframes x (S-1) x K.  Replaces demodOneFrameCUDA / demodOptimized
  * (gpuLS.cu:575-769) and the cpuLS_main loop (cpuLS_main.cpp:80-92), for a
  * whole batch of frames in one call.  C in {1024, 2048, 4096} runs the fused
- * one-pass kernels (FFT + LS, FFT + MRC + normalise + rotate); other powers
- * of two run FFT, LS and MRC as stages through the workspace's staging
- * buffer. */
+ * one-pass kernels (FFT + LS, FFT + MRC + normalise + rotate); at C = 1024
+ * both run in ONE launch (estimator workgroups publish each frame's estimate
+ * to the MRC workgroups through the workspace's flag words, agent-scope
+ * release/acquire), except on a stream being captured into a graph, where
+ * the two launches are used.  Other powers of two run FFT, LS and MRC as
+ * stages through the workspace's staging buffer. */
 int ofdm_frame_demod(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, int cp_len,
                      const ofdm_cf32 *d_X, void *d_ws, size_t ws_bytes, ofdm_cf32 *d_out,
                      ofdm_stream_t stream);

@@ -29,6 +29,8 @@ ap.add_argument("--frames", type=int, default=400)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--partial", action="store_true", help="time frame_mrc_partial (numerators)")
 ap.add_argument("--ls", action="store_true", help="time frame_estimate (the LS kernel) instead of the MRC")
+ap.add_argument("--demod", action="store_true",
+                help="time frame_demod (LS + MRC: one launch at C = 1024 unless DEMOD1K_FUSED=0)")
 ap.add_argument("--freq", action="store_true",
                 help="frequency-domain frames: time frame_demod_freq (LS + MRC, no FFT)")
 ap.add_argument("--allocs", type=int, default=1,
@@ -77,6 +79,9 @@ def run():
     if a.ls:
         ofdm.frame_estimate(iq, X, 0, ws)
         return
+    if a.demod:
+        ofdm.frame_demod(iq, X, 0, ws=ws, out=out)
+        return
     if a.partial:
         ofdm.frame_mrc_partial(iq, ws, 0, num=out)
     else:
@@ -117,6 +122,8 @@ for ai, iq in enumerate(iqs):
                     d = (out - ref).abs().max().item()
                 chk[v] = (errs, d)
     b_sym = (R * C * 8 * 2 / (S - 1)) if a.ls else (R * C * 8 + K * 8)  # LS: pilot rows in + Hc out
+    if a.demod:
+        b_sym = R * C * 8 * S / (S - 1) + K * 8  # pilot + data rows in, outputs
     for v in a.variants:
         ms = sorted(res[v])[len(res[v]) // 2]
         tbs = Q * b_sym / (ms * 1e-3) / 1e12

@@ -58,6 +58,9 @@ def main():
     global MRC, LS
     if cfg.get("domain") == "freq":  # bench.py --mode freq
         MRC, LS = "k_mrc_freq", "k_ls_freq"
+    one = cfg.get("flow") == "one-launch"  # bench.py's one-launch flow: k_demod_td1024 is the kernel
+    if one:
+        MRC = "k_demod_td"
 
     rows = []
     for k in sorted(fetch, key=lambda k: -fetch[k]):
@@ -76,8 +79,10 @@ def main():
     q = cfg["data_symbols_per_gpu"]
     b_sym = cfg["R"] * cfg["C"] * 8 + (cfg["C"] - 1) * 8
     alg = q * b_sym
+    if one:  # + the pilot symbol and pilot vector per frame
+        alg += cfg["frames_per_gpu"] * (cfg["R"] * cfg["C"] * 8 + (cfg["C"] - 1) * 8)
     out = {"tag": tag, "config": dict({k: cfg[k] for k in ("R", "C", "S", "prefix", "frames_per_gpu")},
-                                      domain=cfg.get("domain", "time")),
+                                      domain=cfg.get("domain", "time"), flow=cfg.get("flow", "two-launch")),
            "mrc_kernel": mrc[0][0] if mrc else None,
            "mrc_hbm_bytes_per_launch": mrc[0][4] if mrc else None,
            "mrc_algorithmic_bytes_per_launch": alg,
