@@ -1764,6 +1764,9 @@ hipError_t launch_zf_apply(const float2 *Wt, const float2 *X, int U, int R, int 
         case 11: if (K >= 2 && U <= 20) return apply_ws16_launch<8, 1, 4, 8, 2>(Wt, X, U, R, K, nsym, Y, 64, s); break;
         case 12: if (K >= 2 && U <= 20) return apply_ws16_launch<8, 1, 4, 8, 1>(Wt, X, U, R, K, nsym, Y, 128, s); break;
         case 9: if (K >= 2 && U <= 40) return apply_ws16_launch<4, 1, 4, 16>(Wt, X, U, R, K, nsym, Y, 32, s); break;
+        case 13: if (K >= 2 && U <= 40) return apply_ws16_launch<4, 1, 8, 8, 1>(Wt, X, U, R, K, nsym, Y, 32, s); break;
+        case 14: if (K >= 2 && U <= 40) return apply_ws16_launch<4, 1, 8, 8, 0>(Wt, X, U, R, K, nsym, Y, 32, s); break;
+        case 15: if (K >= 2 && U <= 20) return apply_ws16_launch<8, 1, 4, 8, 0>(Wt, X, U, R, K, nsym, Y, 64, s); break;
         default: break;
     }
 #endif
@@ -1772,8 +1775,13 @@ hipError_t launch_zf_apply(const float2 *Wt, const float2 *X, int U, int R, int 
     // same-process A/B at R = 64, K = 1023, 10 000 symbols:
     // U = 4 / 8 / 16 / 24 / 32: 1.82 / 1.96 / 2.38 / 3.16 / 4.42 ms -> 1.50 /
     // 1.53 / 1.94-1.96 / 2.93 / 3.58 ms.  Fewer than 8 antenna rows fill less
-    // than one 8-row tile: the register-tiled kernels below.
-    if (K >= 2 && R >= 8 && U <= 20) return apply_ws16_launch<8, 1, 4, 8>(Wt, X, U, R, K, nsym, Y, 64, s);
+    // than one 8-row tile: the register-tiled kernels below.  8-row tiles run
+    // every block of a 64-symbol chunk on one XCD (row blocks adjacent,
+    // XM = 1): same-process A/B vs chunk groups round-robin over the XCDs,
+    // U = 4 / 8 / 16 / 20: 1.320 / 1.358 / 1.743 / 2.004 -> 1.235 / 1.253 /
+    // 1.718 / 1.996 ms (profiles/r3/r3l_zf_apply_xmap.jsonl); the same map
+    // on the 4-row tiles is 1.7x slower.
+    if (K >= 2 && R >= 8 && U <= 20) return apply_ws16_launch<8, 1, 4, 8, 1>(Wt, X, U, R, K, nsym, Y, 64, s);
     if (K >= 2 && R >= 8 && U <= 40) return apply_ws16_launch<4, 1, 8, 8>(Wt, X, U, R, K, nsym, Y, 32, s);
     return gemm_dispatch<false>(Wt, 1, R, X, U, R, K, nsym, Y, s);
 }
