@@ -237,7 +237,7 @@ def main():
     # and after the combine (MRC).  The LS of step i is timed from step i-1's
     # end event (one event before the loop for i = 0), so no event sits
     # between two steps' kernels beyond the one the MRC timing needs.
-    # One-launch flow: the step is ofdm_frame_demod (k_demod_td1024, LS and
+    # One-launch flow: the step is ofdm_frame_demod (k_demod_td<C>, LS and
     # MRC in one grid), timed from the previous step's end event.
     def step(evs=None):
         if one:
@@ -304,7 +304,7 @@ def main():
         mrc_name = "k_mrc_freq_frames (MRC+normalise+rotate)" if C >= 512 else "k_mrc_freq (MRC+normalise+rotate)"
     bytes_launch = Q * b_sym
     if one:  # + the pilot symbol and pilot vector per frame
-        mrc_name = "k_demod_td1024 (LS + FFT+MRC+normalise+rotate, one launch)"
+        mrc_name = f"k_demod_td{C} (LS + FFT+MRC+normalise+rotate, one launch)"
         bytes_launch += F * (R * C * 8 + K * 8)
     achieved = bytes_launch / (mrc_ms * 1e-3) / 1e9
     traffic, tsrc = pmc_traffic(args.pmc, cfg)

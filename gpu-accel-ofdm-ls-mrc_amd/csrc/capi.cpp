@@ -60,12 +60,15 @@ hipError_t mrc_fused(const float2 *iq, long long F, int S, int R, int C, int pre
     return ofdm::launch_mrc_td4096(iq, F, S, R, prefix, Hc, P, out, mode, s);
 }
 
-// ofdm_frame_demod at C = 1024 runs LS and MRC as ONE launch
-// (k_demod_td1024) unless the stream is being captured into a graph: its
-// per-launch flag epoch would be frozen in the graph, and a replay would
-// find every flag already set.
+// ofdm_frame_demod at C = 1024 runs LS and MRC as ONE launch (k_demod_td1024)
+// unless the stream is being captured into a graph: its per-launch flag
+// epoch would be frozen in the graph, and a replay would find every flag
+// already set.  The same kernels at C = 2048 / 4096 (k_demod_td2048 / 4096)
+// measured no faster than the two launches and are in the
+// A/B build only (OFDM_AB_DEMOD_WIDE=1).
 bool one_launch_demod(int C, hipStream_t s) {
-    if (C != 1024 || !ofdm::ab_knob("DEMOD1K_FUSED", 1)) return false;
+    if (!ofdm::ab_knob("DEMOD_FUSED", 1)) return false;
+    if (C != 1024 && !(fused_c(C) && ofdm::ab_knob("DEMOD_WIDE", 0))) return false;
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(s, &st) != hipSuccess) return false;
     return st == hipStreamCaptureStatusNone;
@@ -431,9 +434,13 @@ int ofdm_frame_demod(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int
     hipStream_t s = hs(stream);
     ws_forget(d_ws);
     if (one_launch_demod(C, s)) {
-        rc = hip_check(ofdm::launch_demod_td1024(F2(d_iq), nframes, S, R, prefix, F2(d_X), w.Hc, w.P, F2(d_out),
-                                                 w.flags, next_epoch(), s),
-                       "launch_demod_td1024");
+        auto launch = ofdm::launch_demod_td1024;
+#ifdef OFDM_AB_KNOBS
+        if (C == 2048) launch = ofdm::launch_demod_td2048;
+        if (C == 4096) launch = ofdm::launch_demod_td4096;
+#endif
+        rc = hip_check(launch(F2(d_iq), nframes, S, R, prefix, F2(d_X), w.Hc, w.P, F2(d_out), w.flags, next_epoch(), s),
+                       "launch_demod_td");
         if (rc == OFDM_OK) ws_record(d_ws, ws_bytes_, nframes, S, R, C, true, false);
         return rc;
     }

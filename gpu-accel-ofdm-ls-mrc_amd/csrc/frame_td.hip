@@ -334,13 +334,9 @@ k_mrc_td1024_hlds(const float2 *__restrict__ iq, int S, int R, int prefix, const
 // goes on, so no dispatch-order or residency assumption is needed for a
 // correct result -- in-order dispatch only makes the wait short.
 // ---------------------------------------------------------------------------
-typedef __attribute__((address_space(1))) unsigned long long gu64;
-constexpr long long SPIN_TICKS = 200000;  // 2 ms at 100 MHz (A/B build: OFDM_AB_DEMOD1K_SPIN)
-
 // LS of frame f by one 8-wave workgroup in the HLDS LDS layout (tables
 // filled): wave w takes rows w, w + 8, ...; partial |H|^2 added in wave
 // order through the transpose images (the k_ls_td1024<8> order).
-template <bool WT>
 __device__ __forceinline__ void hlds_ls_frame(const float2 *__restrict__ iq, int S, int R, int prefix,
                                               const float2 *__restrict__ X, float2 *Hc, float *P, long long f,
                                               int w, int t, float2 *T, float2 *T0, const float2 *tw1,
@@ -371,20 +367,9 @@ __device__ __forceinline__ void hlds_ls_frame(const float2 *__restrict__ iq, int
             x[k] = h;
             p[k] = p[k] + (h.x * h.x) + (h.y * h.y);
         }
-        if constexpr (WT) {  // write-through (sc1, aux 16): visible at agent scope once vmcnt drains
-            // (a buffer store, not inline asm: the compiler must see the
-            // store-data VGPRs to resolve the VALU-write hazard in front of it)
-            typedef int v4i __attribute__((ext_vector_type(4)));
-            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(Hf, (short)0, R * C * 8, 0x00020000);
+        // hc_store's layout, write-through (sc1): visible at agent scope once vmcnt drains
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const v4i v = {__builtin_bit_cast(int, x[2 * i].x), __builtin_bit_cast(int, x[2 * i].y),
-                               __builtin_bit_cast(int, x[2 * i + 1].x), __builtin_bit_cast(int, x[2 * i + 1].y)};
-                __builtin_amdgcn_raw_buffer_store_b128(v, rs, (r * (C / 2) + i * 64 + t) * 16, 0, 16);
-            }
-        } else {
-            hc_store(Hf + (long long)r * (C / 2), t, x);
-        }
+        for (int i = 0; i < 8; ++i) store16_wt(Hf, R * C * 8, (r * (C / 2) + i * 64 + t) * 16, x[2 * i], x[2 * i + 1]);
     }
     __syncthreads();  // every wave is done with its transpose image
     float *pp = reinterpret_cast<float *>(T0);  // [WAVES][C], over the images
@@ -397,30 +382,18 @@ __device__ __forceinline__ void hlds_ls_frame(const float2 *__restrict__ iq, int
         float sum = pp[b];
         for (int i = 1; i < nw; ++i) sum = sum + pp[i * C + b];
         const float v = b == 0 ? 1.f : sum;
-        if constexpr (WT)
-            __hip_atomic_store((__attribute__((address_space(1))) unsigned *)(Pf + b), __builtin_bit_cast(unsigned, v),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else
-            Pf[b] = v;
+        store4_wt(Pf + b, v);
     }
     __syncthreads();  // pp (the transpose images) read before they are reused
 }
 
-__device__ __forceinline__ bool wait_flag(unsigned long long *flag, unsigned long long epoch, long long ticks) {
-    const long long t0 = wall_clock64();
-    while (__hip_atomic_load((gu64 *)(flag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
-        if (wall_clock64() - t0 >= ticks) return false;
-        __builtin_amdgcn_s_sleep(2);
-    }
-    return true;
-}
-
-// WT: the estimate is stored write-through (sc1: 16-B Hc stores, 4-B agent
-// atomic P stores) and published without the release fence, whose L2
+// The estimate is stored write-through (sc1: 16-B Hc stores, 4-B agent
+// atomic P stores) and published without a release fence, whose L2
 // write-back would also flush the output lines the MRC workgroups of the
-// same XCD left dirty (Guideline 16, R1 write-through form); else plain
-// stores + release fence.
-template <int DBG = 0, bool WT = true>
+// same XCD left dirty (wave_fft1024.hpp: publish_flag / consume_flags;
+// same-process A/B vs plain stores + release fence: equal to 1 % faster,
+// DESIGN.md 4.6).
+template <int DBG = 0>
 __global__ void __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 4)))
 k_demod_td1024(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ X, float2 *Hc,
                float *P, float2 *__restrict__ out, long long nq, long long nblocks, long long per_xcd,
@@ -440,15 +413,8 @@ k_demod_td1024(const float2 *__restrict__ iq, int S, int R, int prefix, const fl
         if (f >= nframes) return;
         fill(tw1, tw2);
         __syncthreads();
-        hlds_ls_frame<WT>(iq, S, R, prefix, X, Hc, P, f, w, t, T, T0, tw1, tw2);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's Hc and P stores
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            if constexpr (!WT) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store((gu64 *)(flags + f), epoch, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        }
+        hlds_ls_frame(iq, S, R, prefix, X, Hc, P, f, w, t, T, T0, tw1, tw2);
+        publish_flag(flags + f, epoch);
         return;
     }
     const long long pb = blockIdx.x - nls;
@@ -467,30 +433,12 @@ k_demod_td1024(const float2 *__restrict__ iq, int S, int R, int prefix, const fl
     const int Cp = C + prefix;
     const float2 *sym = iq + (f * S + s) * (long long)R * Cp + prefix;
 
-    // wait for the estimates of frames f0 .. fl (one lane polls; hfree, not
-    // used before the rows, carries the outcome to the other waves)
-    int *seen = reinterpret_cast<int *>(hfree);
-    if (threadIdx.x == 0) {
-        const bool ok = wait_flag(flags + f0, epoch, spin_ticks) &&
-                        (fl == f0 || wait_flag(flags + fl, epoch, spin_ticks));
-        *seen = ok ? 1 : 0;
-        if (ok) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();  // tables filled; the acquire has completed
-    if (!*seen) {
-        // not published in time: estimate here (identical bytes), then read
-        // them back behind an acquire of our own
-        __syncthreads();  // every wave has read the word
-        for (long long ff = f0; ff <= fl; ++ff)
-            hlds_ls_frame<WT>(iq, S, R, prefix, X, Hc, P, ff, w, t, T, T0, tw1, tw2);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __syncthreads();
+    // wait for the estimates of frames f0 .. fl (hfree, not used before the
+    // rows, carries the outcome); not published in time: estimate here
+    // (identical bytes) and read them back behind an acquire of our own
+    if (!consume_flags(flags, f0, fl, epoch, spin_ticks, reinterpret_cast<int *>(hfree))) {
+        for (long long ff = f0; ff <= fl; ++ff) hlds_ls_frame(iq, S, R, prefix, X, Hc, P, ff, w, t, T, T0, tw1, tw2);
+        acquire_all();
     }
 
     float2 acc[16];
@@ -582,13 +530,10 @@ hipError_t launch_demod_td1024(const float2 *iq, long long nframes, int S, int R
     const long long pxcd = (nb + 7) / 8;
     const long long nls = (nframes + 7) / 8 * 8;
     if (pxcd * 8 + nls > 0x7fffffffll) return hipErrorInvalidValue;
-    auto kern = k_demod_td1024<0, true>;
-#ifdef OFDM_AB_KNOBS
-    if (!ab_knob("DEMOD1K_WT", 1)) kern = k_demod_td1024<0, false>;  // plain stores + release fence
-#endif
+    auto kern = k_demod_td1024<0>;
     hipLaunchKernelGGL(kern, dim3((unsigned)(nls + pxcd * 8)), dim3(64 * hlds::WAVES), hlds::LDS_BYTES, s, iq, S,
                        R, prefix, X, Hc, P, out, nq, nb, pxcd, flags, epoch, (int)nls, nframes,
-                       (long long)ab_knob("DEMOD1K_SPIN", (int)SPIN_TICKS));
+                       (long long)ab_knob("DEMOD_SPIN", (int)SPIN_TICKS));
     return hipGetLastError();
 }
 

@@ -75,19 +75,18 @@ __device__ __forceinline__ void row_fft2048(const float2 *__restrict__ src, int 
 constexpr int LS_WAVES = 4;
 constexpr size_t LS_LDS = lds_bytes(LS_WAVES) + (size_t)C * sizeof(float2);
 
-__global__ void __launch_bounds__(256) k_ls_td2048(const float2 *__restrict__ iq, int S, int R,
-                                                   int prefix, const float2 *__restrict__ X,
-                                                   float2 *__restrict__ Hc, float *__restrict__ P,
-                                                   int partial) {
-    extern __shared__ __attribute__((aligned(16))) float2 lds[];
-    const int w = threadIdx.x >> 6, t = threadIdx.x & 63;
+// LS of frame f by a 4-wave workgroup.  WT (the one-launch kernel): Hc and P
+// stored write-through (sc1) for the agent-scope hand-off.
+template <bool WT>
+__device__ __forceinline__ void ls_frame2048(const float2 *__restrict__ iq, int S, int R, int prefix,
+                                             const float2 *__restrict__ X, float2 *Hc, float *P, long long f,
+                                             float2 *lds, int w, int t, int partial) {
     float2 *T = lds + TAB + w * hl::TS;
     float2 *xs = lds + TAB + LS_WAVES * hl::TS;  // xs[b] = X[b - 1], xs[0] unused
     fill_tables(lds);
     for (int b = threadIdx.x; b < C; b += blockDim.x) xs[b] = b ? X[b - 1] : float2{1.f, 0.f};
     __syncthreads();
 
-    const long long f = blockIdx.x;
     const int Cp = C + prefix;
     const float2 *pilot = iq + f * (long long)S * R * Cp + prefix;
     float4 *Hf = reinterpret_cast<float4 *>(Hc + f * (long long)R * C);
@@ -108,7 +107,10 @@ __global__ void __launch_bounds__(256) k_ls_td2048(const float2 *__restrict__ iq
             const float2 ho = ls_conj(xo[k], xs[be + 1]);
             pe[k] = pe[k] + (he.x * he.x) + (he.y * he.y);  // findDistSqrd order
             po[k] = po[k] + (ho.x * ho.x) + (ho.y * ho.y);
-            hr[k * 64 + t] = float4{he.x, he.y, ho.x, ho.y};
+            if constexpr (WT)
+                td1024::store16_wt(Hf, R * C * 8, (r * (C / 2) + k * 64 + t) * 16, he, ho);
+            else
+                hr[k * 64 + t] = float4{he.x, he.y, ho.x, ho.y};
         }
     }
     __syncthreads();
@@ -124,8 +126,22 @@ __global__ void __launch_bounds__(256) k_ls_td2048(const float2 *__restrict__ iq
     for (int b = threadIdx.x; b < C; b += blockDim.x) {
         float sum = pp[b];
         for (int i = 1; i < LS_WAVES; ++i) sum = sum + pp[i * C + b];  // antennas in order
-        Pf[b] = b == 0 ? (partial ? 0.f : 1.f) : sum;
+        const float v = b == 0 ? (partial ? 0.f : 1.f) : sum;
+        if constexpr (WT)
+            td1024::store4_wt(Pf + b, v);
+        else
+            Pf[b] = v;
     }
+    __syncthreads();  // pp (the transpose images) read before they are reused
+}
+
+__global__ void __launch_bounds__(256) k_ls_td2048(const float2 *__restrict__ iq, int S, int R,
+                                                   int prefix, const float2 *__restrict__ X,
+                                                   float2 *__restrict__ Hc, float *__restrict__ P,
+                                                   int partial) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int w = threadIdx.x >> 6, t = threadIdx.x & 63;
+    ls_frame2048<false>(iq, S, R, prefix, X, Hc, P, blockIdx.x, lds, w, t, partial);
 }
 
 // ---------------------------------------------------------------------------
@@ -193,22 +209,12 @@ __device__ __forceinline__ void il_row(const float2 *__restrict__ src, const flo
     }
 }
 
+// The MRC of data symbol q (< nq) by wave w (twiddle tables filled): rows,
+// normalise (mode 0), rotated and staged stores.
 template <int DBG = 0, int PK = 6, int IL = 1>
-__global__ void __attribute__((amdgpu_flat_work_group_size(256, 256), amdgpu_waves_per_eu(2, 2)))
-k_mrc_td2048(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
-             const float *__restrict__ P, float2 *__restrict__ out, long long nq, long long nblocks,
-             long long per_xcd, int mode) {
-    extern __shared__ __attribute__((aligned(16))) float2 lds[];
-    const int w = threadIdx.x >> 6, t = threadIdx.x & 63;
-    float2 *T = lds + TAB + w * hl::TS;
-    const long long pb = blockIdx.x;
-    const long long lb = (pb & 7) * per_xcd + (pb >> 3);
-    if (lb >= nblocks) return;
-    fill_tables(lds);
-    __syncthreads();
-    const long long q = lb * MRC_WAVES + w;
-    if (q >= nq) return;  // no block-level sync follows
-
+__device__ __forceinline__ void mrc2048_symbol(const float2 *__restrict__ iq, int S, int R, int prefix,
+                                               const float2 *Hc, const float *P, float2 *__restrict__ out,
+                                               long long q, int t, float2 *T, float2 *lds, int mode) {
     const int nsym = S - 1;
     const long long f = q / nsym;
     const int s = 1 + (int)(q % nsym);
@@ -331,6 +337,64 @@ k_mrc_td2048(const float2 *__restrict__ iq, int S, int R, int prefix, const floa
     }
 }
 
+template <int DBG = 0, int PK = 6, int IL = 1>
+__global__ void __attribute__((amdgpu_flat_work_group_size(256, 256), amdgpu_waves_per_eu(2, 2)))
+k_mrc_td2048(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
+             const float *__restrict__ P, float2 *__restrict__ out, long long nq, long long nblocks,
+             long long per_xcd, int mode) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int w = threadIdx.x >> 6, t = threadIdx.x & 63;
+    float2 *T = lds + TAB + w * hl::TS;
+    const long long pb = blockIdx.x;
+    const long long lb = (pb & 7) * per_xcd + (pb >> 3);
+    if (lb >= nblocks) return;
+    fill_tables(lds);
+    __syncthreads();
+    const long long q = lb * MRC_WAVES + w;
+    if (q >= nq) return;  // no block-level sync follows
+    mrc2048_symbol<DBG, PK, IL>(iq, S, R, prefix, Hc, P, out, q, t, T, lds, mode);
+
+}
+
+// One-launch frame demod (ofdm_frame_demod, C = 2048; frame_td.hip
+// k_demod_td1024 for the protocol): workgroups 0 .. nls-1 estimate one frame
+// each (write-through) and publish it; the MRC workgroups behind them wait
+// for the (one or two) frames of their four symbols, or estimate them
+// themselves when the bounded wait expires.  LDS: the LS layout (the MRC's
+// plus the pilot row, whose first word carries the wait's outcome).
+template <int DBG = 0>
+__global__ void __attribute__((amdgpu_flat_work_group_size(256, 256), amdgpu_waves_per_eu(2, 2)))
+k_demod_td2048(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ X, float2 *Hc,
+               float *P, float2 *__restrict__ out, long long nq, long long nblocks, long long per_xcd,
+               unsigned long long *flags, unsigned long long epoch, int nls, long long nframes,
+               long long spin_ticks) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int w = threadIdx.x >> 6, t = threadIdx.x & 63;
+    if ((int)blockIdx.x < nls) {  // estimator workgroup
+        const long long f = blockIdx.x;
+        if (f >= nframes) return;
+        ls_frame2048<true>(iq, S, R, prefix, X, Hc, P, f, lds, w, t, 0);
+        td1024::publish_flag(flags + f, epoch);
+        return;
+    }
+    const long long pb = blockIdx.x - nls;
+    const long long lb = (pb & 7) * per_xcd + (pb >> 3);
+    if (lb >= nblocks) return;
+    const int nsym = S - 1;
+    const long long q0 = lb * MRC_WAVES, ql = q0 + MRC_WAVES - 1 < nq ? q0 + MRC_WAVES - 1 : nq - 1;
+    int *seen = reinterpret_cast<int *>(lds + TAB + LS_WAVES * hl::TS);
+    if (!td1024::consume_flags(flags, q0 / nsym, ql / nsym, epoch, spin_ticks, seen)) {
+        for (long long ff = q0 / nsym; ff <= ql / nsym; ++ff)
+            ls_frame2048<true>(iq, S, R, prefix, X, Hc, P, ff, lds, w, t, 0);
+        td1024::acquire_all();
+    }
+    fill_tables(lds);
+    __syncthreads();
+    const long long q = q0 + w;
+    if (q >= nq) return;
+    mrc2048_symbol<DBG>(iq, S, R, prefix, Hc, P, out, q, t, lds + TAB + w * hl::TS, lds, 0);
+}
+
 }  // namespace td2048
 
 hipError_t launch_ls_td2048(const float2 *iq, long long nframes, int S, int R, int prefix,
@@ -376,5 +440,25 @@ hipError_t launch_mrc_td2048(const float2 *iq, long long nframes, int S, int R, 
                        R, prefix, Hc, P, out, nq, nblocks, per_xcd, mode);
     return hipGetLastError();
 }
+
+#ifdef OFDM_AB_KNOBS  // A/B build only: no faster than the two launches
+hipError_t launch_demod_td2048(const float2 *iq, long long nframes, int S, int R, int prefix, const float2 *X,
+                               float2 *Hc, float *P, float2 *out, unsigned long long *flags,
+                               unsigned long long epoch, hipStream_t s) {
+    using namespace td2048;
+    const long long nq = nframes * (S - 1);
+    if (nq <= 0) return hipSuccess;
+    const long long nblocks = (nq + MRC_WAVES - 1) / MRC_WAVES;
+    const long long per_xcd = (nblocks + 7) / 8;
+    const long long nls = (nframes + 7) / 8 * 8;
+    if (per_xcd * 8 + nls > 0x7fffffffll) return hipErrorInvalidValue;
+    auto kern = k_demod_td2048<0>;
+    if (hipError_t e = opt_in_lds(reinterpret_cast<const void *>(kern), (int)LS_LDS); e != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3((unsigned)(nls + per_xcd * 8)), dim3(64 * MRC_WAVES), LS_LDS, s, iq, S, R,
+                       prefix, X, Hc, P, out, nq, nblocks, per_xcd, flags, epoch, (int)nls, nframes,
+                       (long long)ab_knob("DEMOD_SPIN", (int)td1024::SPIN_TICKS));
+    return hipGetLastError();
+}
+#endif
 
 }  // namespace ofdm

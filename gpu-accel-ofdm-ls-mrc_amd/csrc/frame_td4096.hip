@@ -102,7 +102,7 @@ __device__ __forceinline__ void row_fft4096(const float2 *__restrict__ src, int 
 constexpr int LS_WAVES = 8;
 constexpr size_t ls_lds(int nw) { return lds_bytes(nw) + (size_t)C * sizeof(float2); }
 
-template <int E, int LS_PAIRS>
+template <int E, int LS_PAIRS, bool WT = false>
 __device__ __forceinline__ void ls_rows(const float2 *pilot, int Cp, int R, int j, int t, float2 *T,
                                         const float2 *lds, const float2 *xs, float2 *Hf, float *pp) {
     const int b0 = lane_bin0(t);
@@ -122,8 +122,13 @@ __device__ __forceinline__ void ls_rows(const float2 *pilot, int Cp, int R, int 
             const float2 ho = ls_conj(xo[k], xs[be + 2]);
             pe[k] = pe[k] + (he.x * he.x) + (he.y * he.y);  // findDistSqrd order
             po[k] = po[k] + (ho.x * ho.x) + (ho.y * ho.y);
-            hr[k * 64 + t] = he;
-            hr[1024 + k * 64 + t] = ho;
+            if constexpr (WT) {  // write-through (sc1) for the one-launch hand-off
+                td1024::store8_wt(hr + k * 64 + t, he);
+                td1024::store8_wt(hr + 1024 + k * 64 + t, ho);
+            } else {
+                hr[k * 64 + t] = he;
+                hr[1024 + k * 64 + t] = ho;
+            }
         }
     }
     __syncthreads();  // every wave is done with its transpose image (pp reuses it)
@@ -135,13 +140,13 @@ __device__ __forceinline__ void ls_rows(const float2 *pilot, int Cp, int R, int 
     }
 }
 
-template <int NW = LS_WAVES>
-__global__ void __launch_bounds__(64 * NW) k_ls_td4096(const float2 *__restrict__ iq, int S, int R,
-                                                       int prefix, const float2 *__restrict__ X,
-                                                       float2 *__restrict__ Hc, float *__restrict__ P,
-                                                       int partial) {
+// LS of frame f by an NW-wave workgroup (LS LDS layout, ls_lds(NW) bytes).
+// WT: Hc and P stored write-through (the one-launch kernel).
+template <int NW = LS_WAVES, bool WT = false>
+__device__ __forceinline__ void ls_frame4096(const float2 *__restrict__ iq, int S, int R, int prefix,
+                                             const float2 *__restrict__ X, float2 *Hc, float *P, long long f,
+                                             float2 *lds, int partial) {
     constexpr int LS_PAIRS = NW / 2;
-    extern __shared__ __attribute__((aligned(16))) float2 lds[];
     const int w = threadIdx.x >> 6, t = threadIdx.x & 63;
     float2 *T = lds + TAB + w * hl::TS;
     float2 *xs = lds + TAB + NW * hl::TS;  // xs[b] = X[b - 1], xs[0] unused
@@ -149,22 +154,35 @@ __global__ void __launch_bounds__(64 * NW) k_ls_td4096(const float2 *__restrict_
     for (int b = threadIdx.x; b < C; b += blockDim.x) xs[b] = b ? X[b - 1] : float2{1.f, 0.f};
     __syncthreads();
 
-    const long long f = blockIdx.x;
     const int Cp = C + prefix;
     const float2 *pilot = iq + f * (long long)S * R * Cp + prefix;
     float2 *Hf = Hc + f * (long long)R * C;
     float *pp = reinterpret_cast<float *>(lds + TAB);  // [LS_PAIRS][C], reuses T
     if (w & 1)
-        ls_rows<1, LS_PAIRS>(pilot, Cp, R, w >> 1, t, T, lds, xs, Hf, pp);
+        ls_rows<1, LS_PAIRS, WT>(pilot, Cp, R, w >> 1, t, T, lds, xs, Hf, pp);
     else
-        ls_rows<0, LS_PAIRS>(pilot, Cp, R, w >> 1, t, T, lds, xs, Hf, pp);
+        ls_rows<0, LS_PAIRS, WT>(pilot, Cp, R, w >> 1, t, T, lds, xs, Hf, pp);
     __syncthreads();
     float *Pf = P + f * C;
     for (int b = threadIdx.x; b < C; b += blockDim.x) {
         float sum = pp[b];
         for (int i = 1; i < LS_PAIRS; ++i) sum = sum + pp[i * C + b];  // antennas in order
-        Pf[b] = b == 0 ? (partial ? 0.f : 1.f) : sum;
+        const float v = b == 0 ? (partial ? 0.f : 1.f) : sum;
+        if constexpr (WT)
+            td1024::store4_wt(Pf + b, v);
+        else
+            Pf[b] = v;
     }
+    __syncthreads();  // pp (the transpose images) read before they are reused
+}
+
+template <int NW = LS_WAVES>
+__global__ void __launch_bounds__(64 * NW) k_ls_td4096(const float2 *__restrict__ iq, int S, int R,
+                                                       int prefix, const float2 *__restrict__ X,
+                                                       float2 *__restrict__ Hc, float *__restrict__ P,
+                                                       int partial) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    ls_frame4096<NW>(iq, S, R, prefix, X, Hc, P, blockIdx.x, lds, partial);
 }
 
 // ---------------------------------------------------------------------------
@@ -445,27 +463,20 @@ __device__ __forceinline__ void h_rows(const float2 *sym, int Cp, int R, const f
 
 constexpr int H_PK = 7;  // packed-f32 split, FFT halves and MAC (pk.hpp)
 
+// The MRC of one logical block (HP pairs = HP data symbols of frame f, pair
+// `pair` on symbol j < nsym when `store`; s = its symbol slot) after the
+// workgroup prologue: Hc row 0 DMA, tables, rows, normalise, staged stores.
 template <int DBG = 0, int TW = 3, int HP = H_PAIRS, int HE = 0, int IL = 0>
-__global__ void __attribute__((amdgpu_flat_work_group_size(128 * HP, 128 * HP), amdgpu_waves_per_eu(2, 2)))
-k_mrc_td4096h(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
-              const float *__restrict__ P, float2 *__restrict__ out, long long nframes, long long nblocks,
-              long long per_xcd, int mode) {
-    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+__device__ __forceinline__ void mrc4096_block(const float2 *__restrict__ iq, int S, int R, int prefix,
+                                              const float2 *Hc, const float *P, float2 *__restrict__ out,
+                                              long long f, int j, bool store, int s, float2 *lds, int mode) {
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), t = threadIdx.x & 63;
     const int e = w & 1, pair = w >> 1;
     const float2 *tw1 = lds, *tw2 = lds + hl::TW1S;
     float2 *T = lds + X_TAB + w * hl::TS;
     const float2 *Tp = lds + X_TAB + (w ^ 1) * hl::TS;
     float2 *HB = lds + X_TAB + 2 * HP * hl::TS;  // [2][C] Hc rows ([1][C] for HP = 2)
-    const long long pb = blockIdx.x;
-    const long long lb = (pb & 7) * per_xcd + (pb >> 3);  // XCD-grouped: a frame's blocks share an L2
-    if (lb >= nblocks) return;  // whole workgroup
     const int nsym = S - 1;
-    const long long bpf = (nsym + HP - 1) / HP;
-    const long long f = lb / bpf;
-    const int j = (int)(lb - f * bpf) * HP + pair;  // data symbol index within the frame
-    const bool store = j < nsym;
-    const int s = 1 + (store ? j : nsym - 1);
     const float2 *Hg = Hc + f * (long long)R * C;
     dma_hc_row<2 * HP>(Hg, lds_addr(HB));  // row 0; landed at the first row's barrier
     hl::fill(lds, lds + hl::TW1S);
@@ -558,6 +569,65 @@ k_mrc_td4096h(const float2 *__restrict__ iq, int S, int R, int prefix, const flo
     }
 }
 
+template <int DBG = 0, int TW = 3, int HP = H_PAIRS, int HE = 0, int IL = 0>
+__global__ void __attribute__((amdgpu_flat_work_group_size(128 * HP, 128 * HP), amdgpu_waves_per_eu(2, 2)))
+k_mrc_td4096h(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
+              const float *__restrict__ P, float2 *__restrict__ out, long long nframes, long long nblocks,
+              long long per_xcd, int mode) {
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    const int pair = __builtin_amdgcn_readfirstlane(threadIdx.x >> 7);
+    const long long pb = blockIdx.x;
+    const long long lb = (pb & 7) * per_xcd + (pb >> 3);  // XCD-grouped: a frame's blocks share an L2
+    if (lb >= nblocks) return;  // whole workgroup
+    const int nsym = S - 1;
+    const long long bpf = (nsym + HP - 1) / HP;
+    const long long f = lb / bpf;
+    const int j = (int)(lb - f * bpf) * HP + pair;  // data symbol index within the frame
+    const bool store = j < nsym;
+    const int s = 1 + (store ? j : nsym - 1);
+    mrc4096_block<DBG, TW, HP, HE, IL>(iq, S, R, prefix, Hc, P, out, f, j, store, s, lds, mode);
+}
+
+
+// One-launch frame demod (ofdm_frame_demod, C = 4096; frame_td.hip
+// k_demod_td1024 for the protocol): workgroups 0 .. nls-1 estimate one frame
+// each in the LS LDS layout (write-through) and publish it; each MRC
+// workgroup (frame-aligned: one frame) waits for its frame, or estimates it
+// itself when the bounded wait expires, before its Hc row 0 DMA.  LDS: the
+// MRC's 140 KiB; the LS layout needs 132, the word after it carries the
+// wait's outcome (inside the second Hc buffer, first written by row 1's DMA).
+template <int DBG = 0>
+__global__ void __attribute__((amdgpu_flat_work_group_size(128 * H_PAIRS, 128 * H_PAIRS), amdgpu_waves_per_eu(2, 2)))
+k_demod_td4096(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ X, float2 *Hc,
+               float *P, float2 *__restrict__ out, long long nblocks, long long per_xcd,
+               unsigned long long *flags, unsigned long long epoch, int nls, long long nframes,
+               long long spin_ticks) {
+    static_assert(ls_lds(2 * H_PAIRS) + 16 <= H_LDS, "the LS layout and the flag word fit the MRC's LDS");
+    extern __shared__ __attribute__((aligned(16))) float2 lds[];
+    if ((int)blockIdx.x < nls) {  // estimator workgroup
+        const long long f = blockIdx.x;
+        if (f >= nframes) return;
+        ls_frame4096<2 * H_PAIRS, true>(iq, S, R, prefix, X, Hc, P, f, lds, 0);
+        td1024::publish_flag(flags + f, epoch);
+        return;
+    }
+    const int pair = __builtin_amdgcn_readfirstlane(threadIdx.x >> 7);
+    const long long pb = blockIdx.x - nls;
+    const long long lb = (pb & 7) * per_xcd + (pb >> 3);
+    if (lb >= nblocks) return;  // whole workgroup
+    const int nsym = S - 1;
+    const long long bpf = (nsym + H_PAIRS - 1) / H_PAIRS;
+    const long long f = lb / bpf;
+    const int j = (int)(lb - f * bpf) * H_PAIRS + pair;
+    const bool store = j < nsym;
+    const int s = 1 + (store ? j : nsym - 1);
+    int *seen = reinterpret_cast<int *>(reinterpret_cast<char *>(lds) + ls_lds(2 * H_PAIRS));
+    if (!td1024::consume_flags(flags, f, f, epoch, spin_ticks, seen)) {
+        ls_frame4096<2 * H_PAIRS, true>(iq, S, R, prefix, X, Hc, P, f, lds, 0);
+        td1024::acquire_all();
+    }
+    mrc4096_block<DBG, 3, H_PAIRS, 0, 3>(iq, S, R, prefix, Hc, P, out, f, j, store, s, lds, 0);
+}
 
 }  // namespace td4096
 
@@ -626,5 +696,24 @@ hipError_t launch_mrc_td4096(const float2 *iq, long long nframes, int S, int R, 
                        Hc, P, out, nframes, nb, pxcd, mode);
     return hipGetLastError();
 }
+
+#ifdef OFDM_AB_KNOBS  // A/B build only: no faster than the two launches
+hipError_t launch_demod_td4096(const float2 *iq, long long nframes, int S, int R, int prefix, const float2 *X,
+                               float2 *Hc, float *P, float2 *out, unsigned long long *flags,
+                               unsigned long long epoch, hipStream_t s) {
+    using namespace td4096;
+    const long long nq = nframes * (S - 1);
+    if (nq <= 0) return hipSuccess;
+    const long long bpf = ((S - 1) + H_PAIRS - 1) / H_PAIRS, nb = nframes * bpf, pxcd = (nb + 7) / 8;
+    const long long nls = (nframes + 7) / 8 * 8;
+    if (pxcd * 8 + nls > 0x7fffffffll) return hipErrorInvalidValue;
+    auto kern = k_demod_td4096<0>;
+    if (hipError_t e = opt_in_lds(reinterpret_cast<const void *>(kern), (int)H_LDS); e != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3((unsigned)(nls + pxcd * 8)), dim3(128 * H_PAIRS), H_LDS, s, iq, S, R, prefix, X,
+                       Hc, P, out, nb, pxcd, flags, epoch, (int)nls, nframes,
+                       (long long)ab_knob("DEMOD_SPIN", (int)td1024::SPIN_TICKS));
+    return hipGetLastError();
+}
+#endif
 
 }  // namespace ofdm

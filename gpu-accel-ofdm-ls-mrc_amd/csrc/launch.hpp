@@ -106,11 +106,21 @@ hipError_t launch_ls_td2048(const float2 *iq, long long nframes, int S, int R, i
                             const float2 *X, float2 *Hc, float *P, int partial, hipStream_t s);
 hipError_t launch_mrc_td2048(const float2 *iq, long long nframes, int S, int R, int prefix,
                              const float2 *Hc, const float *P, float2 *out, int mode, hipStream_t s);
+#ifdef OFDM_AB_KNOBS  // one launch at C = 2048 (A/B build only)
+hipError_t launch_demod_td2048(const float2 *iq, long long nframes, int S, int R, int prefix, const float2 *X,
+                               float2 *Hc, float *P, float2 *out, unsigned long long *flags,
+                               unsigned long long epoch, hipStream_t s);
+#endif
 // fused time-domain receiver, C = 4096 (frame_td4096.hip); same contracts
 hipError_t launch_ls_td4096(const float2 *iq, long long nframes, int S, int R, int prefix,
                             const float2 *X, float2 *Hc, float *P, int partial, hipStream_t s);
 hipError_t launch_mrc_td4096(const float2 *iq, long long nframes, int S, int R, int prefix,
                              const float2 *Hc, const float *P, float2 *out, int mode, hipStream_t s);
+#ifdef OFDM_AB_KNOBS  // one launch at C = 4096 (A/B build only)
+hipError_t launch_demod_td4096(const float2 *iq, long long nframes, int S, int R, int prefix, const float2 *X,
+                               float2 *Hc, float *P, float2 *out, unsigned long long *flags,
+                               unsigned long long epoch, hipStream_t s);
+#endif
 hipError_t launch_conj_product(const float2 *Y, long long nsyms, int R, int C, const float2 *Hc,
                                float2 *prod, hipStream_t s);
 hipError_t launch_combine(const float2 *prod, long long nsyms, int R, int K, const float *P,

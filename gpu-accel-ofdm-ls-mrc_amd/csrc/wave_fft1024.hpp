@@ -208,6 +208,88 @@ __device__ __forceinline__ void hc_load(const float4 *__restrict__ src, int t, f
     }
 }
 
+// ---------------------------------------------------------------------------
+// In-launch hand-off of per-frame estimates (the one-launch frame demod
+// kernels, k_demod_td*): cdna_hip_programming.md Guideline 16, R1 in its
+// write-through form.  The producer stores the payload with sc1 (write-
+// through, aux 16 on the buffer / atomic stores -- compiler-generated, so
+// the hazard recognizer sees the store-data registers), every storing wave
+// drains vmcnt, a workgroup barrier, then ONE lane stores the 64-bit flag
+// (relaxed, agent scope).  The consumer polls the flag with one lane
+// (relaxed, agent scope, s_sleep between polls, bounded by the 100 MHz wall
+// clock), then ONE agent acquire, vmcnt(0) and a workgroup barrier before
+// any load of the payload.
+// ---------------------------------------------------------------------------
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned gu32;
+constexpr long long SPIN_TICKS = 200000;  // 2 ms at 100 MHz (A/B build: OFDM_AB_DEMOD_SPIN)
+
+// 16 B {a, b} at byte offset off of [base, base + bytes), write-through
+__device__ __forceinline__ void store16_wt(const void *base, int bytes, int off, float2 a, float2 b) {
+    typedef int v4i __attribute__((ext_vector_type(4)));
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, bytes, 0x00020000);
+    const v4i v = {__builtin_bit_cast(int, a.x), __builtin_bit_cast(int, a.y), __builtin_bit_cast(int, b.x),
+                   __builtin_bit_cast(int, b.y)};
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 16);
+}
+__device__ __forceinline__ void store8_wt(float2 *p, float2 v) {
+    __hip_atomic_store((gu64 *)(p), __builtin_bit_cast(unsigned long long, v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void store4_wt(float *p, float v) {
+    __hip_atomic_store((gu32 *)(p), __builtin_bit_cast(unsigned, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// producer, every thread of the workgroup: its stores drained, barrier, one
+// lane publishes
+__device__ __forceinline__ void publish_flag(unsigned long long *flag, unsigned long long epoch) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store((gu64 *)(flag), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+__device__ __forceinline__ bool wait_flag(unsigned long long *flag, unsigned long long epoch, long long ticks) {
+    const long long t0 = wall_clock64();
+    while (__hip_atomic_load((gu64 *)(flag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+        if (wall_clock64() - t0 >= ticks) return false;
+        __builtin_amdgcn_s_sleep(2);
+    }
+    return true;
+}
+
+// consumer, every thread of the workgroup: thread 0 waits for flags f0..fl,
+// acquires; returns whether they were seen (false: the bounded wait expired
+// -- the caller estimates the frames itself, then calls acquire_all()).
+// seen: an LDS word no other code touches before the caller's next barrier.
+__device__ __forceinline__ bool consume_flags(unsigned long long *flags, long long f0, long long fl,
+                                              unsigned long long epoch, long long ticks, int *seen) {
+    if (threadIdx.x == 0) {
+        bool ok = true;
+        for (long long f = f0; f <= fl && ok; ++f) ok = wait_flag(flags + f, epoch, ticks);
+        *seen = ok ? 1 : 0;
+        if (ok) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    const bool ok = *seen != 0;
+    __syncthreads();  // every wave has read the word before it may be reused
+    return ok;
+}
+// after the workgroup wrote an estimate itself: drain, acquire, barrier
+__device__ __forceinline__ void acquire_all() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+}
+
 // Twiddle tables and the two FFT halves in the LDS layout of the HLDS
 // kernels (k_mrc_td1024_hlds, frame_td2048.hip); see frame_td.hip.
 namespace hlds {

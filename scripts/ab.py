@@ -30,7 +30,7 @@ ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--partial", action="store_true", help="time frame_mrc_partial (numerators)")
 ap.add_argument("--ls", action="store_true", help="time frame_estimate (the LS kernel) instead of the MRC")
 ap.add_argument("--demod", action="store_true",
-                help="time frame_demod (LS + MRC: one launch at C = 1024 unless DEMOD1K_FUSED=0)")
+                help="time frame_demod (LS + MRC: one launch at C = 1024 / 2048 / 4096 unless DEMOD_FUSED=0)")
 ap.add_argument("--freq", action="store_true",
                 help="frequency-domain frames: time frame_demod_freq (LS + MRC, no FFT)")
 ap.add_argument("--allocs", type=int, default=1,

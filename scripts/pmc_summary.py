@@ -58,7 +58,7 @@ def main():
     global MRC, LS
     if cfg.get("domain") == "freq":  # bench.py --mode freq
         MRC, LS = "k_mrc_freq", "k_ls_freq"
-    one = cfg.get("flow") == "one-launch"  # bench.py's one-launch flow: k_demod_td1024 is the kernel
+    one = cfg.get("flow") == "one-launch"  # bench.py's one-launch flow: k_demod_td<C> is the kernel
     if one:
         MRC = "k_demod_td"
 

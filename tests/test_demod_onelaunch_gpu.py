@@ -1,16 +1,18 @@
-"""The one-launch C = 1024 frame demod (k_demod_td1024: estimator workgroups
-publish each frame's estimate to the MRC workgroups of the same grid through
-the workspace's flag words).  ofdm_frame_demod at C = 1024 takes this path;
+"""The one-launch frame demod (k_demod_td1024: estimator workgroups publish
+each frame's estimate to the MRC workgroups of the same grid through the
+workspace's flag words; k_demod_td2048 / 4096 in the A/B build only).
+ofdm_frame_demod at C = 1024 takes this path;
 these tests hold it to the two-launch flow (ofdm_frame_estimate +
 ofdm_frame_combine, itself tested against the oracle in test_gpu_parity.py)
 and to the oracle, on shapes with straddling workgroups (8 symbols spanning
 two frames) and tail waves, on a reused workspace with new data (the flags
 of the previous launch must not release the next one), and with the bounded
 wait forced to expire (A/B build: every MRC workgroup estimates its frames
-itself).  Tolerance: helpers.RTOL.  The estimator sums |H|^2 over antennas
-in the 8-wave order (rows w, w+8, ... per wave, then waves in order), the
-two-launch LS in its own wave order, so the outputs agree to rounding, not
-bit for bit."""
+itself).  Tolerance: helpers.RTOL.  At C = 1024 the estimator sums |H|^2
+over antennas in the 8-wave order (rows w, w+8, ... per wave, then waves in
+order), the two-launch LS in its own wave order, so the outputs agree to
+rounding, not bit for bit; at C = 2048 / 4096 (A/B build) the estimator is
+the LS kernel's own code and the outputs are bit-identical."""
 import os
 import subprocess
 import sys
@@ -48,14 +50,14 @@ def two_launch(ofdm, iq, X, prefix):
     return host(out)
 
 
-# (F, S, R, prefix): 100 x 101 x 16 is BASELINE configs[1]; S - 1 = 100 and
-# 6 symbols per frame put workgroups across frame boundaries; 7 x 3 = 21
-# symbols leaves tail waves in the last workgroup; R = 1 and R = 9 leave
-# estimator waves without rows / with one extra row.
-@pytest.mark.parametrize("F,S,R,prefix", [(100, 101, 16, 0), (7, 4, 1, 0), (5, 7, 9, 8), (3, 101, 64, 72),
-                                          (1, 2, 4, 0), (40, 13, 16, 0)])
-def test_one_launch_matches_two_launch(ofdm, dev, F, S, R, prefix):
-    C = 1024
+# (C, F, S, R, prefix): C=1024 100 x 101 x 16 is BASELINE configs[1]; S - 1
+# = 100 and 6 symbols per frame put workgroups across frame boundaries;
+# 7 x 3 = 21 symbols leaves tail waves in the last workgroup; R = 1 and R = 9
+# leave estimator waves without rows / with one extra row.  C = 4096
+# workgroups are frame-aligned (4 symbols): S = 7 leaves tail pairs.
+@pytest.mark.parametrize("C,F,S,R,prefix", [(1024, 100, 101, 16, 0), (1024, 7, 4, 1, 0), (1024, 5, 7, 9, 8),
+                                            (1024, 3, 101, 64, 72), (1024, 1, 2, 4, 0), (1024, 40, 13, 16, 0)])
+def test_one_launch_matches_two_launch(ofdm, dev, C, F, S, R, prefix):
     X = pilots(dev, C - 1)
     iq = ofdm.synth_frames(F, S, R, C, X, prefix=prefix, seed=F * 1000 + S * 10 + R, noise_std=0.01)
     got = host(ofdm.frame_demod(iq, X, prefix))
@@ -66,9 +68,10 @@ def test_one_launch_matches_two_launch(ofdm, dev, F, S, R, prefix):
                                             seed=F * 1000 + S * 10 + R).item()) == 0
 
 
-def test_one_launch_vs_oracle(ofdm, oracle, dev):
+@pytest.mark.parametrize("C", [1024])
+def test_one_launch_vs_oracle(ofdm, oracle, dev, C):
     """First and last frame of a straddling batch against the C oracle."""
-    F, S, R, C, prefix = 6, 7, 5, 1024, 8
+    F, S, R, prefix = 6, 7, 5, 8
     X = pilots(dev, C - 1, seed=9)
     iq = ofdm.synth_frames(F, S, R, C, X, prefix=prefix, seed=77, noise_std=0.02)
     out = host(ofdm.frame_demod(iq, X, prefix))
@@ -78,11 +81,12 @@ def test_one_launch_vs_oracle(ofdm, oracle, dev):
         parity(out[f], ref)
 
 
-def test_reused_workspace_new_data(ofdm, dev):
+@pytest.mark.parametrize("C", [1024])
+def test_reused_workspace_new_data(ofdm, dev, C):
     """Launch N+1 on the workspace of launch N with other frames: its MRC
     workgroups must wait for the new estimates (new epoch), not read the old
     ones the flags of launch N still vouch for."""
-    F, S, R, C = 24, 21, 16, 1024
+    F, S, R = 24, 21, 16
     X = pilots(dev, C - 1)
     a = ofdm.synth_frames(F, S, R, C, X, seed=1, noise_std=0.01)
     b = ofdm.synth_frames(F, S, R, C, X, seed=2, noise_std=0.01)
@@ -135,25 +139,34 @@ def test_graph_capture_takes_two_launches(ofdm, dev):
 @pytest.mark.skipif(not os.path.exists(os.path.join(ROOT, "gpu-accel-ofdm-ls-mrc_amd", "lib",
                                                     "libofdm_lsmrc_ab.so")),
                     reason="A/B build (make -C gpu-accel-ofdm-ls-mrc_amd ab) not present")
-def test_bounded_wait_fallback_ab_build():
-    """OFDM_AB_DEMOD1K_SPIN=0: no MRC workgroup waits for a flag; each
-    estimates its frame(s) itself.  Same outputs as the normal path (run in a
-    child process on the A/B library)."""
+@pytest.mark.parametrize("C", [1024, 2048, 4096])
+def test_bounded_wait_fallback_ab_build(C):
+    """OFDM_AB_DEMOD_SPIN=0: no MRC workgroup waits for a flag; each
+    estimates its frame(s) itself.  Same outputs as the normal path, and the
+    one launch agrees with two (run in a child process on the A/B library)."""
     code = r"""
 import os, sys, numpy as np, torch
 sys.path.insert(0, os.path.join(sys.argv[1], "gpu-accel-ofdm-ls-mrc_amd"))
 import ofdm_lsmrc as ofdm
-F, S, R, C = 9, 13, 16, 1024
+F, S, R, C = 9, 13, 16, int(sys.argv[2])
 a = np.float32(0.70710678); rng = np.random.default_rng(5)
 X = torch.from_numpy((rng.choice([-a, a], C - 1) + 1j * rng.choice([-a, a], C - 1)).astype(np.complex64)).cuda()
 iq = ofdm.synth_frames(F, S, R, C, X, seed=11, noise_std=0.01)
+os.environ["OFDM_AB_DEMOD_FUSED"] = "0"
+two = ofdm.frame_demod(iq, X).cpu().numpy()
+os.environ.pop("OFDM_AB_DEMOD_FUSED")
 ref = ofdm.frame_demod(iq, X).cpu().numpy()
-os.environ["OFDM_AB_DEMOD1K_SPIN"] = "0"
+os.environ["OFDM_AB_DEMOD_SPIN"] = "0"
 got = ofdm.frame_demod(iq, X).cpu().numpy()
 d = np.abs(got - ref).max() / np.abs(ref).max()
-print("maxrel", d)
-sys.exit(0 if d <= 1e-6 else 1)
+d2 = np.abs(ref - two).max() / np.abs(two).max()
+print("maxrel fallback vs one launch", d, "one launch vs two", d2)
+ok = d <= 1e-6 and d2 <= 1e-5 and (C == 1024 or d2 == 0)
+sys.exit(0 if ok else 1)
 """
-    env = dict(os.environ, OFDM_LSMRC_LIB="ab")
-    p = subprocess.run([sys.executable, "-c", code, ROOT], env=env, capture_output=True, text=True, timeout=300)
+    # C = 2048 / 4096: the one-launch kernels of the A/B build (OFDM_AB_DEMOD_WIDE;
+    # no faster than two launches, not in the product), bit-identical to two launches
+    env = dict(os.environ, OFDM_LSMRC_LIB="ab", OFDM_AB_DEMOD_WIDE="1")
+    p = subprocess.run([sys.executable, "-c", code, ROOT, str(C)], env=env, capture_output=True, text=True,
+                       timeout=300)
     assert p.returncode == 0, p.stdout + p.stderr
