@@ -174,7 +174,30 @@ __device__ __forceinline__ void hlds_row_pf(const float2 *next, const float4 *hr
 // during the second half, the Hc exchange and the MAC; no extra registers).
 // Otherwise (a workgroup straddling a frame boundary) each wave loads its
 // own Hc row from L2.
-template <bool SHARED, int DBG = 0>
+// R0: row 0 is already in this wave's transpose image, DMA'd there at the
+// workgroup's start (row0_dma) and landed (vmcnt drained, barrier passed).
+template <bool R0>
+__device__ __forceinline__ void row0(const float2 *sym, int t, const float2 *T, float2 (&a)[16]) {
+    if constexpr (R0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA (the compiler does not count asm loads)
+#pragma unroll
+        for (int m = 0; m < 16; ++m) a[m] = T[t + 64 * m];
+    } else {
+        row_load<true>(sym, t, a);
+    }
+}
+// Row 0 of this wave's symbol (8 KiB) into its transpose image by LDS-DMA:
+// no registers held, in flight through the table fill (and the estimate
+// wait of the one-launch kernel).  The image's row tails carry other waves'
+// Hc words only from row 0's exchange on, after every wave has read row 0.
+__device__ __forceinline__ void row0_dma(const float2 *sym, int t, float2 *T) {
+    const char *src = reinterpret_cast<const char *>(sym) + t * 16;
+    const unsigned dst = lds_addr(T);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) dma16(src + j * 1024, dst + j * 1024);
+}
+
+template <bool SHARED, int DBG = 0, bool R0 = false>
 __device__ __forceinline__ void hlds_rows(const float2 *sym, int Cp, int R, const float4 *Hf, int t,
                                           float2 *T, const float2 *tw1, const float2 *tw2,
                                           float2 *T0, float4 *hfree, float2 (&acc)[16]) {
@@ -183,7 +206,7 @@ __device__ __forceinline__ void hlds_rows(const float2 *sym, int Cp, int R, cons
     for (int k = 0; k < 16; ++k) acc[k] = float2{0.f, 0.f};
     if constexpr (SHARED) {
         float2 a[16];
-        row_load<true>(sym, t, a);
+        row0<R0>(sym, t, T, a);
         const float4 *lo = hfree + t;
         const float4 *hi = hslot(T0, hfree, 256 + t);
         float4 *mine = hslot(T0, hfree, threadIdx.x);
@@ -196,7 +219,10 @@ __device__ __forceinline__ void hlds_rows(const float2 *sym, int Cp, int R, cons
     } else {
         for (int r = 0; r < R; ++r) {
             float2 a[16], x[16], h[16];
-            row_load<true>(sym + (long long)r * Cp, t, a);
+            if (r == 0)
+                row0<R0>(sym, t, T, a);
+            else
+                row_load<true>(sym + (long long)r * Cp, t, a);
             row_fft_a(a, t, T, tw1);
             row_fft_b(t, T, tw2, x);
             __builtin_amdgcn_sched_barrier(0);
@@ -269,7 +295,7 @@ __device__ __forceinline__ void hlds_epilogue(const float2 (&acc)[16], const flo
 // (blocks b and b+8 share an XCD under round-robin dispatch, so a frame's
 // workgroups share its Hc rows in one L2; speed only, never correctness).
 // mode 0: out[q][out_pos(j)] = acc / P;  mode 1: out[q][j] = acc (numerator).
-template <int DBG = 0>
+template <int DBG = 0, bool R0 = false>
 __global__ void __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 4)))
 k_mrc_td1024_hlds(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
                   const float *__restrict__ P, float2 *__restrict__ out, long long nq, long long nblocks,
@@ -285,8 +311,6 @@ k_mrc_td1024_hlds(const float2 *__restrict__ iq, int S, int R, int prefix, const
     const long long pb = blockIdx.x;
     const long long lb = (pb & 7) * per_xcd + (pb >> 3);  // XCD-grouped logical block
     if (lb >= nblocks) return;
-    fill(tw1, tw2);
-    __syncthreads();
 
     // every wave takes part in the per-row barriers: tail waves duplicate the
     // last symbol and do not store
@@ -302,14 +326,17 @@ k_mrc_td1024_hlds(const float2 *__restrict__ iq, int S, int R, int prefix, const
     const int s = 1 + (int)(q % nsym);
     const int Cp = C + prefix;
     const float2 *sym = iq + (f * S + s) * (long long)R * Cp + prefix;
+    if constexpr (R0) row0_dma(sym, t, T);
+    fill(tw1, tw2);
+    __syncthreads();
 
     float2 acc[16];
     if (f0 == fl)
-        hlds_rows<true, DBG>(sym, Cp, R, reinterpret_cast<const float4 *>(Hc + f0 * (long long)R * C), t, T, tw1,
-                        tw2, T0, hfree, acc);
+        hlds_rows<true, DBG, R0>(sym, Cp, R, reinterpret_cast<const float4 *>(Hc + f0 * (long long)R * C), t, T,
+                                 tw1, tw2, T0, hfree, acc);
     else
-        hlds_rows<false>(sym, Cp, R, reinterpret_cast<const float4 *>(Hc + f * (long long)R * C), t, T, tw1,
-                         tw2, T0, hfree, acc);
+        hlds_rows<false, 0, R0>(sym, Cp, R, reinterpret_cast<const float4 *>(Hc + f * (long long)R * C), t, T,
+                                tw1, tw2, T0, hfree, acc);
     if (!store) return;
     hlds_epilogue<DBG>(acc, P, f, q, t, T, out, mode);
 }
@@ -393,7 +420,7 @@ __device__ __forceinline__ void hlds_ls_frame(const float2 *__restrict__ iq, int
 // same XCD left dirty (wave_fft1024.hpp: publish_flag / consume_flags;
 // same-process A/B vs plain stores + release fence: equal to 1 % faster,
 // DESIGN.md 4.6).
-template <int DBG = 0>
+template <int DBG = 0, bool R0 = false>
 __global__ void __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 4)))
 k_demod_td1024(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ X, float2 *Hc,
                float *P, float2 *__restrict__ out, long long nq, long long nblocks, long long per_xcd,
@@ -420,7 +447,6 @@ k_demod_td1024(const float2 *__restrict__ iq, int S, int R, int prefix, const fl
     const long long pb = blockIdx.x - nls;
     const long long lb = (pb & 7) * per_xcd + (pb >> 3);  // XCD-grouped logical block
     if (lb >= nblocks) return;
-    fill(tw1, tw2);
 
     const int nsym = S - 1;
     const long long qw = lb * HW + w;
@@ -432,22 +458,27 @@ k_demod_td1024(const float2 *__restrict__ iq, int S, int R, int prefix, const fl
     const int s = 1 + (int)(q % nsym);
     const int Cp = C + prefix;
     const float2 *sym = iq + (f * S + s) * (long long)R * Cp + prefix;
+    if constexpr (R0) row0_dma(sym, t, T);  // in flight through the wait
+    fill(tw1, tw2);
 
     // wait for the estimates of frames f0 .. fl (hfree, not used before the
     // rows, carries the outcome); not published in time: estimate here
     // (identical bytes) and read them back behind an acquire of our own
     if (!consume_flags(flags, f0, fl, epoch, spin_ticks, reinterpret_cast<int *>(hfree))) {
+        if constexpr (R0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA lands before the images are reused
+        __syncthreads();
         for (long long ff = f0; ff <= fl; ++ff) hlds_ls_frame(iq, S, R, prefix, X, Hc, P, ff, w, t, T, T0, tw1, tw2);
         acquire_all();
+        if constexpr (R0) row0_dma(sym, t, T);  // the estimate used the images: again
     }
 
     float2 acc[16];
     if (f0 == fl)
-        hlds_rows<true, DBG>(sym, Cp, R, reinterpret_cast<const float4 *>(Hc + f0 * (long long)R * C), t, T, tw1,
-                             tw2, T0, hfree, acc);
+        hlds_rows<true, DBG, R0>(sym, Cp, R, reinterpret_cast<const float4 *>(Hc + f0 * (long long)R * C), t, T,
+                                 tw1, tw2, T0, hfree, acc);
     else
-        hlds_rows<false>(sym, Cp, R, reinterpret_cast<const float4 *>(Hc + f * (long long)R * C), t, T, tw1, tw2,
-                         T0, hfree, acc);
+        hlds_rows<false, 0, R0>(sym, Cp, R, reinterpret_cast<const float4 *>(Hc + f * (long long)R * C), t, T,
+                                tw1, tw2, T0, hfree, acc);
     if (!store) return;
     hlds_epilogue<DBG>(acc, P, f, q, t, T, out, 0);
 }
@@ -499,8 +530,13 @@ hipError_t launch_mrc_td1024(const float2 *iq, long long nframes, int S, int R, 
     const long long nb = (nq + hlds::WAVES - 1) / hlds::WAVES;
     const long long pxcd = (nb + 7) / 8;
     if (pxcd * 8 > 0x7fffffffll) return hipErrorInvalidValue;
-    auto kern = k_mrc_td1024_hlds<0>;
+    // R0: each wave's row 0 DMA'd into its transpose image ahead of the table
+    // fill (same process, bit-identical: R=16 x 100 frames 0.301 -> 0.293 ms,
+    // R=64 x 400 3.961 -> 3.922; profiles/r3/r3p_row0_dma_ab.jsonl).  The
+    // one-launch kernel loses with it (+3-5 %) and keeps the register load.
+    auto kern = k_mrc_td1024_hlds<0, true>;
 #ifdef OFDM_AB_KNOBS
+    if (!ab_knob("MRC1K_R0", 1)) kern = k_mrc_td1024_hlds<0, false>;  // row 0 by register load (round 2)
     switch (ab_knob("MRC1K_DBG", 0)) {
         case 1: kern = k_mrc_td1024_hlds<1>; break;
         case 2: kern = k_mrc_td1024_hlds<2>; break;
@@ -530,7 +566,10 @@ hipError_t launch_demod_td1024(const float2 *iq, long long nframes, int S, int R
     const long long pxcd = (nb + 7) / 8;
     const long long nls = (nframes + 7) / 8 * 8;
     if (pxcd * 8 + nls > 0x7fffffffll) return hipErrorInvalidValue;
-    auto kern = k_demod_td1024<0>;
+    auto kern = k_demod_td1024<0, false>;
+#ifdef OFDM_AB_KNOBS
+    if (ab_knob("MRC1K_R0", 0)) kern = k_demod_td1024<0, true>;  // row 0 by LDS-DMA
+#endif
     hipLaunchKernelGGL(kern, dim3((unsigned)(nls + pxcd * 8)), dim3(64 * hlds::WAVES), hlds::LDS_BYTES, s, iq, S,
                        R, prefix, X, Hc, P, out, nq, nb, pxcd, flags, epoch, (int)nls, nframes,
                        (long long)ab_knob("DEMOD_SPIN", (int)SPIN_TICKS));
