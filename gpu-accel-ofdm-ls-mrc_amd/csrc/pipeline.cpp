@@ -85,7 +85,10 @@ void release(ofdm_pipeline *p) {
     for (auto &s : p->slots) {
         if (s.iq) (void)hipFree(s.iq);
         if (s.out) (void)hipFree(s.out);
-        if (s.ws) (void)hipFree(s.ws);
+        if (s.ws) {
+            (void)ofdm_workspace_release(s.ws);  // its registry entry must not outlive the memory
+            (void)hipFree(s.ws);
+        }
         if (s.in_done) (void)hipEventDestroy(s.in_done);
         if (s.comp_done) (void)hipEventDestroy(s.comp_done);
         if (s.out_done) (void)hipEventDestroy(s.out_done);
