@@ -110,6 +110,36 @@ def test_reused_workspace_new_data(ofdm, dev, C):
     parity(host(e[1]), host(e2[1]), rtol=RTOL)
 
 
+def test_one_launch_under_uneven_load(ofdm, dev):
+    """The hand-off under uneven load (cdna_hip_programming.md Guideline 16:
+    test with the GPU busy elsewhere, consumers L1-warm): frame_demod runs
+    repeatedly on one stream while another stream streams a large
+    elementwise kernel, on a reused workspace, with the batch alternating
+    between two inputs; every output must match its two-launch reference."""
+    import torch
+    F, S, R, C = 60, 13, 16, 1024
+    X = pilots(dev, C - 1)
+    a = ofdm.synth_frames(F, S, R, C, X, seed=21, noise_std=0.01)
+    b = ofdm.synth_frames(F, S, R, C, X, seed=22, noise_std=0.01)
+    ref = {0: two_launch(ofdm, a, X, 0), 1: two_launch(ofdm, b, X, 0)}
+    ws = ofdm.workspace(F, S, R, C, dev)
+    outs = [ofdm.c64((F, S - 1, C - 1), dev) for _ in range(6)]
+    hog = torch.empty(1 << 28, dtype=torch.float32, device=dev).uniform_()
+    busy, work = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    with torch.cuda.stream(busy):
+        for _ in range(6):
+            hog.mul_(1.0000001).add_(1e-7)
+    for i, o in enumerate(outs):
+        ofdm.frame_demod(a if i % 2 == 0 else b, X, 0, ws=ws, out=o, stream=work)
+        if i == 2:
+            with torch.cuda.stream(busy):
+                hog.mul_(0.9999999)
+    torch.cuda.synchronize()
+    for i, o in enumerate(outs):
+        parity(host(o), ref[i % 2])
+
+
 def test_graph_capture_takes_two_launches(ofdm, dev):
     """Under stream capture ofdm_frame_demod uses the two launches (a frozen
     epoch would let a replay read stale estimates); the replayed graph then
