@@ -236,7 +236,14 @@ __device__ __forceinline__ void dma_hc_row(const float2 *g, unsigned lds) {
 // after this row's first barrier.  HP = 2 (A/B candidate): ONE Hc buffer,
 // refilled after a third barrier once every wave has read both planes of this
 // row (before its second FFT) and published at the next row's second barrier.
-template <int E, int PK, bool PREF, int DBG = 0, int TW = 3, int HP = 4, int HE = 0, int IL = 0>
+// SW (IL rows only): the pair's two images swap roles every row -- the
+// exchange half goes into the image this wave transposed in the previous
+// row, the partner's half is read from the other, and this wave's FFT
+// transposes then reuse the image it just read (its own reads precede its
+// writes in LDS order; the partner no longer touches it), so the second
+// workgroup barrier of the row (partner done reading before the FFT
+// overwrites) is not needed.  T = the image written, Tp = the image read.
+template <int E, int PK, bool PREF, int DBG = 0, int TW = 3, int HP = 4, int HE = 0, int IL = 0, bool SW = false>
 __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const float2 *__restrict__ hr,
                                       int t, float2 *T, const float2 *Tp, const float2 *tw1,
                                       const float2 *tw2, pk::v2f wb0, pk::v2f wb1, float2 (&a)[16],
@@ -263,7 +270,7 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
         else v[m] = V(Tp[hl::swz(m, t)]);    // c
     }
     if (HP != 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this row's Hc DMA landed
-    if (!(DBG & 1) && !(DBG & 8)) td1024::lds_barrier();  // the partner has read T before the FFT reuses it
+    if (!SW && !(DBG & 1) && !(DBG & 8)) td1024::lds_barrier();  // the partner has read T before the FFT reuses it
     // E = 0: u = a, v = c:  z0 = a + c, z2 = (a - c) W^(2 n0)
     // E = 1: u = b, v = d:  z1 = (b + (-i) d) W^(n0), z3 = (b - (-i) d) W^(3 n0)
 #pragma unroll
@@ -293,6 +300,7 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
     float2 z[16], x[16];
     if constexpr (IL != 0) {
         static_assert(PK == 7 && TW == 3 && HP == 4, "the interleaved row uses the packed, recurrence-twiddle FFT");
+        float2 *TF = SW ? const_cast<float2 *>(Tp) : T;  // the FFT's transpose image
         // Both FFT1024s of the row software-pipelined through the one
         // transpose image: A(u) -> write(u) -> read(u) issued -> A(v) computed
         // while u's transpose is in flight -> write(v), read(v) issued (LDS
@@ -311,11 +319,11 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
         (void)cb;
         const hl::TwAnchors a_tw = hl::anchors_a(tw1, t);
         hl::fa_compute(u, a_tw);
-        hl::fa_write(u, t, T);
-        hl::fb_read(t, T, xu);
+        hl::fa_write(u, t, TF);
+        hl::fb_read(t, TF, xu);
         hl::fa_compute(v, a_tw);
-        hl::fa_write(v, t, T);
-        hl::fb_read(t, T, u);  // u's registers are free: v's transpose lands in them
+        hl::fa_write(v, t, TF);
+        hl::fb_read(t, TF, u);  // u's registers are free: v's transpose lands in them
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int k = 0; k < 16; ++k) h[k] = hr[k * 64 + t];  // plane 0, lands during B(u)
@@ -426,7 +434,7 @@ constexpr size_t H_LDS = h_lds(H_PAIRS);
 static_assert(H_LDS <= 160 * 1024, "one workgroup per CU");
 static_assert(2 * h_lds(2) <= 160 * 1024, "two 2-pair workgroups per CU");
 
-template <int E, int PK, int DBG = 0, int TW = 3, int HP = 4, int HE = 0, int IL = 0>
+template <int E, int PK, int DBG = 0, int TW = 3, int HP = 4, int HE = 0, int IL = 0, bool SW = false>
 __device__ __forceinline__ void h_rows(const float2 *sym, int Cp, int R, const float2 *Hg, float2 *HB, int t,
                                        float2 *T, const float2 *Tp, const float2 *tw1, const float2 *tw2,
                                        pk::v2f wb0, pk::v2f wb1, float2 (&ae)[16], float2 (&ao)[16]) {
@@ -453,12 +461,17 @@ __device__ __forceinline__ void h_rows(const float2 *sym, int Cp, int R, const f
     const unsigned hb0 = lds_addr(HB), hb1 = lds_addr(HB + C);
     constexpr int NB = HP == 4 ? 2 : 1;  // Hc buffers
     const hl::TwAnchors ca = {}, cb = {};  // (read per row inside x_row)
+    // SW: odd rows swap the images (x_row)
+    float2 *Tq = const_cast<float2 *>(Tp);
     for (int r = 0; r + 1 < R; ++r)
-        x_row<E, PK, true, DBG, TW, HP, HE, IL>(sym + (long long)(r + 1) * Cp, HB + (NB == 2 ? (r & 1) * C : 0) + E * 2048,
-                                        t, T, Tp, tw1, tw2, wb0, wb1, a, b, ae, ao, Hg + (long long)(r + 1) * C,
-                                        NB == 2 && !(r & 1) ? hb1 : hb0, ca, cb);
-    x_row<E, PK, false, DBG, TW, HP, HE, IL>(sym, HB + (NB == 2 ? ((R - 1) & 1) * C : 0) + E * 2048, t, T, Tp, tw1, tw2,
-                                     wb0, wb1, a, b, ae, ao, nullptr, 0, ca, cb);
+        x_row<E, PK, true, DBG, TW, HP, HE, IL, SW>(sym + (long long)(r + 1) * Cp,
+                                                    HB + (NB == 2 ? (r & 1) * C : 0) + E * 2048, t,
+                                                    SW && (r & 1) ? Tq : T, SW && (r & 1) ? T : Tp, tw1, tw2, wb0,
+                                                    wb1, a, b, ae, ao, Hg + (long long)(r + 1) * C,
+                                                    NB == 2 && !(r & 1) ? hb1 : hb0, ca, cb);
+    x_row<E, PK, false, DBG, TW, HP, HE, IL, SW>(sym, HB + (NB == 2 ? ((R - 1) & 1) * C : 0) + E * 2048, t,
+                                                 SW && ((R - 1) & 1) ? Tq : T, SW && ((R - 1) & 1) ? T : Tp, tw1,
+                                                 tw2, wb0, wb1, a, b, ae, ao, nullptr, 0, ca, cb);
 }
 
 constexpr int H_PK = 7;  // packed-f32 split, FFT halves and MAC (pk.hpp)
@@ -466,7 +479,7 @@ constexpr int H_PK = 7;  // packed-f32 split, FFT halves and MAC (pk.hpp)
 // The MRC of one logical block (HP pairs = HP data symbols of frame f, pair
 // `pair` on symbol j < nsym when `store`; s = its symbol slot) after the
 // workgroup prologue: Hc row 0 DMA, tables, rows, normalise, staged stores.
-template <int DBG = 0, int TW = 3, int HP = H_PAIRS, int HE = 0, int IL = 0>
+template <int DBG = 0, int TW = 3, int HP = H_PAIRS, int HE = 0, int IL = 0, bool SW = false>
 __device__ __forceinline__ void mrc4096_block(const float2 *__restrict__ iq, int S, int R, int prefix,
                                               const float2 *Hc, const float *P, float2 *__restrict__ out,
                                               long long f, int j, bool store, int s, float2 *lds, int mode) {
@@ -490,9 +503,9 @@ __device__ __forceinline__ void mrc4096_block(const float2 *__restrict__ iq, int
 #pragma unroll
     for (int k = 0; k < 16; ++k) ae[k] = ao[k] = float2{0.f, 0.f};
     if (e)
-        h_rows<1, H_PK, DBG, TW, HP, HE, IL>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
+        h_rows<1, H_PK, DBG, TW, HP, HE, IL, SW>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
     else
-        h_rows<0, H_PK, DBG, TW, HP, HE, IL>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
+        h_rows<0, H_PK, DBG, TW, HP, HE, IL, SW>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
     const long long q = f * nsym + j;
     const int b0 = lane_bin0(t);
     float2 *o = out + q * K;
@@ -569,7 +582,7 @@ __device__ __forceinline__ void mrc4096_block(const float2 *__restrict__ iq, int
     }
 }
 
-template <int DBG = 0, int TW = 3, int HP = H_PAIRS, int HE = 0, int IL = 0>
+template <int DBG = 0, int TW = 3, int HP = H_PAIRS, int HE = 0, int IL = 0, bool SW = false>
 __global__ void __attribute__((amdgpu_flat_work_group_size(128 * HP, 128 * HP), amdgpu_waves_per_eu(2, 2)))
 k_mrc_td4096h(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
               const float *__restrict__ P, float2 *__restrict__ out, long long nframes, long long nblocks,
@@ -585,7 +598,7 @@ k_mrc_td4096h(const float2 *__restrict__ iq, int S, int R, int prefix, const flo
     const int j = (int)(lb - f * bpf) * HP + pair;  // data symbol index within the frame
     const bool store = j < nsym;
     const int s = 1 + (store ? j : nsym - 1);
-    mrc4096_block<DBG, TW, HP, HE, IL>(iq, S, R, prefix, Hc, P, out, f, j, store, s, lds, mode);
+    mrc4096_block<DBG, TW, HP, HE, IL, SW>(iq, S, R, prefix, Hc, P, out, f, j, store, s, lds, mode);
 }
 
 
@@ -680,6 +693,7 @@ hipError_t launch_mrc_td4096(const float2 *iq, long long nframes, int S, int R, 
     if (ab_knob("MRC4K_IL", 0) == 3) kern = k_mrc_td4096h<0, 3, H_PAIRS, 0, 3>;  // + a quarter at row start
     if (ab_knob("MRC4K_IL", 0) == 67) kern = k_mrc_td4096h<64, 3, H_PAIRS, 0, 3>;  // IL=3 compute only (diag)
     if (ab_knob("MRC4K_IL", 0) == 65) kern = k_mrc_td4096h<64, 3, H_PAIRS, 0, 1>;  // + compute only (diag)
+    if (ab_knob("MRC4K_SW", 0) == 1) kern = k_mrc_td4096h<0, 3, H_PAIRS, 0, 3, true>;  // one barrier per row
     if (ab_knob("MRC4K_HP", 4) == 2) {  // two independent 2-pair workgroups per CU, single Hc buffer
         const long long bpf2 = ((S - 1) + 1) / 2, nb2 = nframes * bpf2, px2 = (nb2 + 7) / 8;
         if (px2 * 8 > 0x7fffffffll) return hipErrorInvalidValue;
