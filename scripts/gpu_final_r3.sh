@@ -20,7 +20,7 @@ mkdir -p $OUT/profiles && cp profiles/${TAG}* profiles/pmc_traffic.json $OUT/pro
 run() { name=$1; shift
   timeout -k 10 400 python -u bench.py "$@" > $OUT/$name.json 2> $OUT/$name.err
   rc=$?; echo "$name rc=$rc"; tail -c 400 $OUT/$name.json; echo; [ $rc -eq 0 ]; }
-run bench && run bench_cfg1 --no-cpu --no-mode-a --R 16 --frames 100 --steps 50 && \
+run bench && run bench_cfg1 --no-cpu --no-mode-a --R 16 --frames 100 --steps 200 --warmup 20 && \
 run bench_c2048 --no-cpu --no-mode-a --steps 10 --R 64 --C 2048 --frames 1000 && \
 run bench_c4096 --no-cpu --no-mode-a --steps 10 --R 32 --C 4096 --frames 400 && \
 run bench_split --no-cpu --mode split --steps 10 || exit 1
