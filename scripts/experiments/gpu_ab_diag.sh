@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # Diagnostic A/B of the three fused MRC kernels (A/B build, scripts/ab.py):
 # default vs no barriers / no Hc / no stores, plus the read-bandwidth probe of
-# the same box.  usage: bash scripts/gpu_ab_diag.sh <tag>
+# the same box.  usage: bash scripts/experiments/gpu_ab_diag.sh <tag>
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=gpurun_out/abdiag_${1:-x}; mkdir -p $OUT

@@ -2,7 +2,7 @@
 # Frequency-domain LS + MRC (SURVEY.md 8(d) mode A) in one GPU session:
 # its parity tests, rocprofv3 stats + FETCH/WRITE PMC of bench.py --mode freq
 # (summarised into profiles/<tag>_freq_*), then the un-profiled bench lines.
-# usage: bash scripts/gpu_freq.sh <tag>
+# usage: bash scripts/experiments/gpu_freq.sh <tag>
 set -o pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$ROOT"; mkdir -p gpurun_out

@@ -12,4 +12,4 @@ if [ -z "$SKIP_TESTS" ]; then
 fi
 timeout -k 10 300 python -u scripts/libab.py --reps 2 --shapes 2048:64:400 --extra=--ls prod base > gpurun_out/ilp2k/ls.txt 2>&1
 timeout -k 10 300 python -u bench.py --C 2048 --R 64 --frames 1000 --no-cpu --no-mode-a > gpurun_out/ilp2k/bench.json 2> gpurun_out/ilp2k/bench.err
-bash scripts/gpu_prof_cfg.sh r2f_c2048 --C 2048 --R 64 --frames 1000 > gpurun_out/ilp2k/prof.txt 2>&1
+bash scripts/experiments/gpu_prof_cfg.sh r2f_c2048 --C 2048 --R 64 --frames 1000 > gpurun_out/ilp2k/prof.txt 2>&1

@@ -6,4 +6,4 @@ mkdir -p gpurun_out/pk2k
 timeout -k 10 400 python -u -m pytest tests -m gpu -k "2048" -x -q --timeout 120 --timeout-method thread \
     > gpurun_out/pk2k/gpu_2048.log 2>&1
 timeout -k 10 300 python -u bench.py --C 2048 --R 64 --frames 1000 --no-cpu --no-mode-a > gpurun_out/pk2k/bench.json 2> gpurun_out/pk2k/bench.err
-bash scripts/gpu_prof_cfg.sh r2h_c2048 --C 2048 --R 64 --frames 1000 > gpurun_out/pk2k/prof.txt 2>&1
+bash scripts/experiments/gpu_prof_cfg.sh r2h_c2048 --C 2048 --R 64 --frames 1000 > gpurun_out/pk2k/prof.txt 2>&1

@@ -1,5 +1,5 @@
 # PMC counters of the MRC kernel for a list of variants (ab_mrc.py workload).
-# usage: [PMC_SETS="A B;C D"] [AB_FRAMES=400] bash scripts/gpu_pmc_ab.sh <tag> default VAR=VAL[,..] ...
+# usage: [PMC_SETS="A B;C D"] [AB_FRAMES=400] bash scripts/experiments/gpu_pmc_ab.sh <tag> default VAR=VAL[,..] ...
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
 TAG=$1; shift
 OUT=$GRAFT_REPO_ROOT/gpurun_out/pmcab_$TAG; mkdir -p $OUT

@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# Profile a non-default bench shape: bash scripts/gpu_prof_cfg.sh <tag> [bench args]
+# Profile a non-default bench shape: bash scripts/experiments/gpu_prof_cfg.sh <tag> [bench args]
 set -o pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$ROOT"; mkdir -p gpurun_out

@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
 # Round 3 GPU session: parity suite + smoke, then bench lines.
-# usage: [AB="ab.py args"] bash scripts/gpu_r3.sh <tag> [bench-set]
+# usage: [AB="ab.py args"] bash scripts/experiments/gpu_r3.sh <tag> [bench-set]
 #   bench-set: "base" (default: headline + split + configs[1] + C=4096) or "none"
 set -o pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}

@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
 # SQ counters (two passes, 8 SQ counters each) of MRC kernel variants from the
-# A/B build, one short ab.py run per pass: scripts/gpu_sq_ab.sh <tag> <C> <R> <variants...>
+# A/B build, one short ab.py run per pass: scripts/experiments/gpu_sq_ab.sh <tag> <C> <R> <variants...>
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-$(pwd)}
 export TMPDIR=/tmp
@@ -14,4 +14,4 @@ for P in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ
     python3 scripts/ab.py --C $C --R $R --frames 100 --reps 1 "$@" > $OUT/p$i.jsonl 2> $OUT/p$i.err
   rc=$?; echo "pass $i rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
-python3 scripts/sq_table.py $OUT
+python3 scripts/experiments/sq_table.py $OUT

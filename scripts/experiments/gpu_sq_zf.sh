@@ -12,4 +12,4 @@ for P in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ
     python3 scripts/zf_ab.py --U 16 --nsym 4000 --reps 1 > $OUT/p$i.jsonl 2> $OUT/p$i.err
   rc=$?; echo "pass $i rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
-python3 scripts/sq_table.py $OUT k_zf_
+python3 scripts/experiments/sq_table.py $OUT k_zf_

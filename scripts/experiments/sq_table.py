@@ -1,5 +1,5 @@
-"""Per-kernel-variant table of the SQ counters collected by scripts/gpu_sq_ab.sh.
-usage: python scripts/sq_table.py gpurun_out/sqab_<tag> [kernel-name filter, default k_mrc_td]
+"""Per-kernel-variant table of the SQ counters collected by scripts/experiments/gpu_sq_ab.sh.
+usage: python scripts/experiments/sq_table.py gpurun_out/sqab_<tag> [kernel-name filter, default k_mrc_td]
 WAVE/WAIT/ACTIVE counters are quad-cycles (MI355X_MICROARCH.md); ratios are
 per wave lifetime (SQ_WAVE_CYCLES)."""
 import csv
