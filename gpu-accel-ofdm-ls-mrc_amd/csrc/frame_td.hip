@@ -469,7 +469,14 @@ k_demod_td1024(const float2 *__restrict__ iq, int S, int R, int prefix, const fl
         __syncthreads();
         for (long long ff = f0; ff <= fl; ++ff) hlds_ls_frame(iq, S, R, prefix, X, Hc, P, ff, w, t, T, T0, tw1, tw2);
         acquire_all();
-        if constexpr (R0) row0_dma(sym, t, T);  // the estimate used the images: again
+        if constexpr (R0) {  // the estimate used the images: again
+            // the symbol pointer laundered so that the compiler recomputes
+            // the 8 DMA addresses here instead of keeping (spilling) the
+            // first DMA's across the wait
+            const float2 *sym2 = sym;
+            asm volatile("" : "+s"(sym2));
+            row0_dma(sym2, t, T);
+        }
     }
 
     float2 acc[16];
