@@ -1214,11 +1214,14 @@ k_zf_mfma_w128(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__
 // crosses the memory system per symbol.  Lane (b, i) = block b = subcarrier
 // k0 + b, as k_zf_mfma; A operands from LDS ([n][16 rows][16 subcarriers],
 // rows >= M zero), input operands from global memory, prefetched PD n-steps
-// ahead in registers.
+// ahead in registers.  PD = 2: same-process A/B at R = 64, 10 000 symbols,
+// bit-identical (profiles/r3/r3z6_zf_detect_prefetch_depth.jsonl): detect
+// U = 16 1.91 ms at PD = 3 (round 3) -> 1.85, U = 32 3.54 -> 3.34; PD = 1
+// and PD = 5 are slower than both.
 // XMAP: block b runs on XCD b % 8 (round-robin dispatch; speed only): the
 // chunk is b % 8 + 8 (b / (8 nkb)) and the subcarrier block (b / 8) % nkb, so
 // one XCD reads all subcarrier pieces of the same symbol rows.
-template <bool CONJ, bool XMAP = false, int MR = 16>
+template <bool CONJ, bool XMAP = false, int MR = 16, int PDT = 2>
 __global__ void __attribute__((amdgpu_flat_work_group_size(MR == 64 ? 256 : 512, MR == 64 ? 256 : 512),
                                amdgpu_waves_per_eu(MR == 64 ? 1 : 2, MR == 64 ? 1 : 2)))
 k_zf_wstat(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__restrict__ in, int N, int M, int K,
@@ -1226,7 +1229,7 @@ k_zf_wstat(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__rest
     // MR rows per tile: 16 (MP = 8 row pairs x SG = 4 symbol quads per wave) or
     // 64 (apply at U = 16: all R = 64 output rows, MP = 32 x SG = 1)
     // MR = 64: 4-wave workgroups, one wave per SIMD (512 registers for 128 accumulators + 32 A pairs)
-    constexpr int MP = MR / 2, SG = MR == 16 ? 4 : 1, SW = 4 * SG, PD = 3, TR = MR * 16, NW = MR == 64 ? 4 : 8;
+    constexpr int MP = MR / 2, SG = MR == 16 ? 4 : 1, SW = 4 * SG, PD = PDT, TR = MR * 16, NW = MR == 64 ? 4 : 8;
     extern __shared__ __attribute__((aligned(16))) float2 smd[];  // [N][MR][16]
     // tile = (subcarrier block, 16-row block); the row blocks of one subcarrier
     // block are adjacent in dispatch order, so they read the same input rows
@@ -1668,7 +1671,7 @@ hipError_t mfma_w128_launch(const float2 *Wt, int a_m, int a_n, const float2 *in
     return hipGetLastError();
 }
 
-template <bool CONJ, bool XMAP, int MR = 16>
+template <bool CONJ, bool XMAP, int MR = 16, int PD = 2>
 hipError_t wstat_launch(const float2 *Wt, int a_m, int a_n, const float2 *in, int N, int M, int K,
                         long long nsym, float2 *out, hipStream_t s) {
     const size_t lds = (size_t)N * MR * 16 * sizeof(float2);  // N * MR <= 1152: <= 144 KiB
@@ -1682,7 +1685,7 @@ hipError_t wstat_launch(const float2 *Wt, int a_m, int a_n, const float2 *in, in
     if (XMAP) nchunk = (nchunk + 7) / 8 * 8;  // empty chunks return at once
     const long long blocks = (long long)nkb * nmb * nchunk;
     if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
-    auto kern = zf::k_zf_wstat<CONJ, XMAP, MR>;
+    auto kern = zf::k_zf_wstat<CONJ, XMAP, MR, PD>;
     if (hipError_t e = opt_in_lds(reinterpret_cast<const void *>(kern), 72 * 256 * (int)sizeof(float2));
         e != hipSuccess)
         return e;
@@ -1720,6 +1723,10 @@ hipError_t gemm_dispatch(const float2 *Wt, int a_m, int a_n, const float2 *in, i
     if (mode == 5) return mfma_lds8_launch<4, 8, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
     if (mode == 8 && N <= 72) return wstat_launch<CONJ, false>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
     if (mode == 10 && N <= 18) return wstat_launch<CONJ, true, 64>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+    // input prefetch depth of the W-stationary kernel: 11 PD = 5, 13 PD = 3, 14 PD = 1 (default 2)
+    if (mode == 11 && N <= 72) return wstat_launch<CONJ, true, 16, 5>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+    if (mode == 13 && N <= 72) return wstat_launch<CONJ, true, 16, 3>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+    if (mode == 14 && N <= 72) return wstat_launch<CONJ, true, 16, 1>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
     if (mode == 4) {
         if (ab_knob("ZF_SG", 4) == 8) return mfma_lds_launch<8, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
         return mfma_lds_launch<4, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
