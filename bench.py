@@ -25,11 +25,21 @@ cpu_baseline: the oracle's C restatement of cpuLS.hpp (oracle/) with its
 
 python bench.py [--gpus N] [--steps K] [--warmup W]
 torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+
+`python bench.py --gpus N` (N > 1) without torchrun starts the N ranks
+itself: the launcher process never touches the GPU (it only counts the
+visible devices, which does not initialise HIP), starts N fresh child
+processes of this script with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set,
+and exits with their status.  Fewer visible GPUs than N is an error (exit
+2), never a silent scale-down; OFDM_BENCH_SHARE_GPU=1 (tests only) maps the
+ranks onto the visible GPUs round-robin.
 """
 import argparse
 import glob
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -137,7 +147,11 @@ def cpu_baseline(args, X, ofdm, torch, dev):
     d1 = time.perf_counter() - t0
     fft = "none (frequency-domain input)" if freq else \
         "float32 scalar radix-2 (oracle_fft_row_f32, twiddle table reused; FFTW's SIMD codelets are not available here)"
-    return {"value": syms / dt, "unit": "symbols/s", "cores": threads, "kind": "port", "fft": fft,
+    # cores = the threads the sample ran on (the bench contract); the host's
+    # own count (sched_getaffinity: on the GPU box the whole machine, of which
+    # this job's CPU share is 16) is reported beside it
+    return {"value": syms / dt, "unit": "symbols/s", "cores": threads, "threads": threads,
+            "host_cores_affinity": cores, "host_cpu_share": 16, "kind": "port", "fft": fft,
             "sample": f"{passes} x {nf} frames x {args.S} symbols (R={args.R}, C={args.C}, prefix="
                       f"{args.prefix}), {'LS+MRC+rotate (frequency domain)' if freq else 'FFT+LS+MRC+rotate'}, "
                       f"FFT: {'none' if freq else 'float32 scalar radix-2'}, OpenMP over frames, "
@@ -168,8 +182,62 @@ def pmc_traffic(path, cfg):
     return None, None
 
 
+def visible_gpus():
+    """Visible device count without initialising HIP in this process
+    (torch.cuda.device_count() does not, on this image)."""
+    import torch
+    return torch.cuda.device_count()
+
+
+def free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """--gpus N > 1 without a launcher: N fresh child processes of this
+    script, one per GPU (never an exec of this process).  Returns the exit
+    status: the first non-zero child status (the others are then
+    terminated, so no rank waits forever in a collective), else 0."""
+    share = os.environ.get("OFDM_BENCH_SHARE_GPU") == "1"
+    have = visible_gpus()
+    if have < n and not share:
+        log(f"error: --gpus {n} but only {have} GPU(s) visible; refusing to run fewer ranks "
+            f"(OFDM_BENCH_SHARE_GPU=1 shares GPUs for rehearsals only)")
+        return 2
+    if have < 1:
+        log("error: no GPU visible")
+        return 2
+    port = os.environ.get("MASTER_PORT") or str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            st = p.poll()
+            if st is None:
+                continue
+            live.remove(p)
+            if st != 0 and rc == 0:
+                rc = st if st > 0 else 1
+                log(f"error: rank {procs.index(p)} exited with status {st}; stopping the other ranks")
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
 def main():
     args = parse()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     import torch
     import torch.distributed as dist
     import ofdm_lsmrc as ofdm
@@ -178,13 +246,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+        log(f"error: --gpus {args.gpus} but WORLD_SIZE={world}")
+        sys.exit(2)
     # rehearsal of the N > 1 path on fewer GPUs (tests only, never the
     # measurement): OFDM_BENCH_SHARE_GPU=1 maps ranks onto the visible GPUs
     # round-robin, OFDM_BENCH_BACKEND=gloo replaces RCCL (which refuses two
     # ranks on one GPU)
+    have = torch.cuda.device_count()
     if os.environ.get("OFDM_BENCH_SHARE_GPU") == "1":
-        local = local % max(1, torch.cuda.device_count())
+        local = local % max(1, have)
+    elif local >= have:
+        log(f"error: rank {rank} needs GPU {local} but only {have} visible")
+        sys.exit(2)
     backend = os.environ.get("OFDM_BENCH_BACKEND", "nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -258,10 +331,16 @@ def main():
         if evs:
             evs[2].record(stream)
 
-    for _ in range(args.warmup):
+    for _ in range(max(1, args.warmup)):
         step()
     torch.cuda.synchronize()
-    errs = int(ofdm.count_symbol_errors(out, S, seed=args.seed, frame0=rank * F).item())
+    errs_warm = int(ofdm.count_symbol_errors(out, S, seed=args.seed, frame0=rank * F).item())
+    # the timed steps recompute the same output from the same input: their
+    # last output must equal the warm-up's bit for bit (guards the one-launch
+    # kernel's inter-workgroup estimate hand-off on the credited run)
+    warm_out = out.clone()
+    out.zero_()
+    torch.cuda.synchronize()
 
     events = [[None] + [torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.steps)]
     ev0 = torch.cuda.Event(enable_timing=True)
@@ -281,13 +360,19 @@ def main():
     mrc_all = sorted(e[0 if one else 1].elapsed_time(e[2]) for e in events)
     mrc_ms = sum(mrc_all) / args.steps
     mrc_median = mrc_all[len(mrc_all) // 2]
-    stats = torch.tensor([elapsed, float(errs)], dtype=torch.float64, device=dev)
+    errs = int(ofdm.count_symbol_errors(out, S, seed=args.seed, frame0=rank * F).item())
+    same = bool(torch.equal(out, warm_out))
+    del warm_out
+    stats = torch.tensor([elapsed, float(errs), float(errs_warm), 0.0 if same else 1.0],
+                         dtype=torch.float64, device=dev)
     if world > 1:
         mx = stats.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         tot = stats.clone()
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        elapsed, errs = float(mx[0]), int(tot[1])
+        elapsed, errs, errs_warm, same = float(mx[0]), int(tot[1]), int(tot[2]), float(tot[3]) == 0.0
+    if not same or errs:
+        log(f"CHECK FAILURE: timed output equals warm-up: {same}, QPSK errors on the timed output: {errs}")
 
     dom = "frequency-domain symbols (FFT upstream)" if freq else "time-domain IQ"
     cfg = {"workload": f"OFDM uplink LS+MRC, {dom} in HBM, {F} frames x {S} symbols "
@@ -331,7 +416,9 @@ def main():
                      "median_launch_ms": mrc_median},
         "stages_ms": {"demod_one_launch": mrc_ms} if one else {"estimate_ls": ls_ms, "combine_mrc": mrc_ms},
         "step_algorithmic_GBps": step_bytes / (elapsed / args.steps) / 1e9,
-        "check": {"qpsk_symbol_errors": errs},
+        "check": {"qpsk_symbol_errors": errs, "timed_equals_warmup": same,
+                  "qpsk_symbol_errors_warmup": errs_warm,
+                  "checked_output": "the last timed step's (zeroed before the timed loop)"},
         "cpu_baseline": None,
     }
     if world == 1 and not freq and not args.no_mode_a:

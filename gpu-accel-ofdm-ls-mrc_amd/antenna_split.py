@@ -117,6 +117,11 @@ class SplitPipeline:
         self.num = [torch.zeros(self.per * self.world, dtype=torch.complex64, device=device)
                     for _ in range(2)]
         self.mine = [torch.empty(self.per, dtype=torch.complex64, device=device) for _ in range(2)]
+        # rehearsal of N ranks on fewer GPUs over gloo (bench.py with
+        # OFDM_BENCH_BACKEND=gloo, tests): gloo's reduce-scatter takes host
+        # tensors only, so both collectives go through host copies,
+        # synchronously.  RCCL (the product backend) never takes this branch.
+        self.host_coll = (dist.get_backend(group) == "gloo" and torch.device(device).type == "cuda")
 
     def run(self, shard, X, out, stream=None):
         """shard: (F, S, R_local, C + prefix) on this rank; out: (F, S-1, K).
@@ -132,13 +137,15 @@ class SplitPipeline:
         return self._run(shard, X, out)
 
     def _run(self, shard, X, out, stream=None):
+        import torch
         import torch.distributed as dist
         F, S, K = self.F, self.S, self.K
         pending = []
 
         def finalize(c, b, wp, wn):
-            wp.wait()
-            wn.wait()
+            if wp is not None:
+                wp.wait()
+                wn.wait()
             f0 = c * self.chunk
             fc = min(self.chunk, F - f0)
             n = fc * (S - 1) * K
@@ -156,13 +163,24 @@ class SplitPipeline:
             part = shard[f0:f0 + fc]
             P = self.P[b][:fc]
             _, self.ws[b] = self.ops.ls_partial(part, X, self.prefix, ws=self.ws[b], P=P, stream=stream)
-            wp = dist.all_reduce(P, group=self.group, async_op=True)
+            if self.host_coll:
+                Ph = P.cpu()
+                dist.all_reduce(Ph, group=self.group)
+                P.copy_(Ph)
+            else:
+                wp = dist.all_reduce(P, group=self.group, async_op=True)
             n = fc * (S - 1) * K
             num = self.num[b][:n].view(fc, S - 1, K)
             self.ops.mrc_partial(part, self.ws[b], self.prefix, num=num, stream=stream)
             flat = self.num[b] if n == self.per * self.world else self._padded(b, n)
-            wn = dist.reduce_scatter_tensor(torch_real(self.mine[b]), torch_real(flat),
-                                            group=self.group, async_op=True)
+            if self.host_coll:
+                mine_h = torch_real(self.mine[b]).cpu()
+                dist.reduce_scatter_tensor(mine_h, torch_real(flat).cpu(), group=self.group)
+                torch_real(self.mine[b]).copy_(mine_h)
+                wp = wn = None
+            else:
+                wn = dist.reduce_scatter_tensor(torch_real(self.mine[b]), torch_real(flat),
+                                                group=self.group, async_op=True)
             pending.append((c, b, wp, wn))
             if len(pending) == 2:
                 finalize(*pending.pop(0))

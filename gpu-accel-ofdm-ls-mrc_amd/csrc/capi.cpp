@@ -63,27 +63,29 @@ hipError_t mrc_fused(const float2 *iq, long long F, int S, int R, int C, int pre
 // ofdm_frame_demod at C = 1024 runs LS and MRC as ONE launch (k_demod_td1024)
 // unless the stream is being captured into a graph: its per-launch flag
 // epoch would be frozen in the graph, and a replay would find every flag
-// already set.  The same kernels at C = 2048 / 4096 (k_demod_td2048 / 4096)
-// measured no faster than the two launches and are in the
-// A/B build only (OFDM_AB_DEMOD_WIDE=1).
+// already set.  The same design at C = 2048 / 4096 measured no faster than
+// the two launches (kept as scripts/experiments/ab_knobs_r3.patch).
 bool one_launch_demod(int C, hipStream_t s) {
-    if (!ofdm::ab_knob("DEMOD_FUSED", 1)) return false;
-    if (C != 1024 && !(fused_c(C) && ofdm::ab_knob("DEMOD_WIDE", 0))) return false;
+    if (C != 1024) return false;
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(s, &st) != hipSuccess) return false;
     return st == hipStreamCaptureStatusNone;
 }
 
-// Per-launch flag values of the one-launch demod: 64 bits, never 0 and never
-// repeated in this process; the high half is drawn once per process so that
-// flags left in recycled memory by another process do not match either.
+// Per-launch flag values of the one-launch demod: 64 bits, never 0, and not
+// repeated in this process before 2^64 launches (a 64-bit counter added to a
+// 64-bit offset drawn once per process, so that flags left in recycled
+// memory by another process do not match either).
 unsigned long long next_epoch() {
     static std::atomic<unsigned long long> ctr{0};
     static const unsigned long long salt = [] {
         std::random_device rd;
-        return ((unsigned long long)rd() << 32) | 0x80000000ull;
+        return ((unsigned long long)rd() << 32) ^ (unsigned long long)rd();
     }();
-    return salt + (ctr.fetch_add(1) & 0x7fffffffull) + 1;
+    for (;;) {
+        const unsigned long long e = salt + ctr.fetch_add(1);
+        if (e != 0) return e;
+    }
 }
 
 long long staging_frames(long long nframes, int S, int R, int C) {
@@ -238,14 +240,6 @@ int set_error(int code, const char *msg) {
     g_err = msg;
     return code;
 }
-#ifdef OFDM_AB_KNOBS
-// OFDM_AB_<name>, re-read on every launch so that one process can compare
-// candidates back to back (A/B build only)
-int ab_knob(const char *name, int def) {
-    const char *v = getenv((std::string("OFDM_AB_") + name).c_str());
-    return (v && *v) ? atoi(v) : def;
-}
-#endif
 }  // namespace ofdm
 
 extern "C" {
@@ -425,21 +419,26 @@ int ofdm_frame_combine(const ofdm_cf32 *d_iq, long long nframes, int S, int R, i
 int ofdm_frame_demod(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, int prefix,
                      const ofdm_cf32 *d_X, void *d_ws, size_t ws_bytes_, ofdm_cf32 *d_out,
                      ofdm_stream_t stream) {
+    return ofdm_frame_demod_ex(d_iq, nframes, S, R, C, prefix, d_X, d_ws, ws_bytes_, d_out, OFDM_FLOW_AUTO, -1,
+                               stream);
+}
+
+int ofdm_frame_demod_ex(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, int prefix,
+                        const ofdm_cf32 *d_X, void *d_ws, size_t ws_bytes_, ofdm_cf32 *d_out, int flow,
+                        long long spin_ticks, ofdm_stream_t stream) {
     int rc = check_frame_args(d_iq, nframes, S, R, C, prefix, d_out, "ofdm_frame_demod");
     if (rc) return rc;
     if (!d_X) return fail(OFDM_E_ARG, "ofdm_frame_demod: null pilots");
+    if (flow != OFDM_FLOW_AUTO && flow != OFDM_FLOW_TWO_LAUNCH)
+        return fail(OFDM_E_ARG, "ofdm_frame_demod_ex: flow=%d (OFDM_FLOW_AUTO or OFDM_FLOW_TWO_LAUNCH)", flow);
     if (nframes == 0) return OFDM_OK;
     Workspace w;
     if ((rc = carve(d_ws, ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
     hipStream_t s = hs(stream);
     ws_forget(d_ws);
-    if (one_launch_demod(C, s)) {
-        auto launch = ofdm::launch_demod_td1024;
-#ifdef OFDM_AB_KNOBS
-        if (C == 2048) launch = ofdm::launch_demod_td2048;
-        if (C == 4096) launch = ofdm::launch_demod_td4096;
-#endif
-        rc = hip_check(launch(F2(d_iq), nframes, S, R, prefix, F2(d_X), w.Hc, w.P, F2(d_out), w.flags, next_epoch(), s),
+    if (flow == OFDM_FLOW_AUTO && one_launch_demod(C, s)) {
+        rc = hip_check(ofdm::launch_demod_td1024(F2(d_iq), nframes, S, R, prefix, F2(d_X), w.Hc, w.P, F2(d_out),
+                                                 w.flags, next_epoch(), spin_ticks, s),
                        "launch_demod_td");
         if (rc == OFDM_OK) ws_record(d_ws, ws_bytes_, nframes, S, R, C, true, false);
         return rc;
@@ -450,9 +449,7 @@ int ofdm_frame_demod(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int
         if (rc) return rc;
         // the estimate is in the workspace once the LS launch is enqueued
         ws_record(d_ws, ws_bytes_, nframes, S, R, C, true, false);
-        return hip_check(mrc_fused(F2(d_iq), nframes, S, R, C, prefix, w.Hc, w.P,
-                                                 F2(d_out), 0, s),
-                         "mrc_fused");
+        return hip_check(mrc_fused(F2(d_iq), nframes, S, R, C, prefix, w.Hc, w.P, F2(d_out), 0, s), "mrc_fused");
     }
     rc = td_staged(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w, F2(d_out), 0, s);
     if (rc == OFDM_OK) ws_record(d_ws, ws_bytes_, nframes, S, R, C, false, false);

@@ -46,9 +46,7 @@ namespace td1024 {
 // ---------------------------------------------------------------------------
 constexpr int LS_WAVES = 4;
 
-// DBG (A/B build only, wrong results by design): 1 return after the twiddle
-// fill, 2 no FFT (the loaded row is used as its transform), 4 no P combine.
-template <int NW, int DBG = 0>
+template <int NW>
 __global__ void __launch_bounds__(64 * NW) k_ls_td1024(const float2 *__restrict__ iq, int S, int R,
                                                        int prefix, const float2 *__restrict__ X,
                                                        float2 *__restrict__ Hc, float *__restrict__ P,
@@ -60,7 +58,6 @@ __global__ void __launch_bounds__(64 * NW) k_ls_td1024(const float2 *__restrict_
     float2 *T = lds + TWBUF + w * TBUF;
     fill_twiddles(tw);
     __syncthreads();
-    if constexpr ((DBG & 1) != 0) return;
 
     const long long f = blockIdx.x;
     const int Cp = C + prefix;
@@ -79,12 +76,7 @@ __global__ void __launch_bounds__(64 * NW) k_ls_td1024(const float2 *__restrict_
     for (int r = w; r < R; r += NW) {
         float2 a[16], x[16];
         row_load(pilot + (long long)r * Cp, t, a);
-        if constexpr ((DBG & 2) != 0) {
-#pragma unroll
-            for (int k = 0; k < 16; ++k) x[k] = a[k];
-        } else {
-            row_fft(a, t, T, tw, x);
-        }
+        row_fft(a, t, T, tw, x);
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             float2 h = ls_conj(x[k], xp[k]);
@@ -93,13 +85,6 @@ __global__ void __launch_bounds__(64 * NW) k_ls_td1024(const float2 *__restrict_
             p[k] = p[k] + (h.x * h.x) + (h.y * h.y);
         }
         hc_store(Hf + (long long)r * (C / 2), t, x);
-    }
-    if constexpr ((DBG & 4) != 0) {
-        if (w == 0) {
-#pragma unroll
-            for (int k = 0; k < 16; ++k) P[f * C + b0 + 16 * k] = p[k];
-        }
-        return;
     }
     __syncthreads();
     float *pp = reinterpret_cast<float *>(lds + TWBUF);  // [NW][C], reuses T
@@ -135,12 +120,7 @@ __global__ void __launch_bounds__(64 * NW) k_ls_td1024(const float2 *__restrict_
 
 // One antenna row of the prefetching loop: a[] holds this row on entry and
 // the next row (`next`, when PREF) on exit.
-// DBG (A/B build only, wrong results by design): bit 0 no barriers around
-// the Hc exchange, bit 1 no Hc traffic at all, bit 2 no epilogue, bit 3 the
-// epilogue without its global stores, bit 4 no |H|^2 loads and divides, bit
-// 5 plain instead of nontemporal output stores (correct results), bit 6 no
-// IQ loads after the first row (compute and synchronisation only).
-template <bool PREF, int DBG = 0>
+template <bool PREF>
 __device__ __forceinline__ void hlds_row_pf(const float2 *next, const float4 *hrow, int t, float2 (&a)[16],
                                             float2 *T, const float2 *tw1, const float2 *tw2,
                                             const float4 *lo, const float4 *hi, float4 *mine,
@@ -149,17 +129,16 @@ __device__ __forceinline__ void hlds_row_pf(const float2 *next, const float4 *hr
     float2 x[16];
     row_fft_a(a, t, T, tw1);
     // a row is 512 float4: each of the 512 threads moves 16 B
-    const float4 hreg = (DBG & 2) ? float4{1.f, 0.f, 0.f, 1.f} : hrow[threadIdx.x];
+    const float4 hreg = hrow[threadIdx.x];
     __builtin_amdgcn_sched_barrier(0);
-    if (PREF && !(DBG & 64)) row_load<true>(next, t, a);
+    if (PREF) row_load<true>(next, t, a);
     row_fft_b(t, T, tw2, x);
-    if (!(DBG & 1)) lds_barrier();  // every wave is done with the previous Hc row
-    if (!(DBG & 2)) *mine = hreg;
-    if (!(DBG & 1)) lds_barrier();
+    lds_barrier();  // every wave is done with the previous Hc row
+    *mine = hreg;
+    lds_barrier();
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        const float4 v = (DBG & 2) ? float4{hreg.x, (float)i, hreg.z, hreg.w}
-                                   : i < 4 ? lo[i * 64] : hi[(i - 4) * TS];  // 2 images = TS float4s
+        const float4 v = i < 4 ? lo[i * 64] : hi[(i - 4) * TS];  // 2 images = TS float4s
         // matrixMultThenSum (cpuLS.hpp:203-204), antennas in order
         acc[2 * i].x = acc[2 * i].x + (x[2 * i].x * v.x - x[2 * i].y * v.y);
         acc[2 * i].y = acc[2 * i].y + (x[2 * i].x * v.y + x[2 * i].y * v.x);
@@ -197,7 +176,7 @@ __device__ __forceinline__ void row0_dma(const float2 *sym, int t, float2 *T) {
     for (int j = 0; j < 8; ++j) dma16(src + j * 1024, dst + j * 1024);
 }
 
-template <bool SHARED, int DBG = 0, bool R0 = false>
+template <bool SHARED, bool R0 = false>
 __device__ __forceinline__ void hlds_rows(const float2 *sym, int Cp, int R, const float4 *Hf, int t,
                                           float2 *T, const float2 *tw1, const float2 *tw2,
                                           float2 *T0, float4 *hfree, float2 (&acc)[16]) {
@@ -213,9 +192,9 @@ __device__ __forceinline__ void hlds_rows(const float2 *sym, int Cp, int R, cons
         // the last row is peeled so that the prefetch is unconditional: the
         // wait for the Hc word before the exchange is then vmcnt(16), not 0
         for (int r = 0; r + 1 < R; ++r)
-            hlds_row_pf<true, DBG>(sym + (long long)(r + 1) * Cp, Hf + (long long)r * (C / 2), t, a, T, tw1,
+            hlds_row_pf<true>(sym + (long long)(r + 1) * Cp, Hf + (long long)r * (C / 2), t, a, T, tw1,
                                    tw2, lo, hi, mine, acc);
-        hlds_row_pf<false, DBG>(sym, Hf + (long long)(R - 1) * (C / 2), t, a, T, tw1, tw2, lo, hi, mine, acc);
+        hlds_row_pf<false>(sym, Hf + (long long)(R - 1) * (C / 2), t, a, T, tw1, tw2, lo, hi, mine, acc);
     } else {
         for (int r = 0; r < R; ++r) {
             float2 a[16], x[16], h[16];
@@ -241,16 +220,8 @@ __device__ __forceinline__ void hlds_rows(const float2 *sym, int Cp, int R, cons
 // still hold other waves' Hc words, so index it as [16][TP]) at their final
 // positions, then store them as 16 contiguous 512-B nontemporal wave stores
 // instead of 4 scattered 128-B runs per instruction.
-template <int DBG = 0>
 __device__ __forceinline__ void hlds_epilogue(const float2 (&acc)[16], const float *P, long long f, long long q,
                                               int t, float2 *T, float2 *__restrict__ out, int mode) {
-    if (DBG & 4) {  // diagnostic: no output stores (keep the sums live)
-        float sacc = 0.f;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) sacc += acc[k].x * acc[k].y;
-        if (sacc == 1234.5f) out[q] = float2{sacc, 0.f};
-        return;
-    }
     const int b0 = lane_bin0(t);
     float2 *o = out + q * K;
     const float *Pf = P + f * C + b0;
@@ -258,7 +229,7 @@ __device__ __forceinline__ void hlds_epilogue(const float2 (&acc)[16], const flo
     // condition the compiler issued them one at a time, each behind a
     // vmcnt(0) wait; neutral at 4 waves/SIMD)
     float pv[16];
-    if ((mode & 1) == 0 && !(DBG & 16)) {
+    if ((mode & 1) == 0) {
 #pragma unroll
         for (int k = 0; k < 16; ++k) pv[k] = Pf[16 * k];
     }
@@ -268,7 +239,7 @@ __device__ __forceinline__ void hlds_epilogue(const float2 (&acc)[16], const flo
         float2 v = acc[k];
         int j = b - 1;
         if ((mode & 1) == 0) {
-            if (!(DBG & 16)) v = float2{acc[k].x / pv[k], acc[k].y / pv[k]};
+            v = float2{acc[k].x / pv[k], acc[k].y / pv[k]};
             j = out_pos(b > 0 ? b - 1 : 0, K);
         }
         if (b > 0) T[(j >> 6) * hlds::TP + (j & 63)] = v;
@@ -279,14 +250,9 @@ __device__ __forceinline__ void hlds_epilogue(const float2 (&acc)[16], const flo
         const int j = t + 64 * m;
         if (j < K) {
             const float2 v = T[m * hlds::TP + t];
-            if (DBG & 8) {  // diagnostic: the epilogue without its global stores
-                if (v.x == 1234.5f) o[j] = v;
-            } else if (DBG & 32) {  // A/B: plain stores
-                o[j] = v;
-            } else {  // nontemporal (streaming) stores: 2-3 % faster than plain ones
-                __builtin_nontemporal_store(__builtin_bit_cast(unsigned long long, v),
-                                            reinterpret_cast<unsigned long long *>(o + j));
-            }
+            // nontemporal (streaming) stores: 2-3 % faster than plain ones
+            __builtin_nontemporal_store(__builtin_bit_cast(unsigned long long, v),
+                                        reinterpret_cast<unsigned long long *>(o + j));
         }
     }
 }
@@ -295,7 +261,7 @@ __device__ __forceinline__ void hlds_epilogue(const float2 (&acc)[16], const flo
 // (blocks b and b+8 share an XCD under round-robin dispatch, so a frame's
 // workgroups share its Hc rows in one L2; speed only, never correctness).
 // mode 0: out[q][out_pos(j)] = acc / P;  mode 1: out[q][j] = acc (numerator).
-template <int DBG = 0, bool R0 = false>
+template <bool R0>
 __global__ void __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 4)))
 k_mrc_td1024_hlds(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
                   const float *__restrict__ P, float2 *__restrict__ out, long long nq, long long nblocks,
@@ -332,13 +298,13 @@ k_mrc_td1024_hlds(const float2 *__restrict__ iq, int S, int R, int prefix, const
 
     float2 acc[16];
     if (f0 == fl)
-        hlds_rows<true, DBG, R0>(sym, Cp, R, reinterpret_cast<const float4 *>(Hc + f0 * (long long)R * C), t, T,
+        hlds_rows<true, R0>(sym, Cp, R, reinterpret_cast<const float4 *>(Hc + f0 * (long long)R * C), t, T,
                                  tw1, tw2, T0, hfree, acc);
     else
-        hlds_rows<false, 0, R0>(sym, Cp, R, reinterpret_cast<const float4 *>(Hc + f * (long long)R * C), t, T,
+        hlds_rows<false, R0>(sym, Cp, R, reinterpret_cast<const float4 *>(Hc + f * (long long)R * C), t, T,
                                 tw1, tw2, T0, hfree, acc);
     if (!store) return;
-    hlds_epilogue<DBG>(acc, P, f, q, t, T, out, mode);
+    hlds_epilogue(acc, P, f, q, t, T, out, mode);
 }
 
 
@@ -420,7 +386,6 @@ __device__ __forceinline__ void hlds_ls_frame(const float2 *__restrict__ iq, int
 // same XCD left dirty (wave_fft1024.hpp: publish_flag / consume_flags;
 // same-process A/B vs plain stores + release fence: equal to 1 % faster,
 // DESIGN.md 4.6).
-template <int DBG = 0, bool R0 = false>
 __global__ void __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 4)))
 k_demod_td1024(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ X, float2 *Hc,
                float *P, float2 *__restrict__ out, long long nq, long long nblocks, long long per_xcd,
@@ -435,59 +400,64 @@ k_demod_td1024(const float2 *__restrict__ iq, int S, int R, int prefix, const fl
     float2 *T0 = lds + TW1S + TW2S;
     float4 *hfree = reinterpret_cast<float4 *>(T0 + HW * TS);
 
-    if ((int)blockIdx.x < nls) {  // estimator workgroup
-        const long long f = blockIdx.x;
-        if (f >= nframes) return;
+    // Frames this workgroup estimates itself, [e0, e1]: an estimator
+    // workgroup its own frame; an MRC workgroup none, or -- when a flag it
+    // waits for is not published within spin_ticks -- the frames it reads.
+    // ONE call site of hlds_ls_frame for both, so that both run the same
+    // inlined code and write the same bytes (two inlined copies
+    // could contract differently).
+    const bool estimator = (int)blockIdx.x < nls;
+    // MRC block map (XCD-grouped logical block; a pure function of blockIdx,
+    // recomputed after the LS loop rather than held across it)
+    auto mrc_block = [&]() { const long long pb = blockIdx.x - nls; return (pb & 7) * per_xcd + (pb >> 3); };
+    auto first_frame = [&](long long lb) { return (lb * HW) / (S - 1); };
+    auto last_frame = [&](long long lb) { return ((lb * HW + HW - 1 < nq ? lb * HW + HW - 1 : nq - 1)) / (S - 1); };
+    long long e0 = 1, e1 = 0;
+    if (estimator) {
+        e0 = e1 = blockIdx.x;
+        if (e0 >= nframes) return;
         fill(tw1, tw2);
         __syncthreads();
-        hlds_ls_frame(iq, S, R, prefix, X, Hc, P, f, w, t, T, T0, tw1, tw2);
-        publish_flag(flags + f, epoch);
+    } else {
+        const long long lb = mrc_block();
+        if (lb >= nblocks) return;
+        fill(tw1, tw2);
+        // wait for the estimates of frames f0 .. fl (hfree, not used before
+        // the rows, carries the outcome); not published in time: estimate
+        // here (identical bytes) and read them back behind an acquire of our own
+        const long long f0 = first_frame(lb), fl = last_frame(lb);
+        if (!consume_flags(flags, f0, fl, epoch, spin_ticks, reinterpret_cast<int *>(hfree))) {
+            __syncthreads();
+            e0 = f0;
+            e1 = fl;
+        }
+    }
+    for (long long ff = e0; ff <= e1; ++ff) hlds_ls_frame(iq, S, R, prefix, X, Hc, P, ff, w, t, T, T0, tw1, tw2);
+    if (estimator) {
+        publish_flag(flags + e0, epoch);
         return;
     }
-    const long long pb = blockIdx.x - nls;
-    const long long lb = (pb & 7) * per_xcd + (pb >> 3);  // XCD-grouped logical block
-    if (lb >= nblocks) return;
+    if (e0 <= e1) acquire_all();
 
+    const long long lb = mrc_block();
     const int nsym = S - 1;
     const long long qw = lb * HW + w;
     const bool store = qw < nq;
     const long long q = store ? qw : nq - 1;
     const long long f = q / nsym;
-    const long long f0 = (lb * HW) / nsym;
-    const long long fl = ((lb * HW + HW - 1 < nq ? lb * HW + HW - 1 : nq - 1)) / nsym;
+    const long long f0 = first_frame(lb), fl = last_frame(lb);
     const int s = 1 + (int)(q % nsym);
     const int Cp = C + prefix;
     const float2 *sym = iq + (f * S + s) * (long long)R * Cp + prefix;
-    if constexpr (R0) row0_dma(sym, t, T);  // in flight through the wait
-    fill(tw1, tw2);
-
-    // wait for the estimates of frames f0 .. fl (hfree, not used before the
-    // rows, carries the outcome); not published in time: estimate here
-    // (identical bytes) and read them back behind an acquire of our own
-    if (!consume_flags(flags, f0, fl, epoch, spin_ticks, reinterpret_cast<int *>(hfree))) {
-        if constexpr (R0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA lands before the images are reused
-        __syncthreads();
-        for (long long ff = f0; ff <= fl; ++ff) hlds_ls_frame(iq, S, R, prefix, X, Hc, P, ff, w, t, T, T0, tw1, tw2);
-        acquire_all();
-        if constexpr (R0) {  // the estimate used the images: again
-            // the symbol pointer laundered so that the compiler recomputes
-            // the 8 DMA addresses here instead of keeping (spilling) the
-            // first DMA's across the wait
-            const float2 *sym2 = sym;
-            asm volatile("" : "+s"(sym2));
-            row0_dma(sym2, t, T);
-        }
-    }
-
     float2 acc[16];
     if (f0 == fl)
-        hlds_rows<true, DBG, R0>(sym, Cp, R, reinterpret_cast<const float4 *>(Hc + f0 * (long long)R * C), t, T,
-                                 tw1, tw2, T0, hfree, acc);
+        hlds_rows<true, false>(sym, Cp, R, reinterpret_cast<const float4 *>(Hc + f0 * (long long)R * C), t, T,
+                               tw1, tw2, T0, hfree, acc);
     else
-        hlds_rows<false, 0, R0>(sym, Cp, R, reinterpret_cast<const float4 *>(Hc + f * (long long)R * C), t, T,
+        hlds_rows<false, false>(sym, Cp, R, reinterpret_cast<const float4 *>(Hc + f * (long long)R * C), t, T,
                                 tw1, tw2, T0, hfree, acc);
     if (!store) return;
-    hlds_epilogue<DBG>(acc, P, f, q, t, T, out, 0);
+    hlds_epilogue(acc, P, f, q, t, T, out, 0);
 }
 
 }  // namespace td1024
@@ -503,17 +473,6 @@ hipError_t launch_ls_td1024(const float2 *iq, long long nframes, int S, int R, i
     auto k16 = k_ls_td1024<16>;
     auto k4 = k_ls_td1024<LS_WAVES>;
     auto k8 = k16;  // 8-wave workgroups: A/B build only
-#ifdef OFDM_AB_KNOBS
-    k8 = k_ls_td1024<8>;
-    nw = ab_knob("LS1K_NW", nw);
-    switch (ab_knob("LS1K_DBG", 0)) {
-        case 1: k16 = k_ls_td1024<16, 1>; k8 = k_ls_td1024<8, 1>; k4 = k_ls_td1024<4, 1>; break;
-        case 2: k16 = k_ls_td1024<16, 2>; k8 = k_ls_td1024<8, 2>; k4 = k_ls_td1024<4, 2>; break;
-        case 4: k16 = k_ls_td1024<16, 4>; k8 = k_ls_td1024<8, 4>; k4 = k_ls_td1024<4, 4>; break;
-        case 6: k16 = k_ls_td1024<16, 6>; k8 = k_ls_td1024<8, 6>; k4 = k_ls_td1024<4, 6>; break;
-        default: break;
-    }
-#endif
     if (nw == 16 || nw == 8) {
         auto kern = nw == 16 ? k16 : k8;
         const size_t lds = (TWBUF + nw * TBUF) * sizeof(float2);
@@ -541,31 +500,19 @@ hipError_t launch_mrc_td1024(const float2 *iq, long long nframes, int S, int R, 
     // fill (same process, bit-identical: R=16 x 100 frames 0.301 -> 0.293 ms,
     // R=64 x 400 3.961 -> 3.922; profiles/r3/r3p_row0_dma_ab.jsonl).  The
     // one-launch kernel loses with it (+3-5 %) and keeps the register load.
-    auto kern = k_mrc_td1024_hlds<0, true>;
-#ifdef OFDM_AB_KNOBS
-    if (!ab_knob("MRC1K_R0", 1)) kern = k_mrc_td1024_hlds<0, false>;  // row 0 by register load (round 2)
-    switch (ab_knob("MRC1K_DBG", 0)) {
-        case 1: kern = k_mrc_td1024_hlds<1>; break;
-        case 2: kern = k_mrc_td1024_hlds<2>; break;
-        case 4: kern = k_mrc_td1024_hlds<4>; break;
-        case 6: kern = k_mrc_td1024_hlds<6>; break;
-        case 8: kern = k_mrc_td1024_hlds<8>; break;
-        case 16: kern = k_mrc_td1024_hlds<16>; break;
-        case 32: kern = k_mrc_td1024_hlds<32>; break;
-        case 64: kern = k_mrc_td1024_hlds<64>; break;
-        default: break;
-    }
-#endif
+    auto kern = k_mrc_td1024_hlds<true>;
     hipLaunchKernelGGL(kern, dim3((unsigned)(pxcd * 8)), dim3(64 * hlds::WAVES), hlds::LDS_BYTES, s, iq, S, R,
                        prefix, Hc, P, out, nq, nb, pxcd, mode);
     return hipGetLastError();
 }
 
 // One-launch LS + MRC (ofdm_frame_demod, mode 0).  flags: nframes 64-bit
-// words of the workspace; epoch: a value none of them holds (per launch).
+// words of the workspace; epoch: a value none of them holds (per launch);
+// spin_ticks: how long (100 MHz ticks) an MRC workgroup waits for a frame's
+// flag before it estimates the frame itself (< 0: SPIN_TICKS).
 hipError_t launch_demod_td1024(const float2 *iq, long long nframes, int S, int R, int prefix, const float2 *X,
                                float2 *Hc, float *P, float2 *out, unsigned long long *flags,
-                               unsigned long long epoch, hipStream_t s) {
+                               unsigned long long epoch, long long spin_ticks, hipStream_t s) {
     using namespace td1024;
     const long long nq = nframes * (S - 1);
     if (nq <= 0) return hipSuccess;
@@ -573,13 +520,9 @@ hipError_t launch_demod_td1024(const float2 *iq, long long nframes, int S, int R
     const long long pxcd = (nb + 7) / 8;
     const long long nls = (nframes + 7) / 8 * 8;
     if (pxcd * 8 + nls > 0x7fffffffll) return hipErrorInvalidValue;
-    auto kern = k_demod_td1024<0, false>;
-#ifdef OFDM_AB_KNOBS
-    if (ab_knob("MRC1K_R0", 0)) kern = k_demod_td1024<0, true>;  // row 0 by LDS-DMA
-#endif
-    hipLaunchKernelGGL(kern, dim3((unsigned)(nls + pxcd * 8)), dim3(64 * hlds::WAVES), hlds::LDS_BYTES, s, iq, S,
-                       R, prefix, X, Hc, P, out, nq, nb, pxcd, flags, epoch, (int)nls, nframes,
-                       (long long)ab_knob("DEMOD_SPIN", (int)SPIN_TICKS));
+    hipLaunchKernelGGL(k_demod_td1024, dim3((unsigned)(nls + pxcd * 8)), dim3(64 * hlds::WAVES), hlds::LDS_BYTES,
+                       s, iq, S, R, prefix, X, Hc, P, out, nq, nb, pxcd, flags, epoch, (int)nls, nframes,
+                       spin_ticks < 0 ? SPIN_TICKS : spin_ticks);
     return hipGetLastError();
 }
 

@@ -102,7 +102,7 @@ __device__ __forceinline__ void row_fft4096(const float2 *__restrict__ src, int 
 constexpr int LS_WAVES = 8;
 constexpr size_t ls_lds(int nw) { return lds_bytes(nw) + (size_t)C * sizeof(float2); }
 
-template <int E, int LS_PAIRS, bool WT = false>
+template <int E, int LS_PAIRS>
 __device__ __forceinline__ void ls_rows(const float2 *pilot, int Cp, int R, int j, int t, float2 *T,
                                         const float2 *lds, const float2 *xs, float2 *Hf, float *pp) {
     const int b0 = lane_bin0(t);
@@ -122,13 +122,8 @@ __device__ __forceinline__ void ls_rows(const float2 *pilot, int Cp, int R, int 
             const float2 ho = ls_conj(xo[k], xs[be + 2]);
             pe[k] = pe[k] + (he.x * he.x) + (he.y * he.y);  // findDistSqrd order
             po[k] = po[k] + (ho.x * ho.x) + (ho.y * ho.y);
-            if constexpr (WT) {  // write-through (sc1) for the one-launch hand-off
-                td1024::store8_wt(hr + k * 64 + t, he);
-                td1024::store8_wt(hr + 1024 + k * 64 + t, ho);
-            } else {
-                hr[k * 64 + t] = he;
-                hr[1024 + k * 64 + t] = ho;
-            }
+            hr[k * 64 + t] = he;
+            hr[1024 + k * 64 + t] = ho;
         }
     }
     __syncthreads();  // every wave is done with its transpose image (pp reuses it)
@@ -141,8 +136,7 @@ __device__ __forceinline__ void ls_rows(const float2 *pilot, int Cp, int R, int 
 }
 
 // LS of frame f by an NW-wave workgroup (LS LDS layout, ls_lds(NW) bytes).
-// WT: Hc and P stored write-through (the one-launch kernel).
-template <int NW = LS_WAVES, bool WT = false>
+template <int NW = LS_WAVES>
 __device__ __forceinline__ void ls_frame4096(const float2 *__restrict__ iq, int S, int R, int prefix,
                                              const float2 *__restrict__ X, float2 *Hc, float *P, long long f,
                                              float2 *lds, int partial) {
@@ -159,19 +153,16 @@ __device__ __forceinline__ void ls_frame4096(const float2 *__restrict__ iq, int 
     float2 *Hf = Hc + f * (long long)R * C;
     float *pp = reinterpret_cast<float *>(lds + TAB);  // [LS_PAIRS][C], reuses T
     if (w & 1)
-        ls_rows<1, LS_PAIRS, WT>(pilot, Cp, R, w >> 1, t, T, lds, xs, Hf, pp);
+        ls_rows<1, LS_PAIRS>(pilot, Cp, R, w >> 1, t, T, lds, xs, Hf, pp);
     else
-        ls_rows<0, LS_PAIRS, WT>(pilot, Cp, R, w >> 1, t, T, lds, xs, Hf, pp);
+        ls_rows<0, LS_PAIRS>(pilot, Cp, R, w >> 1, t, T, lds, xs, Hf, pp);
     __syncthreads();
     float *Pf = P + f * C;
     for (int b = threadIdx.x; b < C; b += blockDim.x) {
         float sum = pp[b];
         for (int i = 1; i < LS_PAIRS; ++i) sum = sum + pp[i * C + b];  // antennas in order
         const float v = b == 0 ? (partial ? 0.f : 1.f) : sum;
-        if constexpr (WT)
-            td1024::store4_wt(Pf + b, v);
-        else
-            Pf[b] = v;
+        Pf[b] = v;
     }
     __syncthreads();  // pp (the transpose images) read before they are reused
 }
@@ -189,8 +180,8 @@ __global__ void __launch_bounds__(64 * NW) k_ls_td4096(const float2 *__restrict_
 // MRC, one read per row: a wave PAIR per data symbol (see the header: radix-4
 // DIF, wave e loads quarters e and e + 2, the pair swaps one half through
 // LDS).  The DIF twiddles W4096^(c n0), n0 = t + 64 m, are the lane's
-// W4096^(c t) times the compile-time W64^(c m).  PK: packed-f32 arithmetic
-// (pk.hpp) in the split and both FFT halves.
+// W4096^(c t) times the compile-time W64^(c m).  Packed-f32 arithmetic
+// (pk.hpp) in the split, both FFT halves and the MAC.
 // ---------------------------------------------------------------------------
 constexpr int X_TAB = hl::TW1S + hl::TW2S;
 
@@ -215,41 +206,22 @@ __device__ __forceinline__ void dma_hc_row(const float2 *g, unsigned lds) {
 }
 
 // One antenna row for wave E of the pair.  On entry a/b hold the row's
-// quarters E and E + 2; with PREF the next row's quarters are loaded into
-// them after the first FFT and stay in flight through the second FFT and
-// MAC.  hr points at this row's Hc in LDS, DMA'd during the previous row;
-// this row's first barrier publishes it (after vmcnt(0)) and the DMA of row
-// r+1 (hnext, into LDS byte address hb_next) is issued right after that
-// barrier, into the buffer every wave finished with in row r-1.
-// DBG (A/B build only, wrong results by design): bit 0 no workgroup barriers
-// (racy exchange and Hc), bit 1 no Hc DMA (Hc read from stale LDS), bit 2 no
-// output stores, bit 3 no second (exchange-read) barrier, bit 4 no first
-// (exchange-write / Hc-publish) barrier, bit 5 the round-1 epilogue
-// (scattered plain stores; correct results), bit 6 no IQ loads after the
-// first row (compute and synchronisation only), bit 7 the row loads alone
-// (no FFT, MAC or Hc; with bit 0 not even the per-row barrier).
-// TW: twiddles by recurrence from one per-lane base (hlds::tw_powers) in the
-// first (bit 0) / second (bit 1) half of each 1024-point FFT instead of 15
-// table reads each: 3-3.5 % faster here (2 waves/SIMD, where the table reads
-// issue one LDS round trip at a time), slower in the C = 1024 / 2048 kernels.
-// HP (pairs per workgroup) = 4: Hc double buffer, the DMA of row r + 1 issued
-// after this row's first barrier.  HP = 2 (A/B candidate): ONE Hc buffer,
-// refilled after a third barrier once every wave has read both planes of this
-// row (before its second FFT) and published at the next row's second barrier.
-// SW (IL rows only): the pair's two images swap roles every row -- the
-// exchange half goes into the image this wave transposed in the previous
-// row, the partner's half is read from the other, and this wave's FFT
-// transposes then reuse the image it just read (its own reads precede its
-// writes in LDS order; the partner no longer touches it), so the second
-// workgroup barrier of the row (partner done reading before the FFT
-// overwrites) is not needed.  T = the image written, Tp = the image read.
-template <int E, int PK, bool PREF, int DBG = 0, int TW = 3, int HP = 4, int HE = 0, int IL = 0, bool SW = false>
+// quarters E and E + 2; with PREF the first quarter of the next row is
+// loaded into a at the row start (in flight through both transforms) and
+// the second into b after the first MAC.  hr points at this row's Hc in LDS,
+// DMA'd during the previous row; this row's first barrier publishes it
+// (after vmcnt(0)) and the DMA of row r+1 (hnext, into LDS byte address
+// hb_next) is issued right after that barrier, into the buffer every wave
+// finished with in row r-1.  The second barrier: the partner has read the
+// exchanged half from T before this wave's FFT transposes reuse it.
+// Twiddles by recurrence from one per-lane base (hlds::tw_powers; 3-3.5 %
+// faster here than 15 table reads per stage).
+template <int E, bool PREF>
 __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const float2 *__restrict__ hr,
                                       int t, float2 *T, const float2 *Tp, const float2 *tw1,
                                       const float2 *tw2, pk::v2f wb0, pk::v2f wb1, float2 (&a)[16],
                                       float2 (&b)[16], float2 (&ae)[16], float2 (&ao)[16],
-                                      const float2 *hnext, unsigned hb_next, const hl::TwAnchors &ca = {},
-                                      const hl::TwAnchors &cb = {}) {
+                                      const float2 *hnext, unsigned hb_next) {
     using namespace pk;
     v2f u[16], v[16];
 #pragma unroll
@@ -257,20 +229,19 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
         u[m] = add(V(a[m]), V(b[m]));  // s
         v[m] = sub(V(a[m]), V(b[m]));  // d
     }
-    float2 h[16], h1[16];
+    float2 h[16];
     // wave 0 sends d and keeps s (= a); wave 1 sends s (= c) and keeps d
 #pragma unroll
     for (int m = 0; m < 16; ++m) T[hl::swz(m, t)] = F(E ? u[m] : v[m]);
-    if (HP == 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this row's Hc DMA landed
-    if (!(DBG & 1) && !(DBG & 16)) td1024::lds_barrier();
-    if (HP == 4 && !(DBG & 2) && hnext) dma_hc_row(hnext, hb_next);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this row's Hc DMA landed
+    td1024::lds_barrier();
+    if (hnext) dma_hc_row(hnext, hb_next);
 #pragma unroll
     for (int m = 0; m < 16; ++m) {
         if (E) u[m] = V(Tp[hl::swz(m, t)]);  // b
         else v[m] = V(Tp[hl::swz(m, t)]);    // c
     }
-    if (HP != 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this row's Hc DMA landed
-    if (!SW && !(DBG & 1) && !(DBG & 8)) td1024::lds_barrier();  // the partner has read T before the FFT reuses it
+    td1024::lds_barrier();  // the partner has read T before the FFT reuses it
     // E = 0: u = a, v = c:  z0 = a + c, z2 = (a - c) W^(2 n0)
     // E = 1: u = b, v = d:  z1 = (b + (-i) d) W^(n0), z3 = (b - (-i) d) W^(3 n0)
 #pragma unroll
@@ -297,123 +268,50 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
     OFDM_TWM(7) OFDM_TWM(8) OFDM_TWM(9) OFDM_TWM(10) OFDM_TWM(11) OFDM_TWM(12) OFDM_TWM(13)
     OFDM_TWM(14) OFDM_TWM(15)
 #undef OFDM_TWM
-    float2 z[16], x[16];
-    if constexpr (IL != 0) {
-        static_assert(PK == 7 && TW == 3 && HP == 4, "the interleaved row uses the packed, recurrence-twiddle FFT");
-        float2 *TF = SW ? const_cast<float2 *>(Tp) : T;  // the FFT's transpose image
-        // Both FFT1024s of the row software-pipelined through the one
-        // transpose image: A(u) -> write(u) -> read(u) issued -> A(v) computed
-        // while u's transpose is in flight -> write(v), read(v) issued (LDS
-        // ops of a wave complete in order, so v's writes follow u's reads) ->
-        // B(u) and MAC(u) while v's transpose is in flight -> next row's
-        // loads -> B(v), MAC(v).
-        v2f xu[16];
-        if constexpr (IL >= 3) {  // first quarter of the next row in flight through both transforms
-            if (PREF && !(DBG & 64)) row_load<true>(next + 1024 * E, t, a);
-        }
-        // twiddle anchors read just in time, not held across the row
-        // (hlds::tw_anchored; as row invariants they cost 37 spilled VGPRs):
-        // stage A's with the LDS queue empty, stage B's behind v's transpose
-        // reads, consumed after B's radix-16
-        (void)ca;
-        (void)cb;
-        const hl::TwAnchors a_tw = hl::anchors_a(tw1, t);
-        hl::fa_compute(u, a_tw);
-        hl::fa_write(u, t, TF);
-        hl::fb_read(t, TF, xu);
-        hl::fa_compute(v, a_tw);
-        hl::fa_write(v, t, TF);
-        hl::fb_read(t, TF, u);  // u's registers are free: v's transpose lands in them
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int k = 0; k < 16; ++k) h[k] = hr[k * 64 + t];  // plane 0, lands during B(u)
-        hl::TwAnchors b_tw = hl::anchors_b(tw2, t);
-        __builtin_amdgcn_sched_barrier(0);
-        hl::fb_compute(xu, b_tw, t, x);
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {  // matrixMultThenSum (cpuLS.hpp:191-206), packed as the default path
-            v2f a0 = V(ae[k]);
-            pk::mac(a0, V(x[k]), V(h[k]));
-            ae[k] = F(a0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int k = 0; k < 16; ++k) h[k] = hr[1024 + k * 64 + t];  // plane 1, lands during B(v)
-        __builtin_amdgcn_sched_barrier(0);
-        if (PREF && !(DBG & 64)) {
-            if (IL == 1) row_load<true>(next + 1024 * E, t, a);
-            row_load<true>(next + 1024 * (E + 2), t, b);
-        }
-        b_tw = hl::anchors_b(tw2, t);
-        hl::fb_compute(u, b_tw, t, x);
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            v2f a0 = V(ao[k]);
-            pk::mac(a0, V(x[k]), V(h[k]));
-            ao[k] = F(a0);
-        }
-        (void)h1;
-        return;
-    }
-    // matrixMultThenSum (cpuLS.hpp:203-204), antennas in order, per bin set
-    auto mac = [&](float2 (&acc)[16]) {
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            if (PK & 4) {
-                v2f a0 = V(acc[k]);
-                pk::mac(a0, V(x[k]), V(h[k]));
-                acc[k] = F(a0);
-            } else {
-                acc[k].x = acc[k].x + (x[k].x * h[k].x - x[k].y * h[k].y);
-                acc[k].y = acc[k].y + (x[k].x * h[k].y + x[k].y * h[k].x);
-            }
-        }
-    };
-#pragma unroll
-    for (int m = 0; m < 16; ++m) z[m] = F(u[m]);
-    hl::row_fft_a<PK, (TW & 1) != 0>(z, t, T, tw1);
-    if constexpr (HE == 1) {
-        // plane 0 of this row's Hc issued before the second FFT stage (all 8
-        // LDS reads in flight behind the transpose reads, landed by the MAC)
-#pragma unroll
-        for (int k = 0; k < 16; ++k) h[k] = hr[k * 64 + t];
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    hl::row_fft_b<PK, (TW & 2) != 0>(t, T, tw2, x);
+    float2 x[16];
+    // Both FFT1024s of the row software-pipelined through the one transpose
+    // image: A(u) -> write(u) -> read(u) issued -> A(v) computed while u's
+    // transpose is in flight -> write(v), read(v) issued (LDS ops of a wave
+    // complete in order, so v's writes follow u's reads) -> B(u) and MAC(u)
+    // while v's transpose is in flight -> next row's loads -> B(v), MAC(v).
+    v2f xu[16];
+    if (PREF) row_load<true>(next + 1024 * E, t, a);  // in flight through both transforms
+    // twiddle anchors read just in time, not held across the row
+    // (hlds::tw_anchored; as row invariants they cost 37 spilled VGPRs):
+    // stage A's with the LDS queue empty, stage B's behind v's transpose
+    // reads, consumed after B's radix-16
+    const hl::TwAnchors a_tw = hl::anchors_a(tw1, t);
+    hl::fa_compute(u, a_tw);
+    hl::fa_write(u, t, T);
+    hl::fb_read(t, T, xu);
+    hl::fa_compute(v, a_tw);
+    hl::fa_write(v, t, T);
+    hl::fb_read(t, T, u);  // u's registers are free: v's transpose lands in them
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (HE == 0) {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) h[k] = hr[k * 64 + t];  // plane 0: bins 4 b + E, from LDS
-#pragma unroll
-        for (int k = 0; k < 16; ++k) h1[k] = hr[1024 + k * 64 + t];  // plane 1: bins 4 b + 2 + E
-    } else if constexpr (HE == 2) {
-        // plane 0 issued as one burst (no reuse of a read register), then the MAC
-#pragma unroll
-        for (int k = 0; k < 16; ++k) h[k] = hr[k * 64 + t];
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    mac(ae);
+    for (int k = 0; k < 16; ++k) h[k] = hr[k * 64 + t];  // plane 0, lands during B(u)
+    hl::TwAnchors b_tw = hl::anchors_b(tw2, t);
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (HE != 0) {  // plane 1 read after the first MAC, consumed after the second FFT
+    hl::fb_compute(xu, b_tw, t, x);
 #pragma unroll
-        for (int k = 0; k < 16; ++k) h1[k] = hr[1024 + k * 64 + t];
+    for (int k = 0; k < 16; ++k) {  // matrixMultThenSum (cpuLS.hpp:191-206), packed
+        v2f a0 = V(ae[k]);
+        pk::mac(a0, V(x[k]), V(h[k]));
+        ae[k] = F(a0);
     }
-    if (HP != 4 && PREF) {  // every wave holds both planes of this row: refill the single buffer
-        td1024::lds_barrier();
-        if (!(DBG & 2) && hnext) dma_hc_row<2 * HP>(hnext, hb_next);
-    }
-    // next row in flight during the second FFT and the next row's exchange
-    if (PREF && !(DBG & 64)) {
-        row_load<true>(next + 1024 * E, t, a);
-        row_load<true>(next + 1024 * (E + 2), t, b);
-    }
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int k = 0; k < 16; ++k) h[k] = h1[k];
+    for (int k = 0; k < 16; ++k) h[k] = hr[1024 + k * 64 + t];  // plane 1, lands during B(v)
+    __builtin_amdgcn_sched_barrier(0);
+    if (PREF) row_load<true>(next + 1024 * (E + 2), t, b);
+    b_tw = hl::anchors_b(tw2, t);
+    hl::fb_compute(u, b_tw, t, x);
 #pragma unroll
-    for (int m = 0; m < 16; ++m) z[m] = F(v[m]);
-    hl::row_fft_a<PK, (TW & 1) != 0>(z, t, T, tw1);
-    hl::row_fft_b<PK, (TW & 2) != 0>(t, T, tw2, x);
-    mac(ao);
+    for (int k = 0; k < 16; ++k) {
+        v2f a0 = V(ao[k]);
+        pk::mac(a0, V(x[k]), V(h[k]));
+        ao[k] = F(a0);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -429,57 +327,26 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
 // workgroup (8 waves, 2 per SIMD as the 242-VGPR x kernel) per CU.
 // ---------------------------------------------------------------------------
 constexpr int H_PAIRS = 4;
-constexpr size_t h_lds(int hp) { return (size_t)(X_TAB + 2 * hp * hl::TS + (hp == 4 ? 2 : 1) * C) * sizeof(float2); }
-constexpr size_t H_LDS = h_lds(H_PAIRS);
+constexpr size_t H_LDS = (size_t)(X_TAB + 2 * H_PAIRS * hl::TS + 2 * C) * sizeof(float2);
 static_assert(H_LDS <= 160 * 1024, "one workgroup per CU");
-static_assert(2 * h_lds(2) <= 160 * 1024, "two 2-pair workgroups per CU");
 
-template <int E, int PK, int DBG = 0, int TW = 3, int HP = 4, int HE = 0, int IL = 0, bool SW = false>
+template <int E>
 __device__ __forceinline__ void h_rows(const float2 *sym, int Cp, int R, const float2 *Hg, float2 *HB, int t,
                                        float2 *T, const float2 *Tp, const float2 *tw1, const float2 *tw2,
                                        pk::v2f wb0, pk::v2f wb1, float2 (&ae)[16], float2 (&ao)[16]) {
     float2 a[16], b[16];
     row_load<true>(sym + 1024 * E, t, a);
     row_load<true>(sym + 1024 * (E + 2), t, b);
-    if constexpr ((DBG & 128) != 0) {  // diagnostic: the row loads alone, one row prefetched
-        for (int r = 0; r < R; ++r) {
-            float2 a2[16], b2[16];
-            const float2 *nx = sym + (long long)(r + 1 < R ? r + 1 : r) * Cp;
-            row_load<true>(nx + 1024 * E, t, a2);
-            row_load<true>(nx + 1024 * (E + 2), t, b2);
-#pragma unroll
-            for (int m = 0; m < 16; ++m) {
-                ae[m] = float2{ae[m].x + a[m].x, ae[m].y + a[m].y};
-                ao[m] = float2{ao[m].x + b[m].x, ao[m].y + b[m].y};
-                a[m] = a2[m];
-                b[m] = b2[m];
-            }
-            if (!(DBG & 1)) td1024::lds_barrier();
-        }
-        return;
-    }
     const unsigned hb0 = lds_addr(HB), hb1 = lds_addr(HB + C);
-    constexpr int NB = HP == 4 ? 2 : 1;  // Hc buffers
-    const hl::TwAnchors ca = {}, cb = {};  // (read per row inside x_row)
-    // SW: odd rows swap the images (x_row)
-    float2 *Tq = const_cast<float2 *>(Tp);
     for (int r = 0; r + 1 < R; ++r)
-        x_row<E, PK, true, DBG, TW, HP, HE, IL, SW>(sym + (long long)(r + 1) * Cp,
-                                                    HB + (NB == 2 ? (r & 1) * C : 0) + E * 2048, t,
-                                                    SW && (r & 1) ? Tq : T, SW && (r & 1) ? T : Tp, tw1, tw2, wb0,
-                                                    wb1, a, b, ae, ao, Hg + (long long)(r + 1) * C,
-                                                    NB == 2 && !(r & 1) ? hb1 : hb0, ca, cb);
-    x_row<E, PK, false, DBG, TW, HP, HE, IL, SW>(sym, HB + (NB == 2 ? ((R - 1) & 1) * C : 0) + E * 2048, t,
-                                                 SW && ((R - 1) & 1) ? Tq : T, SW && ((R - 1) & 1) ? T : Tp, tw1,
-                                                 tw2, wb0, wb1, a, b, ae, ao, nullptr, 0, ca, cb);
+        x_row<E, true>(sym + (long long)(r + 1) * Cp, HB + (r & 1) * C + E * 2048, t, T, Tp, tw1, tw2, wb0, wb1, a,
+                       b, ae, ao, Hg + (long long)(r + 1) * C, (r & 1) ? hb0 : hb1);
+    x_row<E, false>(sym, HB + ((R - 1) & 1) * C + E * 2048, t, T, Tp, tw1, tw2, wb0, wb1, a, b, ae, ao, nullptr, 0);
 }
 
-constexpr int H_PK = 7;  // packed-f32 split, FFT halves and MAC (pk.hpp)
-
-// The MRC of one logical block (HP pairs = HP data symbols of frame f, pair
+// The MRC of one logical block (H_PAIRS pairs = data symbols of frame f, pair
 // `pair` on symbol j < nsym when `store`; s = its symbol slot) after the
 // workgroup prologue: Hc row 0 DMA, tables, rows, normalise, staged stores.
-template <int DBG = 0, int TW = 3, int HP = H_PAIRS, int HE = 0, int IL = 0, bool SW = false>
 __device__ __forceinline__ void mrc4096_block(const float2 *__restrict__ iq, int S, int R, int prefix,
                                               const float2 *Hc, const float *P, float2 *__restrict__ out,
                                               long long f, int j, bool store, int s, float2 *lds, int mode) {
@@ -488,10 +355,10 @@ __device__ __forceinline__ void mrc4096_block(const float2 *__restrict__ iq, int
     const float2 *tw1 = lds, *tw2 = lds + hl::TW1S;
     float2 *T = lds + X_TAB + w * hl::TS;
     const float2 *Tp = lds + X_TAB + (w ^ 1) * hl::TS;
-    float2 *HB = lds + X_TAB + 2 * HP * hl::TS;  // [2][C] Hc rows ([1][C] for HP = 2)
+    float2 *HB = lds + X_TAB + 2 * H_PAIRS * hl::TS;  // [2][C] Hc rows
     const int nsym = S - 1;
     const float2 *Hg = Hc + f * (long long)R * C;
-    dma_hc_row<2 * HP>(Hg, lds_addr(HB));  // row 0; landed at the first row's barrier
+    dma_hc_row(Hg, lds_addr(HB));  // row 0; landed at the first row's barrier
     hl::fill(lds, lds + hl::TW1S);
     __syncthreads();
 
@@ -503,43 +370,13 @@ __device__ __forceinline__ void mrc4096_block(const float2 *__restrict__ iq, int
 #pragma unroll
     for (int k = 0; k < 16; ++k) ae[k] = ao[k] = float2{0.f, 0.f};
     if (e)
-        h_rows<1, H_PK, DBG, TW, HP, HE, IL, SW>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
+        h_rows<1>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
     else
-        h_rows<0, H_PK, DBG, TW, HP, HE, IL, SW>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
+        h_rows<0>(sym, Cp, R, Hg, HB, t, T, Tp, tw1, tw2, wb0, wb1, ae, ao);
     const long long q = f * nsym + j;
     const int b0 = lane_bin0(t);
     float2 *o = out + q * K;
     const float *Pf = P + f * C;
-    if (DBG & 4) {  // diagnostic: no output stores (keep the sums live)
-        float sacc = 0.f;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) sacc += ae[k].x * ae[k].y + ao[k].x * ao[k].y;
-        if (store && sacc == 1234.5f) out[q] = float2{sacc, 0.f};
-        return;
-    }
-    if (DBG & 32) {  // A/B: the round-1 epilogue, scattered plain stores
-        if (!store) return;
-        if ((mode & 1) == 0) {
-#pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                const int be = 4 * (b0 + 16 * k) + e;
-                if (be > 0) {
-                    const float pv = Pf[be];
-                    o[out_pos(be - 1, K)] = float2{ae[k].x / pv, ae[k].y / pv};
-                }
-                const float pv = Pf[be + 2];
-                o[out_pos(be + 1, K)] = float2{ao[k].x / pv, ao[k].y / pv};
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                const int be = 4 * (b0 + 16 * k) + e;
-                if (be > 0) o[be - 1] = ae[k];
-                o[be + 1] = ao[k];
-            }
-        }
-        return;
-    }
     // Normalise, then stage the pair's 4095 outputs through its two transpose
     // images, 1024 positions per image and pass (pass h in image h & 1), and
     // store them as contiguous 512-B nontemporal wave stores: wave e stores
@@ -582,8 +419,7 @@ __device__ __forceinline__ void mrc4096_block(const float2 *__restrict__ iq, int
     }
 }
 
-template <int DBG = 0, int TW = 3, int HP = H_PAIRS, int HE = 0, int IL = 0, bool SW = false>
-__global__ void __attribute__((amdgpu_flat_work_group_size(128 * HP, 128 * HP), amdgpu_waves_per_eu(2, 2)))
+__global__ void __attribute__((amdgpu_flat_work_group_size(128 * H_PAIRS, 128 * H_PAIRS), amdgpu_waves_per_eu(2, 2)))
 k_mrc_td4096h(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
               const float *__restrict__ P, float2 *__restrict__ out, long long nframes, long long nblocks,
               long long per_xcd, int mode) {
@@ -593,54 +429,14 @@ k_mrc_td4096h(const float2 *__restrict__ iq, int S, int R, int prefix, const flo
     const long long lb = (pb & 7) * per_xcd + (pb >> 3);  // XCD-grouped: a frame's blocks share an L2
     if (lb >= nblocks) return;  // whole workgroup
     const int nsym = S - 1;
-    const long long bpf = (nsym + HP - 1) / HP;
-    const long long f = lb / bpf;
-    const int j = (int)(lb - f * bpf) * HP + pair;  // data symbol index within the frame
-    const bool store = j < nsym;
-    const int s = 1 + (store ? j : nsym - 1);
-    mrc4096_block<DBG, TW, HP, HE, IL, SW>(iq, S, R, prefix, Hc, P, out, f, j, store, s, lds, mode);
-}
-
-
-// One-launch frame demod (ofdm_frame_demod, C = 4096; frame_td.hip
-// k_demod_td1024 for the protocol): workgroups 0 .. nls-1 estimate one frame
-// each in the LS LDS layout (write-through) and publish it; each MRC
-// workgroup (frame-aligned: one frame) waits for its frame, or estimates it
-// itself when the bounded wait expires, before its Hc row 0 DMA.  LDS: the
-// MRC's 140 KiB; the LS layout needs 132, the word after it carries the
-// wait's outcome (inside the second Hc buffer, first written by row 1's DMA).
-template <int DBG = 0>
-__global__ void __attribute__((amdgpu_flat_work_group_size(128 * H_PAIRS, 128 * H_PAIRS), amdgpu_waves_per_eu(2, 2)))
-k_demod_td4096(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ X, float2 *Hc,
-               float *P, float2 *__restrict__ out, long long nblocks, long long per_xcd,
-               unsigned long long *flags, unsigned long long epoch, int nls, long long nframes,
-               long long spin_ticks) {
-    static_assert(ls_lds(2 * H_PAIRS) + 16 <= H_LDS, "the LS layout and the flag word fit the MRC's LDS");
-    extern __shared__ __attribute__((aligned(16))) float2 lds[];
-    if ((int)blockIdx.x < nls) {  // estimator workgroup
-        const long long f = blockIdx.x;
-        if (f >= nframes) return;
-        ls_frame4096<2 * H_PAIRS, true>(iq, S, R, prefix, X, Hc, P, f, lds, 0);
-        td1024::publish_flag(flags + f, epoch);
-        return;
-    }
-    const int pair = __builtin_amdgcn_readfirstlane(threadIdx.x >> 7);
-    const long long pb = blockIdx.x - nls;
-    const long long lb = (pb & 7) * per_xcd + (pb >> 3);
-    if (lb >= nblocks) return;  // whole workgroup
-    const int nsym = S - 1;
     const long long bpf = (nsym + H_PAIRS - 1) / H_PAIRS;
     const long long f = lb / bpf;
-    const int j = (int)(lb - f * bpf) * H_PAIRS + pair;
+    const int j = (int)(lb - f * bpf) * H_PAIRS + pair;  // data symbol index within the frame
     const bool store = j < nsym;
     const int s = 1 + (store ? j : nsym - 1);
-    int *seen = reinterpret_cast<int *>(reinterpret_cast<char *>(lds) + ls_lds(2 * H_PAIRS));
-    if (!td1024::consume_flags(flags, f, f, epoch, spin_ticks, seen)) {
-        ls_frame4096<2 * H_PAIRS, true>(iq, S, R, prefix, X, Hc, P, f, lds, 0);
-        td1024::acquire_all();
-    }
-    mrc4096_block<DBG, 3, H_PAIRS, 0, 3>(iq, S, R, prefix, Hc, P, out, f, j, store, s, lds, 0);
+    mrc4096_block(iq, S, R, prefix, Hc, P, out, f, j, store, s, lds, mode);
 }
+
 
 }  // namespace td4096
 
@@ -664,46 +460,11 @@ hipError_t launch_mrc_td4096(const float2 *iq, long long nframes, int S, int R, 
     if (nq <= 0) return hipSuccess;
     const long long bpf = ((S - 1) + H_PAIRS - 1) / H_PAIRS, nb = nframes * bpf, pxcd = (nb + 7) / 8;
     if (pxcd * 8 > 0x7fffffffll) return hipErrorInvalidValue;
-    // IL = 3: the row's two FFT1024s software-pipelined through the transpose
+    // The row's two FFT1024s software-pipelined through the transpose
     // image and the first quarter of the next row issued at the row start
     // (same-process A/B, R=32 x 300 frames: 6.81 vs 7.53 ms, bit-identical;
     // profiles/r3/r3_ab_il*_c4096.jsonl)
-    auto kern = k_mrc_td4096h<0, 3, H_PAIRS, 0, 3>;
-#ifdef OFDM_AB_KNOBS
-    if (ab_knob("MRC4K_IL", 3) == 0) kern = k_mrc_td4096h<0>;  // round 2's row (FFTs one after the other)
-    switch (ab_knob("MRC4K_DBG", 0)) {
-        case 1: kern = k_mrc_td4096h<1>; break;
-        case 2: kern = k_mrc_td4096h<2>; break;
-        case 4: kern = k_mrc_td4096h<4>; break;
-        case 8: kern = k_mrc_td4096h<8>; break;
-        case 16: kern = k_mrc_td4096h<16>; break;
-        case 32: kern = k_mrc_td4096h<32>; break;
-        case 64: kern = k_mrc_td4096h<64>; break;
-        case 65: kern = k_mrc_td4096h<65>; break;
-        case 128: kern = k_mrc_td4096h<128>; break;
-        default: break;
-    }
-    if (ab_knob("MRC4K_TW", 3) == 0) kern = k_mrc_td4096h<0, 0>;  // table twiddles (round 1)
-    switch (ab_knob("MRC4K_HE", 0)) {  // when this row's Hc planes are read from LDS (x_row)
-        case 1: kern = k_mrc_td4096h<0, 3, H_PAIRS, 1>; break;
-        case 2: kern = k_mrc_td4096h<0, 3, H_PAIRS, 2>; break;
-        default: break;
-    }
-    if (ab_knob("MRC4K_IL", 0) == 1) kern = k_mrc_td4096h<0, 3, H_PAIRS, 0, 1>;  // FFTs software-pipelined
-    if (ab_knob("MRC4K_IL", 0) == 3) kern = k_mrc_td4096h<0, 3, H_PAIRS, 0, 3>;  // + a quarter at row start
-    if (ab_knob("MRC4K_IL", 0) == 67) kern = k_mrc_td4096h<64, 3, H_PAIRS, 0, 3>;  // IL=3 compute only (diag)
-    if (ab_knob("MRC4K_IL", 0) == 65) kern = k_mrc_td4096h<64, 3, H_PAIRS, 0, 1>;  // + compute only (diag)
-    if (ab_knob("MRC4K_SW", 0) == 1) kern = k_mrc_td4096h<0, 3, H_PAIRS, 0, 3, true>;  // one barrier per row
-    if (ab_knob("MRC4K_HP", 4) == 2) {  // two independent 2-pair workgroups per CU, single Hc buffer
-        const long long bpf2 = ((S - 1) + 1) / 2, nb2 = nframes * bpf2, px2 = (nb2 + 7) / 8;
-        if (px2 * 8 > 0x7fffffffll) return hipErrorInvalidValue;
-        auto k2 = k_mrc_td4096h<0, 3, 2>;
-        if (hipError_t e = opt_in_lds(reinterpret_cast<const void *>(k2), (int)h_lds(2)); e != hipSuccess) return e;
-        hipLaunchKernelGGL(k2, dim3((unsigned)(px2 * 8)), dim3(256), h_lds(2), s, iq, S, R, prefix, Hc, P, out,
-                           nframes, nb2, px2, mode);
-        return hipGetLastError();
-    }
-#endif
+    auto kern = k_mrc_td4096h;
     if (hipError_t e = opt_in_lds(reinterpret_cast<const void *>(kern), (int)H_LDS); e != hipSuccess)
         return e;  // > 64 KiB of dynamic LDS
     hipLaunchKernelGGL(kern, dim3((unsigned)(pxcd * 8)), dim3(128 * H_PAIRS), H_LDS, s, iq, S, R, prefix,
@@ -711,23 +472,5 @@ hipError_t launch_mrc_td4096(const float2 *iq, long long nframes, int S, int R, 
     return hipGetLastError();
 }
 
-#ifdef OFDM_AB_KNOBS  // A/B build only: no faster than the two launches
-hipError_t launch_demod_td4096(const float2 *iq, long long nframes, int S, int R, int prefix, const float2 *X,
-                               float2 *Hc, float *P, float2 *out, unsigned long long *flags,
-                               unsigned long long epoch, hipStream_t s) {
-    using namespace td4096;
-    const long long nq = nframes * (S - 1);
-    if (nq <= 0) return hipSuccess;
-    const long long bpf = ((S - 1) + H_PAIRS - 1) / H_PAIRS, nb = nframes * bpf, pxcd = (nb + 7) / 8;
-    const long long nls = (nframes + 7) / 8 * 8;
-    if (pxcd * 8 + nls > 0x7fffffffll) return hipErrorInvalidValue;
-    auto kern = k_demod_td4096<0>;
-    if (hipError_t e = opt_in_lds(reinterpret_cast<const void *>(kern), (int)H_LDS); e != hipSuccess) return e;
-    hipLaunchKernelGGL(kern, dim3((unsigned)(nls + pxcd * 8)), dim3(128 * H_PAIRS), H_LDS, s, iq, S, R, prefix, X,
-                       Hc, P, out, nb, pxcd, flags, epoch, (int)nls, nframes,
-                       (long long)ab_knob("DEMOD_SPIN", (int)td1024::SPIN_TICKS));
-    return hipGetLastError();
-}
-#endif
 
 }  // namespace ofdm

@@ -29,17 +29,6 @@ inline hipError_t opt_in_lds(const void *kernel, int bytes) {
     return e;
 }
 
-// Experiment switches.  The product library (make) has none: ab_knob() is the
-// compile-time default and no environment variable changes what a kernel
-// computes or which kernel runs.  The A/B build (make ab ->
-// lib/libofdm_lsmrc_ab.so, -DOFDM_AB_KNOBS) reads OFDM_AB_<name> on every
-// launch, for same-process comparisons of candidate kernels in scripts/.
-#ifdef OFDM_AB_KNOBS
-int ab_knob(const char *name, int def);
-#else
-constexpr int ab_knob(const char *, int def) { return def; }
-#endif
-
 // Sets ofdm_last_error() for the calling thread and returns `code`.
 int set_error(int code, const char *msg);
 
@@ -98,7 +87,7 @@ hipError_t launch_mrc_td1024(const float2 *iq, long long nframes, int S, int R, 
 // a per-launch value no flag holds.  mode 0 (full demod) only.
 hipError_t launch_demod_td1024(const float2 *iq, long long nframes, int S, int R, int prefix, const float2 *X,
                                float2 *Hc, float *P, float2 *out, unsigned long long *flags,
-                               unsigned long long epoch, hipStream_t s);
+                               unsigned long long epoch, long long spin_ticks, hipStream_t s);
 
 // Stage-wise operations of the reference's per-stage gpuLS methods (stages.hip).
 // fused time-domain receiver, C = 2048 (frame_td2048.hip); same contracts
@@ -106,21 +95,11 @@ hipError_t launch_ls_td2048(const float2 *iq, long long nframes, int S, int R, i
                             const float2 *X, float2 *Hc, float *P, int partial, hipStream_t s);
 hipError_t launch_mrc_td2048(const float2 *iq, long long nframes, int S, int R, int prefix,
                              const float2 *Hc, const float *P, float2 *out, int mode, hipStream_t s);
-#ifdef OFDM_AB_KNOBS  // one launch at C = 2048 (A/B build only)
-hipError_t launch_demod_td2048(const float2 *iq, long long nframes, int S, int R, int prefix, const float2 *X,
-                               float2 *Hc, float *P, float2 *out, unsigned long long *flags,
-                               unsigned long long epoch, hipStream_t s);
-#endif
 // fused time-domain receiver, C = 4096 (frame_td4096.hip); same contracts
 hipError_t launch_ls_td4096(const float2 *iq, long long nframes, int S, int R, int prefix,
                             const float2 *X, float2 *Hc, float *P, int partial, hipStream_t s);
 hipError_t launch_mrc_td4096(const float2 *iq, long long nframes, int S, int R, int prefix,
                              const float2 *Hc, const float *P, float2 *out, int mode, hipStream_t s);
-#ifdef OFDM_AB_KNOBS  // one launch at C = 4096 (A/B build only)
-hipError_t launch_demod_td4096(const float2 *iq, long long nframes, int S, int R, int prefix, const float2 *X,
-                               float2 *Hc, float *P, float2 *out, unsigned long long *flags,
-                               unsigned long long epoch, hipStream_t s);
-#endif
 hipError_t launch_conj_product(const float2 *Y, long long nsyms, int R, int C, const float2 *Hc,
                                float2 *prod, hipStream_t s);
 hipError_t launch_combine(const float2 *prod, long long nsyms, int R, int K, const float *P,

@@ -215,7 +215,7 @@ hipError_t launch_mrc_freq(const float2 *Y, long long frame_stride, long long sy
                            long long p_fstride, int p_jofs, float2 *out, int mode, hipStream_t s) {
     const long long nq = nframes * nsym;
     if (nq <= 0) return hipSuccess;
-    if (ab_knob("MRCF_V", 1) == 1 && C >= 512 && hc_jofs == 0 && hc_ld == C && (hc_fstride % 2) == 0 &&
+    if (C >= 512 && hc_jofs == 0 && hc_ld == C && (hc_fstride % 2) == 0 &&
         (sym_stride % 2) == 0 &&
         (frame_stride % 2) == 0 && ((uintptr_t)Hc % 16) == 0 && ((uintptr_t)Y % 16) == 0) {
         const int bps = C / 2 / 256;
@@ -223,20 +223,6 @@ hipError_t launch_mrc_freq(const float2 *Y, long long frame_stride, long long sy
         // (2 waves/SIMD, 32 KiB in flight per wave), 4 at C = 4096
         auto kern = C >= 4096 ? k_mrc_freq_frames<4, 4> : k_mrc_freq_frames<8, 4>;
         int g = C >= 4096 ? 4 : 8;
-#ifdef OFDM_AB_KNOBS
-        switch (ab_knob("MRCF_GU", 0)) {
-            case 24: kern = k_mrc_freq_frames<2, 4>; g = 2; break;
-            case 28: kern = k_mrc_freq_frames<2, 8>; g = 2; break;
-            case 42: kern = k_mrc_freq_frames<4, 2>; g = 4; break;
-            case 48: kern = k_mrc_freq_frames<4, 8>; g = 4; break;
-            case 82: kern = k_mrc_freq_frames<8, 2>; g = 8; break;
-            case 84: kern = k_mrc_freq_frames<8, 4>; g = 8; break;
-            case 18: kern = k_mrc_freq_frames<1, 8>; g = 1; break;
-            case 44: kern = k_mrc_freq_frames<4, 4>; g = 4; break;
-            case 144: kern = k_mrc_freq_frames<4, 4, false>; g = 4; break;
-            default: break;
-        }
-#endif
         const long long nbg = nframes * ((nsym + g - 1) / g) * bps, pxg = (nbg + 7) / 8;
         if (pxg * 8 > 0x7fffffffll) return hipErrorInvalidValue;
         hipLaunchKernelGGL(kern, dim3((unsigned)(pxg * 8)), dim3(256), 0, s, Y, frame_stride, sym_stride, nsym, R,

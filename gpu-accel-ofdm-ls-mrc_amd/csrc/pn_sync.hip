@@ -56,7 +56,7 @@ __device__ __forceinline__ void cmac_exact(v2f &acc, v2f p, v2f v) {
     asm("v_pk_add_f32 %0, %0, %1" : "+v"(acc) : "v"(t1));
 }
 
-template <bool STORE, bool PK>
+template <bool STORE>
 __global__ void __launch_bounds__(NT) k_pn_correlate(const float2 *__restrict__ buf, long long N,
                                                      const float2 *__restrict__ pn, int L,
                                                      float thres, long long nl, int nblk,
@@ -74,13 +74,9 @@ __global__ void __launch_bounds__(NT) k_pn_correlate(const float2 *__restrict__ 
     // one tap are constant offsets (0, 512, 1024, 1536 B) from one address
     const int lb = (t >> 6) * (64 * LPT) + (t & 63);
 
-    float ar[LPT], ai[LPT];
     v2f acc[LPT];
 #pragma unroll
-    for (int k = 0; k < LPT; ++k) {
-        ar[k] = ai[k] = 0.f;
-        acc[k] = (v2f){0.f, 0.f};
-    }
+    for (int k = 0; k < LPT; ++k) acc[k] = (v2f){0.f, 0.f};
 
     for (int j0 = 0; j0 < L; j0 += JC) {
         const int jn = L - j0 < JC ? L - j0 : JC;
@@ -111,14 +107,7 @@ __global__ void __launch_bounds__(NT) k_pn_correlate(const float2 *__restrict__ 
 #pragma unroll
                 for (int k = 0; k < LPT; ++k) {
                     const float2 v = xl[j + u + 64 * k];
-                    if constexpr (PK) {
-                        cmac_exact(acc[k], __builtin_bit_cast(v2f, p), __builtin_bit_cast(v2f, v));
-                        continue;
-                    }
-                    const float pr = p.x * v.x - p.y * v.y;  // std::complex<float> operator*
-                    const float pi = p.x * v.y + p.y * v.x;
-                    ar[k] = ar[k] + pr;
-                    ai[k] = ai[k] + pi;
+                    cmac_exact(acc[k], __builtin_bit_cast(v2f, p), __builtin_bit_cast(v2f, v));
                 }
             }
         }
@@ -127,14 +116,7 @@ __global__ void __launch_bounds__(NT) k_pn_correlate(const float2 *__restrict__ 
 #pragma unroll
             for (int k = 0; k < LPT; ++k) {
                 const float2 v = xl[j + 64 * k];
-                if constexpr (PK) {
-                    cmac_exact(acc[k], __builtin_bit_cast(v2f, p), __builtin_bit_cast(v2f, v));
-                    continue;
-                }
-                const float pr = p.x * v.x - p.y * v.y;
-                const float pi = p.x * v.y + p.y * v.x;
-                ar[k] = ar[k] + pr;
-                ai[k] = ai[k] + pi;
+                cmac_exact(acc[k], __builtin_bit_cast(v2f, p), __builtin_bit_cast(v2f, v));
             }
         }
     }
@@ -142,11 +124,7 @@ __global__ void __launch_bounds__(NT) k_pn_correlate(const float2 *__restrict__ 
     for (int k = 0; k < LPT; ++k) {
         const long long i = i0 + lb + 64 * k;
         if (i >= nl) continue;
-        if constexpr (PK) {
-            ar[k] = acc[k].x;
-            ai[k] = acc[k].y;
-        }
-        const double dr = ar[k], di = ai[k];
+        const double dr = acc[k].x, di = acc[k].y;
         const float m = (float)__builtin_sqrt(dr * dr + di * di) / (float)L;  // hypotf / L
         const unsigned long long key = (unsigned long long)ch * nl + i;
         if (STORE) mag[key] = m;
@@ -184,20 +162,13 @@ hipError_t launch_pn_correlate(const float2 *buf, int R, long long N, const floa
     const long long nblk = (nl + pn::TILE - 1) / pn::TILE;
     if (nblk * R > 0x7fffffffll) return hipErrorInvalidValue;
     auto *best = reinterpret_cast<unsigned long long *>(pos);
-    // packed exact MAC (the scalar form, bit-identical and 5 % slower, is
-    // kept for the A/B build: OFDM_AB_PN_PK=0)
-    const bool pk = ab_knob("PN_PK", 1) != 0;
-#define OFDM_PN_LAUNCH(ST, PKV)                                                                  \
-    hipLaunchKernelGGL((pn::k_pn_correlate<ST, PKV>), dim3((unsigned)(nblk * R)), dim3(pn::NT), 0, \
-                       s, buf, N, pn, L, thres, nl, (int)nblk, best, mag)
-    if (mag) {
-        if (pk) OFDM_PN_LAUNCH(true, true);
-        else OFDM_PN_LAUNCH(true, false);
-    } else {
-        if (pk) OFDM_PN_LAUNCH(false, true);
-        else OFDM_PN_LAUNCH(false, false);
-    }
-#undef OFDM_PN_LAUNCH
+    // packed exact MAC (the scalar form is bit-identical and 5 % slower)
+    if (mag)
+        hipLaunchKernelGGL((pn::k_pn_correlate<true>), dim3((unsigned)(nblk * R)), dim3(pn::NT), 0, s, buf,
+                           N, pn, L, thres, nl, (int)nblk, best, mag);
+    else
+        hipLaunchKernelGGL((pn::k_pn_correlate<false>), dim3((unsigned)(nblk * R)), dim3(pn::NT), 0, s,
+                           buf, N, pn, L, thres, nl, (int)nblk, best, mag);
     return hipGetLastError();
 }
 

@@ -24,9 +24,9 @@
 //     for MT * ST complex MACs.  At U = 16, R = 64 the work is ~13 flop per HBM
 //     byte, under the FP32 ridge (~20): HBM-bound on paper (at U = 32, 26
 //     flop/B, compute-bound).  The f32 matrix peak of gfx950 equals its f32
-//     vector peak (MI355X_MICROARCH.md); k_zf_mfma / k_zf_mfma_lds below put
-//     the MACs on the matrix cores anyway (16-block 4x4x1 MFMA, one block per
-//     subcarrier) and win only for detect at U >= 32.
+//     vector peak (MI355X_MICROARCH.md); the k_zf_mfma_* / k_zf_wstat kernels
+//     below put the MACs on the matrix cores anyway (16-block 4x4x1 MFMA, one
+//     block per subcarrier) and win for detect at U > 8.
 //     The W tile of a (subcarrier block, row block) is re-read for every symbol
 //     step; block ids are mapped so that all workgroups of one XCD share the
 //     same few tiles (dispatch is round-robin over the 8 XCDs), keeping those
@@ -458,132 +458,10 @@ k_zf_gemm_lds(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__r
     }
 }
 
-// The same GEMM with the chunks DMA'd straight into LDS (global_load_lds_dword:
-// lane l of an instruction moves dword l of a 256-B half row, so rows of
-// 64 subcarriers land in LDS in their natural float2 order; 4-B granules
-// because a row starts at an odd multiple of 8 B when K is odd).  No VGPR
-// staging, so NB = 4 LDS buffers of one n-step each keep three steps of
-// loads in flight behind the MACs.  Per step: wait until this wave's loads of
-// step c have landed (vmcnt = the two younger steps' loads), one barrier
-// (everyone's rows of step c visible, everyone done with step c - 1), issue
-// step c + 3 into step c - 1's buffer, MACs.
 typedef __attribute__((address_space(3))) void lvoid_t;
 
-// One global_load_lds_dword: lane l's dword lands at LDS byte lds + 4 l.  In
-// inline asm on purpose: through __builtin_amdgcn_global_load_lds the
-// compiler cannot tell which buffer a ds_read may alias and puts
-// s_waitcnt vmcnt(0) in front of every LDS read, draining the prefetch.  The
-// loop's own s_waitcnt vmcnt(N) + s_barrier publish the data instead.  M0 is
-// compiler-reserved: saved and restored in the same statement, with the
-// s_nop the M0 write -> LDS-DMA hazard needs (cdna_hip_programming.md).
-__device__ __forceinline__ void dma_dword(const float *g, unsigned lds) {
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\t"
-                 "s_mov_b32 m0, %0"
-                 : "=&s"(keep)
-                 : "v"(g), "s"(lds)
-                 : "memory");
-}
-
-template <int MG, bool CONJ>
-__global__ void __launch_bounds__(256) k_zf_gemm_dma(const float2 *__restrict__ Wt, int a_m, int a_n,
-                                                     const float2 *__restrict__ in, int N, int M, int K,
-                                                     long long nsym, float2 *__restrict__ out, int ntile,
-                                                     int tpx, int nkb, long long chunk_steps) {
-    constexpr int MT = 8, ST = 8, SG = 4 / MG, MB = MG * MT, SB = SG * ST, NB = 4;
-    constexpr int ROWS = MB + SB, RPW = ROWS / 4, LPW = 2 * RPW;
-    static_assert(ROWS % 4 == 0 && (NB - 2) * LPW <= 63, "rows per wave / vmcnt range");
-    __shared__ float2 sm[NB][ROWS * 64];
-    const int b = blockIdx.x, xcd = b & 7, j = b >> 3;  // XCD-aware mapping as k_zf_gemm
-    const int tile = xcd + 8 * (j % tpx);
-    if (tile >= ntile) return;  // whole workgroup
-    const long long chunk = j / tpx;
-    const int kb = tile % nkb, mb = tile / nkb;
-    const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int k = kb * 64 + lane;
-    const int mg = w % MG, sg = w / MG, mb0 = mb * MB;
-    const long long nsteps_total = (nsym + SB - 1) / SB;
-    const long long step0 = chunk * chunk_steps, step1 = min(step0 + chunk_steps, nsteps_total);
-    const long long nseq = (step1 - step0) * N;  // one n per LDS chunk
-    if (nseq <= 0) return;  // whole workgroup
-    // this lane's dword within a half row: element e0 + (lane >> 1) (clamped
-    // to K - 1 past the end: those subcarriers are computed, never stored)
-    const int eh0 = min(kb * 64 + (lane >> 1), K - 1), eh1 = min(kb * 64 + 32 + (lane >> 1), K - 1);
-    const int comp = lane & 1;
-
-    auto issue = [&](long long c) {  // step c (clamped: the tail re-loads the last step)
-        c = min(c, nseq - 1);
-        const int buf = (int)(c % NB);
-        const long long s0 = (step0 + c / N) * SB;
-        const int n = (int)(c % N);
-#pragma unroll
-        for (int i = 0; i < RPW; ++i) {
-            const int row = w + 4 * i;
-            const float2 *src;
-            if (row < MB) {
-                const int m = min(mb0 + row, M - 1);
-                src = Wt + ((long long)m * a_m + (long long)n * a_n) * K;
-            } else {
-                const long long s = min(s0 + (row - MB), nsym - 1);
-                src = in + (s * N + n) * (long long)K;
-            }
-            const unsigned la = (unsigned)(size_t)(lvoid_t *)&sm[buf][row * 64];  // LDS byte address
-            dma_dword(reinterpret_cast<const float *>(src + eh0) + comp, la);
-            dma_dword(reinterpret_cast<const float *>(src + eh1) + comp, la + 256);
-        }
-    };
-
-    float2 acc[MT][ST];
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int jj = 0; jj < ST; ++jj) acc[i][jj] = float2{0.f, 0.f};
-#pragma unroll
-    for (int p = 0; p < NB - 1; ++p) issue(p);
-    for (long long c = 0; c < nseq; ++c) {
-        // no __syncthreads(): its fence would wait for every load in flight
-        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((NB - 2) * LPW) : "memory");
-        issue(c + NB - 1);  // into the buffer of step c - 1, which everyone has finished
-        const float2 *sa = sm[c % NB] + (mg * MT) * 64 + lane;
-        const float2 *sx = sm[c % NB] + (MB + sg * ST) * 64 + lane;
-        float2 a[MT], x[ST];
-#pragma unroll
-        for (int i = 0; i < MT; ++i) a[i] = sa[i * 64];
-#pragma unroll
-        for (int jj = 0; jj < ST; ++jj) x[jj] = sx[jj * 64];
-#pragma unroll
-        for (int i = 0; i < MT; ++i) {
-            const float ar = a[i].x, ai = CONJ ? -a[i].y : a[i].y;
-#pragma unroll
-            for (int jj = 0; jj < ST; ++jj) {
-                acc[i][jj].x = fmaf(ar, x[jj].x, fmaf(-ai, x[jj].y, acc[i][jj].x));
-                acc[i][jj].y = fmaf(ar, x[jj].y, fmaf(ai, x[jj].x, acc[i][jj].y));
-            }
-        }
-        if (c % N == N - 1) {  // last n of a symbol step: store, reset
-            const long long s0 = (step0 + c / N) * SB + sg * ST;
-            const int m0 = mb0 + mg * MT;
-            if (k < K) {
-#pragma unroll
-                for (int jj = 0; jj < ST; ++jj) {
-                    if (s0 + jj >= nsym) break;
-                    float2 *o = out + ((s0 + jj) * M) * (long long)K + k;
-#pragma unroll
-                    for (int i = 0; i < MT; ++i)
-                        if (m0 + i < M) o[(long long)(m0 + i) * K] = acc[i][jj];
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < MT; ++i)
-#pragma unroll
-                for (int jj = 0; jj < ST; ++jj) acc[i][jj] = float2{0.f, 0.f};
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the tail re-loads before exit
-}
-
-// The same GEMM on the matrix cores (k_zf_mfma): v_mfma_f32_4x4x1_16b_f32
+// The GEMM on the matrix cores (the k_zf_mfma_* / k_zf_wstat kernels below):
+// v_mfma_f32_4x4x1_16b_f32
 // runs 16 INDEPENDENT 4 x 4 x 1 outer products per instruction, one per
 // 4-lane block, at the full f32 matrix rate (64 flop/clk/SIMD, the f32 vector
 // peak, MI355X_MICROARCH.md) -- so each block is one subcarrier and the
@@ -602,276 +480,19 @@ __global__ void __launch_bounds__(256) k_zf_gemm_dma(const float2 *__restrict__ 
 // accumulation is an exact f32 fma chain (MI355X_MICROARCH.md).
 typedef float mf4 __attribute__((ext_vector_type(4)));
 
-template <int MP, int SG, bool CONJ>
-__global__ void __launch_bounds__(256) k_zf_mfma(const float2 *__restrict__ Wt, int a_m, int a_n,
-                                                 const float2 *__restrict__ in, int N, int M, int K,
-                                                 long long nsym, float2 *__restrict__ out, int ntile, int tpx,
-                                                 int nkb, long long chunk_steps) {
-    constexpr int SW = 4 * SG, SBLK = 4 * SW;  // symbols per wave / per workgroup step
-    const int bid = blockIdx.x, xcd = bid & 7, jb = bid >> 3;  // XCD-aware mapping as k_zf_gemm
-    const int tile = xcd + 8 * (jb % tpx);
-    if (tile >= ntile) return;
-    const long long chunk = jb / tpx;
-    const int kb = tile % nkb, mb = tile / nkb;
-    const int lane = threadIdx.x & 63, b = lane >> 2, i = lane & 3;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int k = kb * 16 + b, kc = min(k, K - 1);  // lanes past K compute on a valid bin, never store
-    const int m0 = mb * 2 * MP;
-    const long long nsteps_total = (nsym + SBLK - 1) / SBLK;
-    const long long step0 = chunk * chunk_steps, step1 = min(step0 + chunk_steps, nsteps_total);
-    const bool odd = i & 1;
-
-    // W rows of this lane (clamped: rows past M compute, never store)
-    const float2 *wrow[MP];
-#pragma unroll
-    for (int p = 0; p < MP; ++p)
-        wrow[p] = Wt + (long long)min(m0 + 2 * p + (i >> 1), M - 1) * a_m * K + kc;
-    const long long anK = (long long)a_n * K, NK = (long long)N * K;
-
-    for (long long st = step0; st < step1; ++st) {
-        const long long s0 = st * SBLK + w * SW;
-        if (s0 >= nsym) break;  // wave-uniform; no barriers in this kernel
-        const float2 *xrow[SG];
-#pragma unroll
-        for (int g = 0; g < SG; ++g) xrow[g] = in + min(s0 + 4 * g + i, nsym - 1) * NK + kc;
-        mf4 acc[MP][SG];
-#pragma unroll
-        for (int p = 0; p < MP; ++p)
-#pragma unroll
-            for (int g = 0; g < SG; ++g) acc[p][g] = mf4{0.f, 0.f, 0.f, 0.f};
-        float2 wv[MP], xv[SG];
-#pragma unroll
-        for (int p = 0; p < MP; ++p) wv[p] = wrow[p][0];
-#pragma unroll
-        for (int g = 0; g < SG; ++g) xv[g] = xrow[g][0];
-        for (int n = 0; n < N; ++n) {
-            const int nn = min(n + 1, N - 1);  // the last one is a redundant reload
-            float2 wn[MP], xn[SG];
-#pragma unroll
-            for (int p = 0; p < MP; ++p) wn[p] = wrow[p][nn * anK];
-#pragma unroll
-            for (int g = 0; g < SG; ++g) xn[g] = xrow[g][nn * (long long)K];
-            float are[MP], aim[MP];
-#pragma unroll
-            for (int p = 0; p < MP; ++p) {
-                const float wy = CONJ ? -wv[p].y : wv[p].y;
-                are[p] = odd ? wy : wv[p].x;
-                aim[p] = odd ? wv[p].x : -wy;
-            }
-#pragma unroll
-            for (int p = 0; p < MP; ++p)
-#pragma unroll
-                for (int g = 0; g < SG; ++g)
-                    acc[p][g] = __builtin_amdgcn_mfma_f32_4x4x1f32(are[p], xv[g].x, acc[p][g], 0, 0, 0);
-#pragma unroll
-            for (int p = 0; p < MP; ++p)
-#pragma unroll
-                for (int g = 0; g < SG; ++g)
-                    acc[p][g] = __builtin_amdgcn_mfma_f32_4x4x1f32(aim[p], xv[g].y, acc[p][g], 0, 0, 0);
-#pragma unroll
-            for (int p = 0; p < MP; ++p) wv[p] = wn[p];
-#pragma unroll
-            for (int g = 0; g < SG; ++g) xv[g] = xn[g];
-        }
-        if (k < K) {
-#pragma unroll
-            for (int g = 0; g < SG; ++g) {
-                const long long s = s0 + 4 * g + i;  // this lane's column j = i
-                if (s >= nsym) break;
-                float2 *o = out + s * M * (long long)K + k;
-#pragma unroll
-                for (int p = 0; p < MP; ++p) {
-                    const int m = m0 + 2 * p;
-                    if (m < M) o[(long long)m * K] = float2{acc[p][g][0], acc[p][g][1]};
-                    if (m + 1 < M) o[(long long)(m + 1) * K] = float2{acc[p][g][2], acc[p][g][3]};
-                }
-            }
-        }
-    }
-}
-
-// k_zf_mfma fed through LDS (k_zf_mfma_lds): the workgroup DMA's each n-step's
-// operand rows -- MB = 16 rows of A and SB = 4 SG symbols of the input, 64
-// subcarriers (512 B) each, coalesced -- into one of NB LDS buffers
-// (global_load_lds_dword, as k_zf_gemm_dma: three steps in flight, one
-// barrier per step, no VGPR staging), and wave w runs the MFMAs of
-// subcarriers 16 w .. 16 w + 15 of the block, reading its operands from LDS.
-// The 16 dword DMAs of one step of k_zf_mfma_lds<4> (8 rows x 2 halves, row r
-// at LDS byte lds + 2048 r, half h at + 256 h) in one statement: M0 is saved
-// and restored once per step instead of once per load.
-__device__ __forceinline__ void dma_rows8(const float *const (&g)[16], unsigned lds) {
-    const unsigned l0 = lds + 0u;
-    const unsigned l1 = lds + 256u;
-    const unsigned l2 = lds + 2048u;
-    const unsigned l3 = lds + 2304u;
-    const unsigned l4 = lds + 4096u;
-    const unsigned l5 = lds + 4352u;
-    const unsigned l6 = lds + 6144u;
-    const unsigned l7 = lds + 6400u;
-    const unsigned l8 = lds + 8192u;
-    const unsigned l9 = lds + 8448u;
-    const unsigned l10 = lds + 10240u;
-    const unsigned l11 = lds + 10496u;
-    const unsigned l12 = lds + 12288u;
-    const unsigned l13 = lds + 12544u;
-    const unsigned l14 = lds + 14336u;
-    const unsigned l15 = lds + 14592u;
-    unsigned keep;
-    asm volatile("s_mov_b32 %[keep], m0\n\t"
-                 "s_mov_b32 m0, %[l0]\n\ts_nop 0\n\tglobal_load_lds_dword %[a0], off\n\t"
-                 "s_mov_b32 m0, %[l1]\n\ts_nop 0\n\tglobal_load_lds_dword %[a1], off\n\t"
-                 "s_mov_b32 m0, %[l2]\n\ts_nop 0\n\tglobal_load_lds_dword %[a2], off\n\t"
-                 "s_mov_b32 m0, %[l3]\n\ts_nop 0\n\tglobal_load_lds_dword %[a3], off\n\t"
-                 "s_mov_b32 m0, %[l4]\n\ts_nop 0\n\tglobal_load_lds_dword %[a4], off\n\t"
-                 "s_mov_b32 m0, %[l5]\n\ts_nop 0\n\tglobal_load_lds_dword %[a5], off\n\t"
-                 "s_mov_b32 m0, %[l6]\n\ts_nop 0\n\tglobal_load_lds_dword %[a6], off\n\t"
-                 "s_mov_b32 m0, %[l7]\n\ts_nop 0\n\tglobal_load_lds_dword %[a7], off\n\t"
-                 "s_mov_b32 m0, %[l8]\n\ts_nop 0\n\tglobal_load_lds_dword %[a8], off\n\t"
-                 "s_mov_b32 m0, %[l9]\n\ts_nop 0\n\tglobal_load_lds_dword %[a9], off\n\t"
-                 "s_mov_b32 m0, %[l10]\n\ts_nop 0\n\tglobal_load_lds_dword %[a10], off\n\t"
-                 "s_mov_b32 m0, %[l11]\n\ts_nop 0\n\tglobal_load_lds_dword %[a11], off\n\t"
-                 "s_mov_b32 m0, %[l12]\n\ts_nop 0\n\tglobal_load_lds_dword %[a12], off\n\t"
-                 "s_mov_b32 m0, %[l13]\n\ts_nop 0\n\tglobal_load_lds_dword %[a13], off\n\t"
-                 "s_mov_b32 m0, %[l14]\n\ts_nop 0\n\tglobal_load_lds_dword %[a14], off\n\t"
-                 "s_mov_b32 m0, %[l15]\n\ts_nop 0\n\tglobal_load_lds_dword %[a15], off\n\t"
-                 "s_mov_b32 m0, %[keep]"
-                 : [keep] "=&s"(keep)
-                 : [a0] "v"(g[0]), [a1] "v"(g[1]), [a2] "v"(g[2]), [a3] "v"(g[3]), [a4] "v"(g[4]), [a5] "v"(g[5]), [a6] "v"(g[6]), [a7] "v"(g[7]), [a8] "v"(g[8]), [a9] "v"(g[9]), [a10] "v"(g[10]), [a11] "v"(g[11]), [a12] "v"(g[12]), [a13] "v"(g[13]), [a14] "v"(g[14]), [a15] "v"(g[15]),
-                   [l0] "s"(l0), [l1] "s"(l1), [l2] "s"(l2), [l3] "s"(l3), [l4] "s"(l4), [l5] "s"(l5), [l6] "s"(l6), [l7] "s"(l7), [l8] "s"(l8), [l9] "s"(l9), [l10] "s"(l10), [l11] "s"(l11), [l12] "s"(l12), [l13] "s"(l13), [l14] "s"(l14), [l15] "s"(l15)
-                 : "memory");
-}
-
-template <int SG, bool CONJ>
-__global__ void __attribute__((amdgpu_flat_work_group_size(256, 256), amdgpu_waves_per_eu(SG == 4 ? 2 : 1)))
-k_zf_mfma_lds(const float2 *__restrict__ Wt, int a_m, int a_n,
-                                                     const float2 *__restrict__ in, int N, int M, int K,
-                                                     long long nsym, float2 *__restrict__ out, int ntile, int tpx,
-                                                     int nkb, long long chunk_steps) {
-    constexpr int MP = 8, MB = 2 * MP, SB = 4 * SG, NB = 4;
-    constexpr int ROWS = MB + SB, RPW = ROWS / 4, WR = MB / 4, LPW = 2 * RPW;
-    static_assert(ROWS % 4 == 0 && MB % 4 == 0 && (NB - 2) * LPW <= 63, "rows per wave / vmcnt range");
-    extern __shared__ __attribute__((aligned(16))) float2 smd[];  // [NB][ROWS][64]
-    const int bid = blockIdx.x, xcd = bid & 7, jb = bid >> 3;    // XCD-aware mapping as k_zf_gemm
-    const int tile = xcd + 8 * (jb % tpx);
-    if (tile >= ntile) return;  // whole workgroup
-    const long long chunk = jb / tpx;
-    const int kb = tile % nkb, mb = tile / nkb;
-    const int lane = threadIdx.x & 63, b = lane >> 2, i = lane & 3;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int k = kb * 64 + 16 * w + b;
-    const int mb0 = mb * MB;
-    const long long nsteps_total = (nsym + SB - 1) / SB;
-    const long long step0 = chunk * chunk_steps, step1 = min(step0 + chunk_steps, nsteps_total);
-    if (step1 <= step0) return;  // whole workgroup
-    const int nst = (int)(step1 - step0);
-    // this lane's dword of each 256-B half row (clamped past K: computed, never stored)
-    const int off0 = min(kb * 64 + (lane >> 1), K - 1) * 2 + (lane & 1);
-    const int off1 = min(kb * 64 + 32 + (lane >> 1), K - 1) * 2 + (lane & 1);
-    const bool odd = i & 1;
-    const long long anK = (long long)a_n * K, NK = (long long)N * K;
-
-    // DMA issue position (step si, n ni, buffer bi); row bases are wave-uniform
-    int si = 0, ni = 0, bi = 0;
-    const float *wbase[WR];
-#pragma unroll
-    for (int r = 0; r < WR; ++r)
-        wbase[r] = reinterpret_cast<const float *>(Wt + (long long)min(mb0 + w + 4 * r, M - 1) * a_m * K);
-    const unsigned lds0 = (unsigned)(size_t)(lvoid_t *)smd + (unsigned)(w * 512);
-    auto issue = [&]() {
-        const unsigned la = lds0 + (unsigned)(bi * ROWS * 512);
-        const long long s0 = (step0 + si) * SB;
-        const float *ga[2 * RPW];
-#pragma unroll
-        for (int r = 0; r < RPW; ++r) {
-            const float *src;
-            if (r < WR) {
-                src = wbase[r] + 2 * (ni * anK);
-            } else {
-                const long long s = min(s0 + (w + 4 * r - MB), nsym - 1);
-                src = reinterpret_cast<const float *>(in + s * NK + (long long)ni * K);
-            }
-            if constexpr (RPW == 8) {
-                ga[2 * r] = src + off0;
-                ga[2 * r + 1] = src + off1;
-            } else {
-                dma_dword(src + off0, la + r * 2048);
-                dma_dword(src + off1, la + r * 2048 + 256);
-            }
-        }
-        if constexpr (RPW == 8) dma_rows8(ga, la);
-        // advance (the tail re-issues the last step: valid addresses, never read)
-        if (si < nst - 1 || ni < N - 1) {
-            if (++ni == N) {
-                ni = 0;
-                ++si;
-            }
-        }
-        bi = (bi + 1) & (NB - 1);
-    };
-
-    mf4 acc[MP][SG];
-#pragma unroll
-    for (int p = 0; p < MP; ++p)
-#pragma unroll
-        for (int g = 0; g < SG; ++g) acc[p][g] = mf4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int p = 0; p < NB - 1; ++p) issue();
-    int bc = 0;  // buffer of the step being computed
-    for (int st = 0; st < nst; ++st) {
-        for (int n = 0; n < N; ++n) {
-            asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((NB - 2) * LPW) : "memory");
-            if (SG == 4) issue();  // into the buffer of the previous step, which everyone has finished
-            const float2 *sb = smd + bc * ROWS * 64 + 16 * w + b;
-            bc = (bc + 1) & (NB - 1);
-            float are[MP], aim[MP];
-#pragma unroll
-            for (int p = 0; p < MP; ++p) {
-                const float2 wv = sb[(2 * p + (i >> 1)) * 64];
-                const float wy = CONJ ? -wv.y : wv.y;
-                are[p] = odd ? wy : wv.x;
-                aim[p] = odd ? wv.x : -wy;
-            }
-            float2 xv[SG];
-#pragma unroll
-            for (int g = 0; g < SG; ++g) xv[g] = sb[(MB + 4 * g + i) * 64];
-#pragma unroll
-            for (int p = 0; p < MP; ++p)
-#pragma unroll
-                for (int g = 0; g < SG; ++g)
-                    acc[p][g] = __builtin_amdgcn_mfma_f32_4x4x1f32(are[p], xv[g].x, acc[p][g], 0, 0, 0);
-            // SG = 8 (one wave per SIMD): the DMA issue runs in the shadow of
-            // the re-step MFMAs instead of in front of them
-            if (SG == 8) issue();
-#pragma unroll
-            for (int p = 0; p < MP; ++p)
-#pragma unroll
-                for (int g = 0; g < SG; ++g)
-                    acc[p][g] = __builtin_amdgcn_mfma_f32_4x4x1f32(aim[p], xv[g].y, acc[p][g], 0, 0, 0);
-        }
-        // store this step's tile and reset
-        const long long s0 = (step0 + st) * SB;
-        if (k < K) {
-#pragma unroll
-            for (int g = 0; g < SG; ++g) {
-                const long long s = s0 + 4 * g + i;
-                if (s >= nsym) break;
-                float2 *o = out + s * M * (long long)K + k;
-#pragma unroll
-                for (int p = 0; p < MP; ++p) {
-                    const int m = mb0 + 2 * p;
-                    if (m < M) o[(long long)m * K] = float2{acc[p][g][0], acc[p][g][1]};
-                    if (m + 1 < M) o[(long long)(m + 1) * K] = float2{acc[p][g][2], acc[p][g][3]};
-                }
-            }
-        }
-#pragma unroll
-        for (int p = 0; p < MP; ++p)
-#pragma unroll
-            for (int g = 0; g < SG; ++g) acc[p][g] = mf4{0.f, 0.f, 0.f, 0.f};
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // drain the tail re-loads before exit
-}
-
+// The MFMA GEMM fed through LDS: the workgroup DMA's each n-step's operand
+// rows -- MB rows of A and SB symbols of the input, 64 subcarriers (512 B)
+// each, coalesced -- into one of NB = 4 LDS buffers (global_load_lds_dword:
+// lane l's dword lands at LDS byte base + 4 l, so rows land in their natural
+// float2 order with no VGPR staging; three steps in flight, one barrier per
+// step), and each wave runs the MFMAs of its 16 subcarriers reading its
+// operands from LDS.  The DMAs are inline asm on purpose: through
+// __builtin_amdgcn_global_load_lds the compiler cannot tell which buffer a
+// ds_read may alias and puts s_waitcnt vmcnt(0) in front of every LDS read,
+// draining the prefetch; the loop's own s_waitcnt vmcnt(N) + s_barrier
+// publish the data instead.  M0 is compiler-reserved: saved and restored in
+// the same statement, with the s_nop the M0 write -> LDS-DMA hazard needs
+// (cdna_hip_programming.md).
 // The 12 dword DMAs of one wave's step in k_zf_mfma_lds8 (6 rows x 2 halves,
 // row r at LDS byte lds + 4096 r, half h at + 256 h), M0 saved once.
 __device__ __forceinline__ void dma_rows6(const float *const (&g)[12], unsigned lds) {
@@ -908,14 +529,13 @@ __device__ __forceinline__ void dma_rows6(const float *const (&g)[12], unsigned 
                  : "memory");
 }
 
-// k_zf_mfma_lds with 8 waves (512 threads) per workgroup: MB = 4 MPW rows of
+// The LDS-fed MFMA GEMM with 8 waves (512 threads) per workgroup: MB = 4 MPW rows of
 // A and SB = 4 SG symbols per step, every wave keeping MPW x SG x 4 = 128
 // accumulators so that two waves share each SIMD.  Wave w computes
 // subcarriers 16 (w & 3) + b of the block for row pairs MPW (w >> 2) .. + MPW-1
 // and stages rows w + 8 r of every step (the first MB / 8 of them A rows).
-// <4, 8>: the 16-row A tile is staged once per 32 symbols (half the re-reads
-// of k_zf_mfma_lds); <8, 4>: 32-row tiles, so at M = 32 every input row is
-// staged once instead of once per 16-row block.
+// <8, 4>: 32-row tiles, so at M = 32 every input row is staged once instead
+// of once per 16-row block.
 template <int MPW, int SG, bool CONJ>
 __global__ void __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(2, 2)))
 k_zf_mfma_lds8(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__restrict__ in, int N, int M,
@@ -1080,7 +700,7 @@ __device__ __forceinline__ void dma_rows4x4(const float *const (&g)[16], unsigne
                  : "memory");
 }
 
-// k_zf_mfma_lds with 128-subcarrier blocks (k_zf_mfma_w128): 8 waves, wave w
+// The LDS-fed MFMA GEMM with 128-subcarrier blocks (k_zf_mfma_w128): 8 waves, wave w
 // computes subcarriers 16 w + b of the block (16 rows x 16 symbols, 128
 // accumulators, 2 waves/SIMD), so every staged row piece is 1 KiB of a row
 // instead of 512 B (the no-MAC diagnostic showed the staging, not the MACs,
@@ -1212,7 +832,7 @@ k_zf_mfma_w128(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__
 // then stream the input straight from HBM -- each wave its own 16 symbols
 // per step, so no input is shared and nothing but the input and output
 // crosses the memory system per symbol.  Lane (b, i) = block b = subcarrier
-// k0 + b, as k_zf_mfma; A operands from LDS ([n][16 rows][16 subcarriers],
+// k0 + b, as in the MFMA scheme above; A operands from LDS ([n][16 rows][16 subcarriers],
 // rows >= M zero), input operands from global memory, prefetched PD n-steps
 // ahead in registers.  PD = 2: same-process A/B at R = 64, 10 000 symbols,
 // bit-identical (profiles/r3/r3z6_zf_detect_prefetch_depth.jsonl): detect
@@ -1479,7 +1099,7 @@ hipError_t launch_zf_transpose(const float2 *W, int U, int R, int K, float2 *Wt,
 
 namespace {
 
-template <int MT, int ST, int MG, bool CONJ, bool PF>
+template <int MT, int ST, int MG, bool CONJ, bool PF = true>
 hipError_t gemm_launch(const float2 *Wt, int a_m, int a_n, const float2 *in, int N, int M, int K,
                        long long nsym, float2 *out, hipStream_t s) {
     constexpr int SBLK = (4 / MG) * ST;
@@ -1500,16 +1120,10 @@ hipError_t gemm_launch(const float2 *Wt, int a_m, int a_n, const float2 *in, int
 template <int MT, int MG, bool CONJ>
 hipError_t gemm_variant(const float2 *Wt, int a_m, int a_n, const float2 *in, int N, int M, int K,
                         long long nsym, float2 *out, hipStream_t s) {
-#ifdef OFDM_AB_KNOBS  // ZF_ST=4: 4 symbols per register tile; ZF_PF=0: no register double buffering
-    const bool st4 = ab_knob("ZF_ST", 8) == 4, pf = ab_knob("ZF_PF", 1) != 0;
-    if (st4) return pf ? gemm_launch<MT, 4, MG, CONJ, true>(Wt, a_m, a_n, in, N, M, K, nsym, out, s)
-                       : gemm_launch<MT, 4, MG, CONJ, false>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-    if (!pf) return gemm_launch<MT, 8, MG, CONJ, false>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-#endif
-    return gemm_launch<MT, 8, MG, CONJ, true>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+    return gemm_launch<MT, 8, MG, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
 }
 
-template <int MG, bool CONJ, bool DMA, int ST = 8>
+template <int MG, bool CONJ, int ST = 8>
 hipError_t gemm_lds_launch(const float2 *Wt, int a_m, int a_n, const float2 *in, int N, int M, int K,
                            long long nsym, float2 *out, hipStream_t s) {
     constexpr int SB = (4 / MG) * ST;
@@ -1521,29 +1135,6 @@ hipError_t gemm_lds_launch(const float2 *Wt, int a_m, int a_n, const float2 *in,
     if (chunk_steps < 4) chunk_steps = 4;
     nchunk = (nsteps + chunk_steps - 1) / chunk_steps;
     const long long blocks = 8LL * tpx * nchunk;
-#ifdef OFDM_AB_KNOBS
-    if constexpr (ST == 4) {  // 8x4 tiles, one n per LDS chunk, 4 waves/SIMD
-        hipLaunchKernelGGL((zf::k_zf_gemm_lds<MG, CONJ, false, 4, 1>), dim3((unsigned)blocks), dim3(256), 0, s,
-                           Wt, a_m, a_n, in, N, M, K, nsym, out, ntile, tpx, nkb, chunk_steps);
-        return hipGetLastError();
-    } else if constexpr (DMA) {
-        hipLaunchKernelGGL((zf::k_zf_gemm_dma<MG, CONJ>), dim3((unsigned)blocks), dim3(256), 0, s, Wt, a_m,
-                           a_n, in, N, M, K, nsym, out, ntile, tpx, nkb, chunk_steps);
-        return hipGetLastError();
-    } else {
-        if (ab_knob("ZF_XMAP", 0)) {
-            const long long nc8 = (nchunk + 7) / 8 * 8;  // one chunk per XCD per round; empty chunks return
-            hipLaunchKernelGGL((zf::k_zf_gemm_lds<MG, CONJ, false, 8, 2, true>), dim3((unsigned)(ntile * nc8)),
-                               dim3(256), 0, s, Wt, a_m, a_n, in, N, M, K, nsym, out, ntile, tpx, nkb, chunk_steps);
-            return hipGetLastError();
-        }
-        if (ab_knob("ZF_NT", 0)) {  // nontemporal input stream
-            hipLaunchKernelGGL((zf::k_zf_gemm_lds<MG, CONJ, true>), dim3((unsigned)blocks), dim3(256), 0, s, Wt,
-                               a_m, a_n, in, N, M, K, nsym, out, ntile, tpx, nkb, chunk_steps);
-            return hipGetLastError();
-        }
-    }
-#endif
     hipLaunchKernelGGL((zf::k_zf_gemm_lds<MG, CONJ>), dim3((unsigned)blocks), dim3(256), 0, s, Wt, a_m,
                        a_n, in, N, M, K, nsym, out, ntile, tpx, nkb, chunk_steps);
     return hipGetLastError();
@@ -1574,60 +1165,6 @@ hipError_t apply_ws16_launch(const float2 *Wt, const float2 *X, int U, int R, in
     return hipGetLastError();
 }
 
-#ifdef OFDM_AB_KNOBS
-template <int MP, int SG, bool CONJ>
-hipError_t mfma_launch(const float2 *Wt, int a_m, int a_n, const float2 *in, int N, int M, int K,
-                       long long nsym, float2 *out, hipStream_t s) {
-    constexpr int SBLK = 16 * SG;
-    const int nkb = (K + 15) / 16, nmb = (M + 2 * MP - 1) / (2 * MP);
-    const int ntile = nkb * nmb, tpx = (ntile + 7) / 8;
-    const long long nsteps = (nsym + SBLK - 1) / SBLK;
-    long long nchunk = (2048 + 8LL * tpx - 1) / (8LL * tpx);
-    long long chunk_steps = (nsteps + nchunk - 1) / nchunk;
-    if (chunk_steps < 2) chunk_steps = 2;
-    nchunk = (nsteps + chunk_steps - 1) / chunk_steps;
-    const long long blocks = 8LL * tpx * nchunk;
-    if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((zf::k_zf_mfma<MP, SG, CONJ>), dim3((unsigned)blocks), dim3(256), 0, s, Wt, a_m, a_n, in,
-                       N, M, K, nsym, out, ntile, tpx, nkb, chunk_steps);
-    return hipGetLastError();
-}
-
-template <bool CONJ>
-hipError_t mfma_dispatch(const float2 *Wt, int a_m, int a_n, const float2 *in, int N, int M, int K,
-                         long long nsym, float2 *out, hipStream_t s) {
-    // OFDM_ZF_SG: symbol quads per wave (2, 4 or 8)
-    const int sg = ab_knob("ZF_SG", 4);
-    if (M <= 4) return mfma_launch<2, 8, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-    if (M <= 8) return mfma_launch<4, 8, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-    if (sg == 8) return mfma_launch<8, 8, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-    if (sg == 2) return mfma_launch<8, 2, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-    return mfma_launch<8, 4, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-}
-
-template <int SG, bool CONJ>
-hipError_t mfma_lds_launch(const float2 *Wt, int a_m, int a_n, const float2 *in, int N, int M, int K,
-                           long long nsym, float2 *out, hipStream_t s) {
-    constexpr int SB = 4 * SG;
-    constexpr size_t lds = (size_t)4 * (16 + SB) * 64 * sizeof(float2);
-    const int nkb = (K + 63) / 64, nmb = (M + 15) / 16;
-    const int ntile = nkb * nmb, tpx = (ntile + 7) / 8;
-    const long long nsteps = (nsym + SB - 1) / SB;
-    long long nchunk = (2048 + 8LL * tpx - 1) / (8LL * tpx);
-    long long chunk_steps = (nsteps + nchunk - 1) / nchunk;
-    if (chunk_steps < 2) chunk_steps = 2;
-    nchunk = (nsteps + chunk_steps - 1) / chunk_steps;
-    const long long blocks = 8LL * tpx * nchunk;
-    if (blocks > 0x7fffffffLL) return hipErrorInvalidValue;
-    auto kern = zf::k_zf_mfma_lds<SG, CONJ>;
-    if (lds > 64 * 1024)
-        if (hipError_t e = opt_in_lds(reinterpret_cast<const void *>(kern), (int)lds); e != hipSuccess) return e;
-    hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), lds, s, Wt, a_m, a_n, in, N, M, K, nsym, out,
-                       ntile, tpx, nkb, chunk_steps);
-    return hipGetLastError();
-}
-
-#endif  // OFDM_AB_KNOBS
 
 template <int MPW, int SG, bool CONJ>
 hipError_t mfma_lds8_launch(const float2 *Wt, int a_m, int a_n, const float2 *in, int N, int M, int K,
@@ -1705,47 +1242,23 @@ hipError_t wstat_launch(const float2 *Wt, int a_m, int a_n, const float2 *in, in
 //   otherwise the LDS VALU kernel when both operands are wide enough (at
 //     N = 4 its per-chunk barriers and stores dominate), else the register-
 //     tiled one.
-// The A/B build (OFDM_AB_KNOBS) also reaches the measured-slower candidates
-// through OFDM_AB_ZF_LDS: 0 register tiles, 1 LDS VALU, 2 DMA-fed LDS, 3
-// MFMA from L1, 4 MFMA through LDS, 5/6 8-wave MFMA (16x32 / 32x16 tiles), 7
-// 128-subcarrier MFMA, 8/9 W-stationary (9: one symbol chunk per XCD), 10
-// W-stationary with 64-row tiles.
+// Measured-slower candidates (register tiles without double buffering,
+// DMA-fed LDS VALU tiles, MFMA from L1 / through 4-wave LDS tiles, other
+// W-stationary depths and tile heights) are kept out of the product sources
+// (scripts/experiments/ab_knobs_r3.patch).
+enum { ZF_REG = 0, ZF_LDS = 1, ZF_MFMA_LDS8 = 6, ZF_MFMA_W128 = 7, ZF_WSTAT = 9 };
 template <bool CONJ>
 hipError_t gemm_dispatch(const float2 *Wt, int a_m, int a_n, const float2 *in, int N, int M, int K,
                          long long nsym, float2 *out, hipStream_t s) {
-    const int wdef = CONJ ? (N < 8 ? 1 : M <= 8 ? 0 : N <= 72 ? 9 : M > 16 ? 6 : 7) : (N >= 32 && N <= 72 ? 9 : 1);
-    const int mode = ab_knob("ZF_LDS", wdef);
-    if (mode == 9 && N <= 72) return wstat_launch<CONJ, true>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-    if (mode == 6) return mfma_lds8_launch<8, 4, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-    if (mode == 7) return mfma_w128_launch<CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-#ifdef OFDM_AB_KNOBS
-    if (mode == 3) return mfma_dispatch<CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-    if (mode == 5) return mfma_lds8_launch<4, 8, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-    if (mode == 8 && N <= 72) return wstat_launch<CONJ, false>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-    if (mode == 10 && N <= 18) return wstat_launch<CONJ, true, 64>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-    // input prefetch depth of the W-stationary kernel: 11 PD = 5, 13 PD = 3, 14 PD = 1 (default 2)
-    if (mode == 11 && N <= 72) return wstat_launch<CONJ, true, 16, 5>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-    if (mode == 13 && N <= 72) return wstat_launch<CONJ, true, 16, 3>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-    if (mode == 14 && N <= 72) return wstat_launch<CONJ, true, 16, 1>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-    if (mode == 4) {
-        if (ab_knob("ZF_SG", 4) == 8) return mfma_lds_launch<8, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-        return mfma_lds_launch<4, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-    }
-    if (M > 4 && N >= 8 && mode == 2) {
-        if (M <= 8) return gemm_lds_launch<1, CONJ, true>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-        if (M <= 16) return gemm_lds_launch<2, CONJ, true>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-        return gemm_lds_launch<4, CONJ, true>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-    }
-    if (M > 4 && N >= 8 && mode == 1 && ab_knob("ZF_ST", 8) == 4) {
-        if (M <= 8) return gemm_lds_launch<1, CONJ, false, 4>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-        if (M <= 16) return gemm_lds_launch<2, CONJ, false, 4>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-        return gemm_lds_launch<4, CONJ, false, 4>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-    }
-#endif
-    if (M > 4 && N >= 8 && mode != 0) {
-        if (M <= 8) return gemm_lds_launch<1, CONJ, false>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-        if (M <= 16) return gemm_lds_launch<2, CONJ, false>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
-        return gemm_lds_launch<4, CONJ, false>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+    const int mode = CONJ ? (N < 8 ? ZF_LDS : M <= 8 ? ZF_REG : N <= 72 ? ZF_WSTAT : M > 16 ? ZF_MFMA_LDS8 : ZF_MFMA_W128)
+                          : (N >= 32 && N <= 72 ? ZF_WSTAT : ZF_LDS);
+    if (mode == ZF_WSTAT && N <= 72) return wstat_launch<CONJ, true>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+    if (mode == ZF_MFMA_LDS8) return mfma_lds8_launch<8, 4, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+    if (mode == ZF_MFMA_W128) return mfma_w128_launch<CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+    if (M > 4 && N >= 8 && mode != ZF_REG) {
+        if (M <= 8) return gemm_lds_launch<1, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+        if (M <= 16) return gemm_lds_launch<2, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
+        return gemm_lds_launch<4, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
     }
     if (M <= 2) return gemm_variant<2, 1, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
     if (M <= 4) return gemm_variant<4, 1, CONJ>(Wt, a_m, a_n, in, N, M, K, nsym, out, s);
@@ -1760,23 +1273,6 @@ hipError_t gemm_dispatch(const float2 *Wt, int a_m, int a_n, const float2 *in, i
 hipError_t launch_zf_apply(const float2 *Wt, const float2 *X, int U, int R, int K, long long nsym,
                            float2 *Y, hipStream_t s) {
     if (K == 0 || nsym == 0) return hipSuccess;
-#ifdef OFDM_AB_KNOBS
-    switch (ab_knob("ZF_A16", 0)) {  // W-stationary 16-B lane tiles <MT, RG, ST, NW>, target groups; -1: round-2 kernels
-        case -1: return gemm_dispatch<false>(Wt, 1, R, X, U, R, K, nsym, Y, s);
-        case 3: if (K >= 2 && U <= 20) return apply_ws16_launch<8, 1, 4, 8>(Wt, X, U, R, K, nsym, Y, 32, s); break;
-        case 5: if (K >= 2 && U <= 20) return apply_ws16_launch<8, 1, 2, 16>(Wt, X, U, R, K, nsym, Y, 32, s); break;
-        case 6: if (K >= 2 && U <= 20) return apply_ws16_launch<8, 1, 2, 16>(Wt, X, U, R, K, nsym, Y, 64, s); break;
-        case 7: if (K >= 2 && U <= 10) return apply_ws16_launch<8, 2, 2, 16>(Wt, X, U, R, K, nsym, Y, 64, s); break;
-        case 10: if (K >= 2 && U <= 20) return apply_ws16_launch<8, 1, 4, 8, 1>(Wt, X, U, R, K, nsym, Y, 64, s); break;
-        case 11: if (K >= 2 && U <= 20) return apply_ws16_launch<8, 1, 4, 8, 2>(Wt, X, U, R, K, nsym, Y, 64, s); break;
-        case 12: if (K >= 2 && U <= 20) return apply_ws16_launch<8, 1, 4, 8, 1>(Wt, X, U, R, K, nsym, Y, 128, s); break;
-        case 9: if (K >= 2 && U <= 40) return apply_ws16_launch<4, 1, 4, 16>(Wt, X, U, R, K, nsym, Y, 32, s); break;
-        case 13: if (K >= 2 && U <= 40) return apply_ws16_launch<4, 1, 8, 8, 1>(Wt, X, U, R, K, nsym, Y, 32, s); break;
-        case 14: if (K >= 2 && U <= 40) return apply_ws16_launch<4, 1, 8, 8, 0>(Wt, X, U, R, K, nsym, Y, 32, s); break;
-        case 15: if (K >= 2 && U <= 20) return apply_ws16_launch<8, 1, 4, 8, 0>(Wt, X, U, R, K, nsym, Y, 64, s); break;
-        default: break;
-    }
-#endif
     // 16-B lanes, W-stationary (k_zf_apply_ws16): 8-row tiles up to U = 20
     // (W tile U x 8 KiB of LDS), 4-row tiles with 8-symbol steps up to U = 40;
     // same-process A/B at R = 64, K = 1023, 10 000 symbols:

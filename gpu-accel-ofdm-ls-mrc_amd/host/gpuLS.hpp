@@ -185,6 +185,16 @@ class gpuLS {
     // MRC + normalise + rotate launch (ofdm_symbols_demod) on the staging
     // buffer against the kept estimate, one synchronising copy of the K
     // outputs.  Otherwise FFT rows in Y, then MRC from Hconj / Hsqrd.
+    // Contract of the fused path: it demodulates against the workspace copy
+    // of the estimate firstVector exported, NOT what Hconj / Hsqrd hold now.
+    // A caller that edits them in place after firstVector (smoothing,
+    // interpolation, another estimate copied in) calls estimateChanged()
+    // first; the next demodOneSymbol then reads Hconj / Hsqrd as the
+    // reference does (gpuLS.cu:410-473).
+    void estimateChanged() {
+        est_H_ = nullptr;
+        est_P_ = nullptr;
+    }
     void demodOneSymbol(hipFloatComplex *dY, hipFloatComplex *Y, hipFloatComplex *Hconj,
                         float *Hsqrd, int rows1, int cols1, int it) {
         const int K = cols1 - 1;

@@ -17,11 +17,9 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-# OFDM_LSMRC_LIB=ab selects the A/B build (make ab: lib/libofdm_lsmrc_ab.so,
-# experiment switches read from OFDM_AB_* variables) for scripts/ comparisons;
-# the product library has no switches.
-# (any other value <v>: lib/libofdm_lsmrc_<v>.so, a build of the same sources with
-# other compiler options, scripts/libab.py).
+# OFDM_LSMRC_LIB=<v> loads lib/libofdm_lsmrc_<v>.so instead, a build of
+# experiment sources for scripts/ comparisons (scripts/libab.py); the product
+# library has no switches.
 _LIBSEL = os.environ.get("OFDM_LSMRC_LIB", "")
 LIB_PATH = os.path.join(HERE, "lib", f"libofdm_lsmrc_{_LIBSEL}.so" if _LIBSEL else "libofdm_lsmrc.so")
 HEADER_PATH = os.path.join(os.path.dirname(HERE), "include", "ofdm_lsmrc.h")
@@ -49,6 +47,7 @@ _SIGS = {
     "ofdm_frame_workspace_bytes": (_c.c_size_t, [_LL, _I, _I, _I]),
     "ofdm_workspace_release": (_I, [_P]),
     "ofdm_frame_demod": (_I, [_P, _LL, _I, _I, _I, _I, _P, _P, _c.c_size_t, _P, _P]),
+    "ofdm_frame_demod_ex": (_I, [_P, _LL, _I, _I, _I, _I, _P, _P, _c.c_size_t, _P, _I, _LL, _P]),
     "ofdm_frame_estimate": (_I, [_P, _LL, _I, _I, _I, _I, _P, _P, _c.c_size_t, _P]),
     "ofdm_frame_combine": (_I, [_P, _LL, _I, _I, _I, _I, _P, _c.c_size_t, _P, _P]),
     "ofdm_frame_demod_freq": (_I, [_P, _LL, _I, _I, _I, _P, _P, _c.c_size_t, _P, _P]),
@@ -254,16 +253,26 @@ def workspace_release(ws):
     lib().ofdm_workspace_release(_c.c_void_p(ptr))
 
 
-def frame_demod(iq, X, prefix=0, ws=None, out=None, stream=None):
-    """iq: (F, S, R, C+prefix) time domain -> (F, S-1, K)."""
+FLOW_AUTO, FLOW_TWO_LAUNCH = 0, 1  # OFDM_FLOW_* of ofdm_frame_demod_ex
+
+
+def frame_demod(iq, X, prefix=0, ws=None, out=None, stream=None, flow=None, spin_ticks=None):
+    """iq: (F, S, R, C+prefix) time domain -> (F, S-1, K).  flow / spin_ticks:
+    ofdm_frame_demod_ex's scheduling choices (default: ofdm_frame_demod's)."""
     F, S, R, Cp = iq.shape
     C = Cp - prefix
     if ws is None:
         ws = workspace(F, S, R, C, iq.device)
     if out is None:
         out = c64((F, S - 1, C - 1), iq.device)
-    _check(lib().ofdm_frame_demod(_dptr(iq), F, S, R, C, prefix, _dptr(X), _dptr(ws), ws.numel(),
-                                  _dptr(out), _stream(stream)), "ofdm_frame_demod")
+    if flow is None and spin_ticks is None:
+        _check(lib().ofdm_frame_demod(_dptr(iq), F, S, R, C, prefix, _dptr(X), _dptr(ws), ws.numel(),
+                                      _dptr(out), _stream(stream)), "ofdm_frame_demod")
+    else:
+        _check(lib().ofdm_frame_demod_ex(_dptr(iq), F, S, R, C, prefix, _dptr(X), _dptr(ws), ws.numel(),
+                                         _dptr(out), FLOW_AUTO if flow is None else flow,
+                                         -1 if spin_ticks is None else spin_ticks, _stream(stream)),
+               "ofdm_frame_demod_ex")
     return out
 
 

@@ -166,6 +166,24 @@ int ofdm_frame_demod(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int
                      const ofdm_cf32 *d_X, void *d_ws, size_t ws_bytes, ofdm_cf32 *d_out,
                      ofdm_stream_t stream);
 
+/* ofdm_frame_demod with its two scheduling choices exposed (same results,
+ * same workspace contract):
+ *   flow        OFDM_FLOW_AUTO (what ofdm_frame_demod does) or
+ *               OFDM_FLOW_TWO_LAUNCH (estimate, then combine, as two launches
+ *               on the stream, at every C);
+ *   spin_ticks  one-launch path (C = 1024): how long, in ticks of the 100 MHz
+ *               device clock, an MRC workgroup waits for the estimate of a
+ *               frame it reads before it estimates that frame itself (the
+ *               same code and bytes as the estimator workgroup); < 0 = the
+ *               default (200 000 = 2 ms), 0 = never wait.  The result does
+ *               not depend on it; a shared GPU that delays the estimator
+ *               workgroups only trades the wait for a re-estimate. */
+#define OFDM_FLOW_AUTO 0
+#define OFDM_FLOW_TWO_LAUNCH 1
+int ofdm_frame_demod_ex(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, int cp_len,
+                        const ofdm_cf32 *d_X, void *d_ws, size_t ws_bytes, ofdm_cf32 *d_out, int flow,
+                        long long spin_ticks, ofdm_stream_t stream);
+
 /* The two stages of ofdm_frame_demod, for callers that pipeline or time them
  * separately: ofdm_frame_estimate FFTs the pilot symbol of every frame and
  * stores the LS estimate (Hconj, |H|^2) in d_ws (gpuLS::firstVector,

@@ -177,3 +177,88 @@ def test_frame_sharded_bench_two_ranks(tmp_path):
     line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["config"]["global_data_symbols"] == 2 * 24 * 100
     assert line["check"]["qpsk_symbol_errors"] == 0
+
+
+def test_eight_shards_c4096_one_gpu_vs_oracle(ofdm, oracle, dev):
+    """configs[4]'s split emulated on one GPU: 256 antennas as 8 shards of 32
+    at C = 4096.  Each shard runs the HIP partial kernels
+    (ofdm_frame_ls_partial / ofdm_frame_mrc_partial); the partial |H|^2 and
+    numerators are summed over the shards in rank order (what all_reduce and
+    reduce_scatter compute) and finalised by ofdm_mrc_finalize.  Reference:
+    the oracle on all 256 antennas (findDistSqrd / matrixMultThenSum over
+    every antenna, cpuLS.hpp:187-228)."""
+    import torch
+    F, S, G, Rg, C = 2, 4, 8, 32, 4096
+    K = C - 1
+    rng = np.random.default_rng(256)
+    a = np.float32(0.70710678)
+    X = torch.from_numpy((rng.choice([-a, a], K) + 1j * rng.choice([-a, a], K)).astype(np.complex64)).to(dev)
+    iq = ofdm.synth_frames(F, S, G * Rg, C, X, seed=41, noise_std=0.02)
+    P = torch.zeros((F, K), dtype=torch.float32, device=dev)
+    num = torch.zeros((F, S - 1, K), dtype=torch.complex64, device=dev)
+    for g in range(G):
+        shard = iq[:, :, g * Rg:(g + 1) * Rg].contiguous()
+        Pg, ws = ofdm.frame_ls_partial(shard, X)
+        P += Pg
+        num += ofdm.frame_mrc_partial(shard, ws)
+    out = ofdm.c64((F, S - 1, K), dev)
+    ofdm.mrc_finalize(num.reshape(-1), 0, S - 1, K, P, out)
+    torch.cuda.synchronize()
+    ref = oracle.frames_demod(iq.cpu().numpy(), X.cpu().numpy(), 0, nthreads=8)
+    parity(out.cpu().numpy(), ref)
+    assert int(ofdm.count_symbol_errors(out, S, seed=41).item()) == 0
+
+
+def _bench(args, share, timeout=300):
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT", "OFDM_BENCH_SHARE_GPU", "OFDM_BENCH_BACKEND"):
+        env.pop(k, None)
+    if share:
+        env.update(OFDM_BENCH_SHARE_GPU="1", OFDM_BENCH_BACKEND="gloo")
+    return subprocess.run([sys.executable, os.path.join(root, "bench.py")] + args, capture_output=True,
+                          text=True, timeout=timeout, env=env, cwd=root)
+
+
+def _line(r):
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return __import__("json").loads(lines[0])
+
+
+@pytest.mark.timeout(400)
+def test_bench_gpus2_launches_two_ranks_itself():
+    """`python bench.py --gpus 2` with no torchrun starts its two ranks
+    itself (here sharing cuda:0 over gloo): n_gpus = 2, both ranks' frames
+    counted, the timed output identical to the warm-up's."""
+    line = _line(_bench(["--gpus", "2", "--frames", "24", "--steps", "2", "--warmup", "1", "--no-cpu"], True))
+    assert line["n_gpus"] == 2 and line["config"]["global_data_symbols"] == 2 * 24 * 100
+    assert line["check"]["qpsk_symbol_errors"] == 0 and line["check"]["timed_equals_warmup"] is True
+
+
+@pytest.mark.timeout(200)
+def test_bench_gpus2_refuses_on_one_gpu():
+    """Asked for more GPUs than are visible, bench.py exits non-zero instead
+    of measuring fewer."""
+    import torch
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("more than one GPU visible")
+    r = _bench(["--gpus", "2", "--frames", "8", "--steps", "1", "--warmup", "1", "--no-cpu"], False)
+    assert r.returncode != 0 and not [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert "refusing" in r.stderr
+
+
+@pytest.mark.timeout(600)
+def test_bench_split_eight_ranks_share_gpu():
+    """bench.py --mode split at configs[4]'s split (8 ranks x 32 antennas =
+    256, C = 4096), the 8 ranks sharing cuda:0 over gloo: the gathered output
+    of the timed steps matches the single-GPU receiver on all 256 antennas
+    (check.vs_full_receiver, 1e-5)."""
+    line = _line(_bench(["--mode", "split", "--gpus", "8", "--frames", "4", "--S", "5", "--chunk", "2",
+                         "--steps", "1", "--warmup", "1", "--no-cpu"], True, timeout=560))
+    assert line["n_gpus"] == 8 and line["config"]["R_total"] == 256 and line["config"]["C"] == 4096
+    chk = line["check"]
+    assert chk["qpsk_symbol_errors"] == 0 and chk["vs_full_receiver"]["ok"], chk

@@ -23,17 +23,13 @@ def test_library_exports_header(ofdm):
 
 def test_product_library_reads_no_environment(ofdm):
     """The shipped library has no experiment switches: it does not even import
-    getenv (the A/B build, lib/libofdm_lsmrc_ab.so, is the one that does)."""
+    getenv."""
     import subprocess
     path = ofdm.LIB_PATH
-    if path.endswith("_ab.so"):
-        pytest.skip("OFDM_LSMRC_LIB=ab selects the A/B build")
+    if os.environ.get("OFDM_LSMRC_LIB"):
+        pytest.skip("OFDM_LSMRC_LIB selects an experiment build")
     syms = subprocess.run(["nm", "-D", "--undefined-only", path], capture_output=True, text=True, check=True).stdout
     assert "getenv" not in syms, "the product library must not read environment variables"
-    ab = os.path.join(os.path.dirname(path), "libofdm_lsmrc_ab.so")
-    if os.path.exists(ab):
-        syms = subprocess.run(["nm", "-D", "--undefined-only", ab], capture_output=True, text=True, check=True).stdout
-        assert "getenv" in syms
 
 
 def test_pilot_rotate_matches_oracle(ofdm, oracle):
@@ -117,19 +113,28 @@ def test_workspace_registry_without_device(ofdm):
 
 def test_product_library_dispatches_only_product_kernels(ofdm):
     """Measured-and-dropped candidates live in scripts/experiments, not in the
-    shipped library: no wave-quad C = 4096 receiver and no register-FFT test
-    kernel."""
+    shipped library or its sources: no wave-quad C = 4096 receiver, no
+    register-FFT test kernel, no one-launch C = 2048 /
+    4096 demod, no A/B-only ZF GEMMs and no experiment-switch build at all
+    (VERDICT r3 item 7)."""
+    import glob
     import subprocess
     path = ofdm.LIB_PATH
-    if path.endswith("_ab.so"):
-        pytest.skip("OFDM_LSMRC_LIB=ab selects the A/B build")
+    if os.environ.get("OFDM_LSMRC_LIB"):
+        pytest.skip("OFDM_LSMRC_LIB selects an experiment build")
     syms = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True,
                           check=True).stdout
-    for bad in ("td4096r", "rfft"):
+    for bad in ("td4096r", "rfft", "k_demod_td2048", "k_demod_td4096", "k_zf_gemm_dma", "k_zf_mfmaILi",
+                "k_zf_mfma_ldsILi"):
         assert bad not in syms, f"{bad} kernel in the product library"
-    mk = open(os.path.join(os.path.dirname(os.path.dirname(path)), "Makefile")).read()
+    pkg = os.path.dirname(os.path.dirname(path))
+    mk = open(os.path.join(pkg, "Makefile")).read()
     srcs = [l for l in mk.splitlines() if l.startswith("SRCS_HIP")][0]
     assert "td4096r" not in srcs and "rfft" not in srcs
+    assert "OFDM_AB_KNOBS" not in mk
+    for src in glob.glob(os.path.join(pkg, "csrc", "*")):
+        text = open(src).read()
+        assert "OFDM_AB_KNOBS" not in text and "ab_knob(" not in text, src
 
 
 def test_workspace_sizes(ofdm):

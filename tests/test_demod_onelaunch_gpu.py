@@ -1,21 +1,18 @@
 """The one-launch frame demod (k_demod_td1024: estimator workgroups publish
 each frame's estimate to the MRC workgroups of the same grid through the
-workspace's flag words; k_demod_td2048 / 4096 in the A/B build only).
+workspace's flag words).
 ofdm_frame_demod at C = 1024 takes this path;
 these tests hold it to the two-launch flow (ofdm_frame_estimate +
 ofdm_frame_combine, itself tested against the oracle in test_gpu_parity.py)
 and to the oracle, on shapes with straddling workgroups (8 symbols spanning
 two frames) and tail waves, on a reused workspace with new data (the flags
 of the previous launch must not release the next one), and with the bounded
-wait forced to expire (A/B build: every MRC workgroup estimates its frames
-itself).  Tolerance: helpers.RTOL.  At C = 1024 the estimator sums |H|^2
-over antennas in the 8-wave order (rows w, w+8, ... per wave, then waves in
-order), the two-launch LS in its own wave order, so the outputs agree to
-rounding, not bit for bit; at C = 2048 / 4096 (A/B build) the estimator is
-the LS kernel's own code and the outputs are bit-identical."""
+wait forced to expire (ofdm_frame_demod_ex spin_ticks = 0: every MRC
+workgroup estimates its frames itself).  Tolerance: helpers.RTOL.  The
+estimator sums |H|^2 over antennas in the 8-wave order (rows w, w+8, ...
+per wave, then waves in order), the two-launch LS in its own wave order, so
+the outputs agree to rounding, not bit for bit."""
 import os
-import subprocess
-import sys
 
 import numpy as np
 import pytest
@@ -166,37 +163,32 @@ def test_graph_capture_takes_two_launches(ofdm, dev):
     parity(host(out), two_launch(ofdm, a, X, 0))
 
 
-@pytest.mark.skipif(not os.path.exists(os.path.join(ROOT, "gpu-accel-ofdm-ls-mrc_amd", "lib",
-                                                    "libofdm_lsmrc_ab.so")),
-                    reason="A/B build (make -C gpu-accel-ofdm-ls-mrc_amd ab) not present")
-@pytest.mark.parametrize("C", [1024, 2048, 4096])
-def test_bounded_wait_fallback_ab_build(C):
-    """OFDM_AB_DEMOD_SPIN=0: no MRC workgroup waits for a flag; each
-    estimates its frame(s) itself.  Same outputs as the normal path, and the
-    one launch agrees with two (run in a child process on the A/B library)."""
-    code = r"""
-import os, sys, numpy as np, torch
-sys.path.insert(0, os.path.join(sys.argv[1], "gpu-accel-ofdm-ls-mrc_amd"))
-import ofdm_lsmrc as ofdm
-F, S, R, C = 9, 13, 16, int(sys.argv[2])
-a = np.float32(0.70710678); rng = np.random.default_rng(5)
-X = torch.from_numpy((rng.choice([-a, a], C - 1) + 1j * rng.choice([-a, a], C - 1)).astype(np.complex64)).cuda()
-iq = ofdm.synth_frames(F, S, R, C, X, seed=11, noise_std=0.01)
-os.environ["OFDM_AB_DEMOD_FUSED"] = "0"
-two = ofdm.frame_demod(iq, X).cpu().numpy()
-os.environ.pop("OFDM_AB_DEMOD_FUSED")
-ref = ofdm.frame_demod(iq, X).cpu().numpy()
-os.environ["OFDM_AB_DEMOD_SPIN"] = "0"
-got = ofdm.frame_demod(iq, X).cpu().numpy()
-d = np.abs(got - ref).max() / np.abs(ref).max()
-d2 = np.abs(ref - two).max() / np.abs(two).max()
-print("maxrel fallback vs one launch", d, "one launch vs two", d2)
-ok = d <= 1e-6 and d2 <= 1e-5 and (C == 1024 or d2 == 0)
-sys.exit(0 if ok else 1)
-"""
-    # C = 2048 / 4096: the one-launch kernels of the A/B build (OFDM_AB_DEMOD_WIDE;
-    # no faster than two launches, not in the product), bit-identical to two launches
-    env = dict(os.environ, OFDM_LSMRC_LIB="ab", OFDM_AB_DEMOD_WIDE="1")
-    p = subprocess.run([sys.executable, "-c", code, ROOT, str(C)], env=env, capture_output=True, text=True,
-                       timeout=300)
-    assert p.returncode == 0, p.stdout + p.stderr
+@pytest.mark.parametrize("F,S,R", [(9, 13, 16), (3, 101, 64), (20, 5, 4)])
+def test_bounded_wait_fallback(ofdm, dev, F, S, R):
+    """ofdm_frame_demod_ex with spin_ticks = 0: no MRC workgroup waits for a
+    flag; each estimates the frame(s) it reads itself, through the same
+    hlds_ls_frame call site as the estimator workgroups.  The output must be
+    bit-identical to the default one-launch path's (same code, same bytes),
+    and within rounding of the two-launch flow (different FFT kernels)."""
+    import torch
+    C = 1024
+    rng = np.random.default_rng(5 + R)
+    a = np.float32(0.70710678)
+    X = torch.from_numpy((rng.choice([-a, a], C - 1) + 1j * rng.choice([-a, a], C - 1))
+                         .astype(np.complex64)).to(dev)
+    iq = ofdm.synth_frames(F, S, R, C, X, seed=11, noise_std=0.01)
+    ref = ofdm.frame_demod(iq, X)
+    got = ofdm.frame_demod(iq, X, spin_ticks=0)
+    two = ofdm.frame_demod(iq, X, flow=ofdm.FLOW_TWO_LAUNCH)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+    parity(host(ref), host(two), rtol=1e-6)
+    assert int(ofdm.count_symbol_errors(got, S, seed=11).item()) == 0
+
+
+def test_frame_demod_ex_rejects_unknown_flow(ofdm, dev):
+    import torch
+    X = torch.ones(1023, dtype=torch.complex64, device=dev)
+    iq = torch.zeros((1, 2, 1, 1024), dtype=torch.complex64, device=dev)
+    with pytest.raises(ofdm.OfdmError, match="flow=7"):
+        ofdm.frame_demod(iq, X, flow=7)

@@ -457,3 +457,25 @@ def test_symbols_demod_matches_frame_combine(ofdm, dev, C, prefix):
     ofdm.frame_estimate_freq(Y, X, wsf)
     with pytest.raises(ofdm.OfdmError, match="frequency-domain"):
         ofdm.symbols_demod(iq[0, 1:].contiguous(), wsf, prefix)
+
+
+@pytest.mark.parametrize("C,prefix", [(1024, 0), (2048, 4), (4096, 0)])
+def test_symbols_demod_never_reads_before_its_run(ofdm, dev, C, prefix):
+    """ofdm_symbols_demod hands the fused MRC kernels a frame base one symbol
+    BEFORE the caller's d_sym (their symbol 1 is d_sym[0]); the kernels must
+    never read that slot (the pilot's, in a real frame).  Here it is filled
+    with NaN inside the same allocation: any read of it would reach the
+    outputs.  Pins the invariant ADVICE r3 named (capi.cpp ofdm_symbols_demod)."""
+    import torch
+    F, S, R = 1, 6, 8
+    X = to_dev(qpsk_pilots(C - 1), dev)
+    iq = ofdm.synth_frames(F, S, R, C, X, prefix=prefix, seed=33, noise_std=0.02)
+    ws = ofdm.workspace(F, S, R, C, dev)
+    ofdm.frame_estimate(iq, X, prefix, ws)
+    ref = host(ofdm.frame_combine(iq, prefix, ws, ofdm.c64((F, S - 1, C - 1), dev)))
+    buf = torch.empty((S, R, C + prefix), dtype=torch.complex64, device=dev)
+    buf[0] = complex(float("nan"), float("nan"))
+    buf[1:] = iq[0, 1:]
+    got = host(ofdm.symbols_demod(buf[1:], ws, prefix, frame=0))
+    assert np.isfinite(got).all()
+    parity(got, ref[0], rtol=1e-6)
