@@ -44,37 +44,71 @@ __device__ __forceinline__ v2f sub_mi(v2f u, v2f v) {
     return r;
 }
 
-// a * b: t = (a.x b.x, a.x b.y); r = (a.y (-b.y) + t.x, a.y b.x + t.y)
+// Each multi-instruction form is ONE asm statement: hipcc pads one wait
+// state (s_nop 0, a 4-cycle issue slot) after an ;;#ASMEND whose outputs the
+// next instruction reads, so two statements chained through a temporary cost
+// a nop each time; VALU -> VALU needs no wait state inside the string.
+// a * b: r = (a.x b.x, a.x b.y); r += (a.y (-b.y), a.y b.x) -- the product
+// accumulated in the (early-clobber) result register itself, no temporary
+// (a temporary freed at ;;#ASMEND and reused by the next statement draws a
+// pad as well)
 __device__ __forceinline__ v2f cmul(v2f a, v2f b) {
-    v2f t, r;
-    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "v"(b));
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
-        : "=v"(r) : "v"(a), "v"(b), "v"(t));
+    v2f r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]\n\t"
+        "v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+        : "=&v"(r) : "v"(a), "v"(b));
     return r;
 }
 // a * w with a wave-uniform (compile-time) w held in an SGPR pair
 __device__ __forceinline__ v2f cmul_s(v2f a, v2f w) {
-    v2f t, r;
-    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "s"(w));
-    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
-        : "=v"(r) : "v"(a), "s"(w), "v"(t));
+    v2f r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]\n\t"
+        "v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+        : "=&v"(r) : "v"(a), "s"(w));
     return r;
 }
 // cmul_s that the compiler may not hoist out of a loop (a loop-invariant
 // twiddle set kept live across the loop costs two VGPRs per twiddle)
 __device__ __forceinline__ v2f cmul_s_v(v2f a, v2f w) {
-    v2f t, r;
-    asm volatile("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(t) : "v"(a), "s"(w));
-    asm volatile("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
-                 : "=v"(r) : "v"(a), "s"(w), "v"(t));
+    v2f r;
+    asm volatile("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1]\n\t"
+                 "v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+                 : "=&v"(r) : "v"(a), "s"(w));
     return r;
 }
 // acc += x * h
 __device__ __forceinline__ void mac(v2f &acc, v2f x, v2f h) {
-    asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[0,1,1]" : "+v"(acc) : "v"(x), "v"(h));
-    asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
+    asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[0,1,1]\n\t"
+        "v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
         : "+v"(acc) : "v"(x), "v"(h));
 }
+// v * (a * b): the twiddle a * b formed and applied in one statement
+// (twiddle generation chains: no pad between the product and its use)
+#define OFDM_PK_CMUL2(DST, A, B)                                                          \
+    "v_pk_mul_f32 " DST ", " A ", " B " op_sel_hi:[0,1]\n\t"                              \
+    "v_pk_fma_f32 " DST ", " A ", " B ", " DST " op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]\n\t"
+__device__ __forceinline__ v2f cmul3(v2f v, v2f a, v2f b) {
+    v2f ab, r;
+    asm(OFDM_PK_CMUL2("%1", "%2", "%3") OFDM_PK_CMUL2("%0", "%4", "%1")
+        : "=&v"(r), "=&v"(ab) : "v"(a), "v"(b), "v"(v));
+    return r;
+}
+// v * (a * w), w wave-uniform (SGPR pair); volatile as cmul_s_v
+__device__ __forceinline__ v2f cmul3_s_v(v2f v, v2f a, v2f w) {
+    v2f ab, r;
+    asm volatile(OFDM_PK_CMUL2("%1", "%2", "%3") OFDM_PK_CMUL2("%0", "%4", "%1")
+                 : "=&v"(r), "=&v"(ab) : "v"(a), "s"(w), "v"(v));
+    return r;
+}
+// radix-2 butterfly with a wave-uniform twiddle: (u + v w, u - v w)
+__device__ __forceinline__ void bfly_s(v2f &u, v2f &v, v2f w) {
+    v2f tv;
+    asm(OFDM_PK_CMUL2("%2", "%1", "%3")
+        "v_pk_add_f32 %1, %0, %2 neg_lo:[0,1] neg_hi:[0,1]\n\t"
+        "v_pk_add_f32 %0, %0, %2"
+        : "+v"(u), "+v"(v), "=&v"(tv) : "s"(w));
+}
+#undef OFDM_PK_CMUL2
 // (x, y) * s for a real s
 __device__ __forceinline__ v2f scale(v2f a, float s) { return a * (v2f){s, s}; }
 
@@ -105,9 +139,10 @@ __device__ __forceinline__ void fft_reg(v2f (&a)[N]) {
                 } else {
                     const int idx = k * (OFDM_TW_N / len);
                     const v2f w = {kTw.v[2 * idx], kTw.v[2 * idx + 1]};
-                    const v2f tv = cmul_s(v, w);
-                    a[i + k] = add(u, tv);
-                    a[i + k + half] = sub(u, tv);
+                    v2f uu = u, vv = v;
+                    bfly_s(uu, vv, w);
+                    a[i + k] = uu;
+                    a[i + k + half] = vv;
                 }
             }
         }
