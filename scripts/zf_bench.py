@@ -15,7 +15,6 @@ plain C, 1 thread) on a bounded sample."""
 import argparse
 import json
 import os
-os.environ.setdefault("OFDM_LSMRC_LIB", "ab")  # the A/B build: OFDM_AB_* switches
 import sys
 import time
 
@@ -47,7 +46,8 @@ def main():
     ap.add_argument("--nsym", type=int, default=10000)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--ab", action="store_true")
+    ap.add_argument("--ab", action="store_true",
+                    help="round 3's A/B build only (OFDM_LSMRC_LIB=ab after scripts/experiments/ab_knobs_r3.patch)")
     a = ap.parse_args()
     import numpy as np
     import torch
