@@ -33,6 +33,9 @@ CASES = [
     ("r4_c256_s5_cp32", 2, 5, 4, 256, 32, "time", 0.05),
     ("r3_c64_s4_odd_antennas", 2, 4, 3, 64, 0, "time", 0.01),
     ("freq_r16_c1024_s3", 1, 3, 16, 1024, 0, "freq", 0.01),
+    # round 4: configs[4]'s C (the wave-pair kernels k_ls_td4096 / k_mrc_td4096h)
+    ("r8_c4096_s3_cp32", 1, 3, 8, 4096, 32, "time", 0.01),
+    ("r32_c4096_s2", 1, 2, 32, 4096, 0, "time", 0.01),
 ]
 
 
@@ -88,7 +91,10 @@ def main():
     raw.tofile(pil)
     X = ref.matrix_readX(pil, 1023)
     np.save(os.path.join(HERE, "pilots_rotated_k1023.npy"), X)
+    only = sys.argv[1:]  # optional: regenerate only the named cases (seeds stay by position)
     for i, c in enumerate(CASES):
+        if only and c[0] not in only:
+            continue
         make_case(o, ref, *c, seed=1234 + i, raw_pilots_path=pil)
         print("wrote", c[0])
 
