@@ -34,7 +34,11 @@ int hip_check(hipError_t e, const char *what) {
     return fail(OFDM_E_HIP, "%s: %s", what, hipGetErrorString(e));
 }
 
-bool pow2_c(int C) { return C >= 4 && C <= 4096 && (C & (C - 1)) == 0; }
+// Every FFT length in [2, 8192]: the fused receivers at 1024 / 2048 / 4096,
+// the radix-4 row FFT for the other powers of two up to 4096 and the
+// mixed-radix one (fft_any.hip) for the rest; the reference takes whatever
+// `dimension` it is built with (ShMemSymBuff.hpp:47, FFTW / cuFFT).
+bool valid_c(int C) { return C >= 2 && C <= ofdm::FFT_ANY_MAX; }
 
 inline hipStream_t hs(ofdm_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
 inline const float2 *F2(const ofdm_cf32 *p) { return reinterpret_cast<const float2 *>(p); }
@@ -186,7 +190,7 @@ int check_frame_args(const void *in, long long F, int S, int R, int C, int prefi
     if (F > 0 && (!in || !out)) return fail(OFDM_E_ARG, "%s: null pointer", fn);
     if (S < 2) return fail(OFDM_E_ARG, "%s: S=%d, a frame needs a pilot and >= 1 data symbol", fn, S);
     if (R < 1) return fail(OFDM_E_ARG, "%s: R=%d < 1", fn, R);
-    if (!pow2_c(C)) return fail(OFDM_E_UNSUPPORTED, "%s: C=%d not a power of two in [4, 4096]", fn, C);
+    if (!valid_c(C)) return fail(OFDM_E_UNSUPPORTED, "%s: C=%d out of [2, 8192]", fn, C);
     if (prefix < 0 || prefix > C) return fail(OFDM_E_ARG, "%s: prefix=%d out of [0, C]", fn, prefix);
     if (!aligned(in, 16)) return fail(OFDM_E_ARG, "%s: input must be 16-byte aligned", fn);
     return OFDM_OK;
@@ -282,7 +286,7 @@ int ofdm_read_pilots(const char *path, int K, float fill, ofdm_cf32 *X) {
 int ofdm_fft_rows(const ofdm_cf32 *d_in, ofdm_cf32 *d_out, long long nrows, int C, int inverse,
                   ofdm_stream_t stream) {
     if (!d_in || !d_out || nrows < 0) return fail(OFDM_E_ARG, "ofdm_fft_rows: bad arguments");
-    if (!pow2_c(C)) return fail(OFDM_E_UNSUPPORTED, "ofdm_fft_rows: C=%d not a power of two in [4, 4096]", C);
+    if (!valid_c(C)) return fail(OFDM_E_UNSUPPORTED, "ofdm_fft_rows: C=%d out of [2, 8192]", C);
     return hip_check(ofdm::launch_fft_rows(F2(d_in), C, 0, F2(d_out), C, 0, nrows, C, inverse != 0,
                                            1.f, hs(stream)),
                      "ofdm_fft_rows");
@@ -292,7 +296,7 @@ int ofdm_ls_estimate(const ofdm_cf32 *d_Y, const ofdm_cf32 *d_X, int R, int C, o
                      float *d_Hsqrd, ofdm_stream_t stream) {
     if (!d_Y || !d_X || !d_Hconj || !d_Hsqrd || R < 1)
         return fail(OFDM_E_ARG, "ofdm_ls_estimate: bad arguments");
-    if (!pow2_c(C)) return fail(OFDM_E_UNSUPPORTED, "ofdm_ls_estimate: C=%d unsupported", C);
+    if (!valid_c(C)) return fail(OFDM_E_UNSUPPORTED, "ofdm_ls_estimate: C=%d out of [2, 8192]", C);
     const int K = C - 1;
     return hip_check(ofdm::launch_ls_freq(F2(d_Y), 0, 1, R, C, F2(d_X), F2(d_Hconj), 0, K, 0, d_Hsqrd,
                                           0, 0, hs(stream)),
@@ -304,7 +308,7 @@ static int mrc_common(const ofdm_cf32 *d_Y, long long nsyms, const ofdm_cf32 *d_
                       ofdm_stream_t stream, const char *fn) {
     if (!d_Y || !d_Hconj || !d_out || (mode == 0 && !d_Hsqrd) || R < 1 || nsyms < 0)
         return fail(OFDM_E_ARG, "%s: bad arguments", fn);
-    if (!pow2_c(C)) return fail(OFDM_E_UNSUPPORTED, "%s: C=%d unsupported", fn, C);
+    if (!valid_c(C)) return fail(OFDM_E_UNSUPPORTED, "%s: C=%d out of [2, 8192]", fn, C);
     if (!aligned(d_Y, 16)) return fail(OFDM_E_ARG, "%s: d_Y must be 16-byte aligned", fn);
     const int K = C - 1;
     // all symbols share one estimate: one "frame" holding nsyms data symbols
@@ -339,7 +343,7 @@ int ofdm_channel_conj_product(const ofdm_cf32 *d_Y, long long nsyms, const ofdm_
                               int R, int C, ofdm_cf32 *d_prod, ofdm_stream_t stream) {
     if (!d_Y || !d_Hconj || !d_prod || nsyms < 0 || R < 1)
         return fail(OFDM_E_ARG, "ofdm_channel_conj_product: bad arguments");
-    if (!pow2_c(C)) return fail(OFDM_E_UNSUPPORTED, "ofdm_channel_conj_product: C=%d unsupported", C);
+    if (!valid_c(C)) return fail(OFDM_E_UNSUPPORTED, "ofdm_channel_conj_product: C=%d out of [2, 8192]", C);
     if (nsyms == 0) return OFDM_OK;
     return hip_check(ofdm::launch_conj_product(F2(d_Y), nsyms, R, C, F2(d_Hconj), F2(d_prod), hs(stream)),
                      "ofdm_channel_conj_product");
@@ -368,7 +372,7 @@ int ofdm_dist_sqrd(const ofdm_cf32 *d_H, int R, int K, float *d_Hsqrd, ofdm_stre
 }
 
 size_t ofdm_frame_workspace_bytes(long long nframes, int S, int R, int C) {
-    if (nframes < 0 || S < 2 || R < 1 || !pow2_c(C)) return 0;
+    if (nframes < 0 || S < 2 || R < 1 || !valid_c(C)) return 0;
     return ws_bytes(nframes, S, R, C, !fused_c(C));
 }
 
@@ -505,7 +509,7 @@ int ofdm_frame_demod_freq_mfma(const ofdm_cf32 *d_Y, long long nframes, int S, i
                                ofdm_stream_t stream) {
     int rc = check_frame_args(d_Y, nframes, S, R, C, 0, d_out, "ofdm_frame_demod_freq_mfma");
     if (rc) return rc;
-    if (C < 64) return fail(OFDM_E_UNSUPPORTED, "ofdm_frame_demod_freq_mfma: C=%d < 64", C);
+    if (C % 64) return fail(OFDM_E_UNSUPPORTED, "ofdm_frame_demod_freq_mfma: C=%d not a multiple of 64", C);
     if (!d_X) return fail(OFDM_E_ARG, "ofdm_frame_demod_freq_mfma: null pilots");
     if (nframes == 0) return OFDM_OK;
     Workspace w;
@@ -614,7 +618,7 @@ int ofdm_frame_export_estimate(const void *d_ws, size_t ws_bytes_, long long nfr
     if (!d_Hconj) return fail(OFDM_E_ARG, "ofdm_frame_export_estimate: null d_Hconj");
     if (nframes < 1 || frame < 0 || frame >= nframes)
         return fail(OFDM_E_ARG, "ofdm_frame_export_estimate: frame %lld outside [0, %lld)", frame, nframes);
-    if (S < 2 || R < 1 || !pow2_c(C)) return fail(OFDM_E_ARG, "ofdm_frame_export_estimate: bad geometry");
+    if (S < 2 || R < 1 || !valid_c(C)) return fail(OFDM_E_ARG, "ofdm_frame_export_estimate: bad geometry");
     WsTag tag;
     int rc = ws_check(d_ws, ws_bytes_, nframes, S, R, C, false, "ofdm_frame_export_estimate", &tag);
     if (rc) return rc;
@@ -630,7 +634,7 @@ int ofdm_synth_frames(ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, i
                       float noise_std, int freq_domain, int r0, ofdm_stream_t stream) {
     if (!d_iq || !d_X || nframes < 0 || S < 1 || R < 1 || prefix < 0 || prefix > C || r0 < 0)
         return fail(OFDM_E_ARG, "ofdm_synth_frames: bad arguments");
-    if (!pow2_c(C)) return fail(OFDM_E_UNSUPPORTED, "ofdm_synth_frames: C=%d unsupported", C);
+    if (!valid_c(C)) return fail(OFDM_E_UNSUPPORTED, "ofdm_synth_frames: C=%d out of [2, 8192]", C);
     return hip_check(ofdm::launch_synth(F2(d_iq), nframes, S, R, C, freq_domain ? 0 : prefix, F2(d_X),
                                         seed, frame0, noise_std, freq_domain, r0, hs(stream)),
                      "ofdm_synth_frames");
@@ -639,7 +643,7 @@ int ofdm_synth_frames(ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, i
 int ofdm_count_symbol_errors(const ofdm_cf32 *d_out, long long nframes, int S, int C,
                              unsigned long long seed, long long frame0,
                              unsigned long long *d_errors, ofdm_stream_t stream) {
-    if (!d_out || !d_errors || nframes < 0 || S < 2 || !pow2_c(C))
+    if (!d_out || !d_errors || nframes < 0 || S < 2 || !valid_c(C))
         return fail(OFDM_E_ARG, "ofdm_count_symbol_errors: bad arguments");
     return hip_check(ofdm::launch_count_errors(F2(d_out), nframes, S, C, seed, frame0, d_errors,
                                                hs(stream)),

@@ -134,15 +134,30 @@ __device__ float2 *stockham_lds(float2 *a, float2 *b) {
 }
 
 // --------------------------------------------------------------------------
-// Receiver index maps (K = C - 1 used subcarriers, odd).
+// Receiver index maps (K = C - 1 used subcarriers).
 // Bin b = j + 1 of the FFT carries subcarrier j (DC dropped, cpuLS.hpp:290-292).
-// Output position of subcarrier j after shiftOneRow (cpuLS.hpp:135-149):
+// Output position of subcarrier j after shiftOneRow (cpuLS.hpp:135-149), odd
+// K (every even C, so every fused receiver and the paired-bin kernels):
 //   out[k] = Z[k + (K-1)/2]        for k <  (K+1)/2
 //   out[k] = Z[k - (K+1)/2]        for k >= (K+1)/2
 // --------------------------------------------------------------------------
 __device__ __forceinline__ int out_pos(int j, int K) {
     const int h = (K - 1) / 2;
     return j >= h ? j - h : j + (K + 1) / 2;
+}
+// Any K: shiftOneRow's three memmoves literally, h = (K-1)/2, n2 = (K+1)/2:
+//   out[k] = Z[k + h] (k < n2),  Z[k - n2] (n2 <= k < n2 + h),  Z[k] (k >= n2 + h)
+// -- for even K (odd C) the CPU reference leaves the last element in place
+// (its GPU kernel, gpuLS.cu:109-125, would duplicate Z[h] there instead; the
+// CPU function is the one the oracle pins).  Equal to out_pos for odd K.
+__device__ __forceinline__ int out_pos_any(int j, int K) {
+    const int h = (K - 1) / 2, n2 = (K + 1) / 2;
+    return j < h ? j + n2 : (j < h + n2 ? j - h : j);
+}
+// the subcarrier that out_pos_any puts at output position k
+__device__ __forceinline__ int out_src(int k, int K) {
+    const int h = (K - 1) / 2, n2 = (K + 1) / 2;
+    return k < n2 ? k + h : (k < n2 + h ? k - n2 : k);
 }
 
 // LS for one subcarrier: conj(y / x) with divideOneRow's naive formula

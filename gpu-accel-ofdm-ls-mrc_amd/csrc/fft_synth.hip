@@ -62,7 +62,7 @@ hipError_t launch_fft_rows(const float2 *in, long long in_stride, int in_off, fl
         OFDM_FFT_CASE(7) OFDM_FFT_CASE(8) OFDM_FFT_CASE(9) OFDM_FFT_CASE(10) OFDM_FFT_CASE(11)
         OFDM_FFT_CASE(12)
 #undef OFDM_FFT_CASE
-    default: return hipErrorInvalidValue;
+    default: return launch_fft_any(in, in_stride, in_off, out, out_stride, out_off, nrows, C, inverse, scale, s);
     }
 }
 
@@ -157,6 +157,81 @@ static hipError_t synth_t(float2 *iq, long long nframes, int S, int R, int prefi
     return hipGetLastError();
 }
 
+// Any other C (fft_any.hip sizes): the same frames in three passes over the
+// output rows -- the bins H x into row[prefix + b] (k_synth_bins), the
+// inverse FFT in place with the 1/sqrt(C) scale, then the noise and the
+// cyclic prefix (k_synth_noise_cp, one workgroup per row: the prefix copies
+// the noisy tail, as k_synth does).  The frequency-domain form adds its noise
+// in the first pass.
+__global__ void __launch_bounds__(256) k_synth_bins(float2 *iq, long long rows, int S, int R, int C, int prefix,
+                                                    const float2 *__restrict__ X, uint64_t seed, long long frame0,
+                                                    float noise_std, int freq_domain, int r0) {
+    const int Cp = freq_domain ? C : C + prefix;
+    const float ns = noise_std * 0.70710678118654752f;
+    for (long long row = blockIdx.y; row < rows; row += gridDim.y) {
+        const int r = (int)(row % R);
+        const long long fs = row / R;
+        const int s = (int)(fs % S);
+        const long long fg = frame0 + fs / S;
+        const int rg = r0 + r;
+        const uint64_t nkey = (((uint64_t)fg * (uint64_t)S + (uint64_t)s) << 20) ^ (uint64_t)rg;
+        float2 *dst = iq + row * Cp + (freq_domain ? 0 : prefix);
+        for (int bin = blockIdx.x * blockDim.x + threadIdx.x; bin < C; bin += gridDim.x * blockDim.x) {
+            float2 v{0.f, 0.f};
+            if (bin > 0) {
+                const int j = bin - 1;
+                const float2 x = s == 0 ? X[j] : qpsk(synth_bits(seed, fg, s, j));
+                v = cmul(synth_channel(seed, fg, rg, j), x);
+            }
+            if (freq_domain) {
+                const float2 g = gauss2(hash4(seed, 3, nkey, (uint64_t)bin));
+                v = float2{v.x + ns * g.x, v.y + ns * g.y};
+            }
+            dst[bin] = v;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_synth_noise_cp(float2 *iq, long long rows, int S, int R, int C, int prefix,
+                                                        uint64_t seed, long long frame0, float noise_std, int r0) {
+    const float ns = noise_std * 0.70710678118654752f;
+    for (long long row = blockIdx.x; row < rows; row += gridDim.x) {
+        const int r = (int)(row % R);
+        const long long fs = row / R;
+        const int s = (int)(fs % S);
+        const long long fg = frame0 + fs / S;
+        const uint64_t nkey = (((uint64_t)fg * (uint64_t)S + (uint64_t)s) << 20) ^ (uint64_t)(r0 + r);
+        float2 *dst = iq + row * (C + prefix);
+        for (int n = threadIdx.x; n < C; n += blockDim.x) {
+            const float2 g = gauss2(hash4(seed, 3, nkey, (uint64_t)n));
+            const float2 v = dst[prefix + n];
+            dst[prefix + n] = float2{v.x + ns * g.x, v.y + ns * g.y};
+        }
+        __syncthreads();  // the prefix copies the noisy tail
+        for (int n = threadIdx.x; n < prefix; n += blockDim.x) dst[n] = dst[C + n];
+        __syncthreads();
+    }
+}
+
+static hipError_t synth_any(float2 *iq, long long nframes, int S, int R, int C, int prefix, const float2 *X,
+                            uint64_t seed, long long frame0, float noise_std, int freq_domain, int r0,
+                            hipStream_t s) {
+    if (!fft_any_supported(C)) return hipErrorInvalidValue;
+    const long long rows = nframes * S * R;
+    const unsigned gx = (unsigned)((C + 255) / 256);
+    const unsigned gy = (unsigned)(rows < 65535 ? rows : 65535);
+    hipLaunchKernelGGL(k_synth_bins, dim3(gx, gy), dim3(256), 0, s, iq, rows, S, R, C, prefix, X, seed, frame0,
+                       noise_std, freq_domain, r0);
+    if (freq_domain) return hipGetLastError();
+    const hipError_t e = launch_fft_any(iq, C + prefix, prefix, iq, C + prefix, prefix, rows, C, true,
+                                        1.0f / sqrtf((float)C), s);
+    if (e != hipSuccess) return e;
+    const unsigned g = (unsigned)(rows < 16384 ? rows : 16384);
+    hipLaunchKernelGGL(k_synth_noise_cp, dim3(g), dim3(256), 0, s, iq, rows, S, R, C, prefix, seed, frame0,
+                       noise_std, r0);
+    return hipGetLastError();
+}
+
 hipError_t launch_synth(float2 *iq, long long nframes, int S, int R, int C, int prefix,
                         const float2 *X, uint64_t seed, long long frame0, float noise_std,
                         int freq_domain, int r0, hipStream_t s) {
@@ -168,7 +243,7 @@ hipError_t launch_synth(float2 *iq, long long nframes, int S, int R, int C, int 
         OFDM_SYN_CASE(7) OFDM_SYN_CASE(8) OFDM_SYN_CASE(9) OFDM_SYN_CASE(10) OFDM_SYN_CASE(11)
         OFDM_SYN_CASE(12)
 #undef OFDM_SYN_CASE
-    default: return hipErrorInvalidValue;
+    default: return synth_any(iq, nframes, S, R, C, prefix, X, seed, frame0, noise_std, freq_domain, r0, s);
     }
 }
 
@@ -182,7 +257,7 @@ __global__ void __launch_bounds__(256) k_count_errors(const float2 *__restrict__
         const long long q = e / K;  // data symbol index
         const long long f = q / (S - 1);
         const int s = 1 + (int)(q % (S - 1));
-        const int j = k < (K + 1) / 2 ? k + (K - 1) / 2 : k - (K + 1) / 2;
+        const int j = out_src(k, K);
         const uint32_t bits = synth_bits(seed, frame0 + f, s, j);
         const float2 v = out[e];
         const bool ok = ((v.x > 0.f) == ((bits & 1u) != 0)) && ((v.y > 0.f) == ((bits & 2u) != 0));

@@ -34,10 +34,18 @@ int set_error(int code, const char *msg);
 
 // Generic batched row FFT (Stockham in LDS), in place or out of place.
 // Row i is read from in + i*in_stride + in_off and written to
-// out + i*out_stride + out_off.  C power of two, 4 <= C <= 4096.
+// out + i*out_stride + out_off.  Any 2 <= C <= FFT_ANY_MAX: powers of two up
+// to 4096 run the radix-4 kernel (fft_synth.hip), every other length the
+// mixed-radix one (fft_any.hip).
+constexpr int FFT_ANY_MAX = 8192;
 hipError_t launch_fft_rows(const float2 *in, long long in_stride, int in_off, float2 *out,
                            long long out_stride, int out_off, long long nrows, int C,
                            bool inverse, float scale, hipStream_t s);
+// The mixed-radix kernel alone (any C in [2, FFT_ANY_MAX]).
+hipError_t launch_fft_any(const float2 *in, long long in_stride, int in_off, float2 *out,
+                          long long out_stride, int out_off, long long nrows, int C, bool inverse,
+                          float scale, hipStream_t s);
+bool fft_any_supported(int C);
 
 // LS channel estimate on frequency-domain pilot symbols.
 // Pilot of frame f: Y + f*frame_stride, R rows of C bins.

@@ -115,6 +115,36 @@ __global__ void __launch_bounds__(256) k_mrc_freq(const float2 *__restrict__ Y, 
     }
 }
 
+// Odd C (no 16-byte bin pairs): one lane = one subcarrier j of one data
+// symbol; Hc(r, j) at r*hc_ld + j + hofs (hofs = 1 in the bin layout).
+__global__ void __launch_bounds__(256) k_mrc_freq1(const float2 *__restrict__ Y, long long frame_stride,
+                                                   long long sym_stride, long long nq, int nsym, int R, int C,
+                                                   const float2 *__restrict__ Hc, long long hc_fstride, int hc_ld,
+                                                   int hofs, const float *__restrict__ P, long long p_fstride,
+                                                   int p_jofs, float2 *__restrict__ out, int mode) {
+    const int K = C - 1;
+    const int bps = (K + blockDim.x - 1) / blockDim.x;
+    const long long q = (long long)blockIdx.x / bps;
+    const int j = (int)(blockIdx.x % bps) * blockDim.x + threadIdx.x;
+    if (q >= nq || j >= K) return;
+    const long long f = q / nsym;
+    const float2 *Ys = Y + f * frame_stride + (q % nsym) * sym_stride + j + 1;
+    const float2 *Hf = Hc + f * hc_fstride + j + hofs;
+    float2 a{0.f, 0.f};
+    for (int r = 0; r < R; ++r) {
+        const float2 y = Ys[(long long)r * C], h = Hf[(long long)r * hc_ld];
+        // matrixMultThenSum (cpuLS.hpp:203-204), antennas in order
+        a.x = a.x + (y.x * h.x - y.y * h.y);
+        a.y = a.y + (y.x * h.y + y.y * h.x);
+    }
+    if (mode == 0) {
+        const float p = P[f * p_fstride + p_jofs + j];
+        out[q * K + out_pos_any(j, K)] = float2{a.x / p, a.y / p};
+    } else {
+        out[q * K + j] = a;
+    }
+}
+
 // Bin-layout MRC over whole frames (ofdm_frame_demod_freq, the staged path):
 // one lane = two adjacent bins of G consecutive data symbols of ONE frame,
 // so each Hc float4 read from L2 serves G symbols, and the antenna loop is
@@ -215,10 +245,10 @@ hipError_t launch_mrc_freq(const float2 *Y, long long frame_stride, long long sy
                            long long p_fstride, int p_jofs, float2 *out, int mode, hipStream_t s) {
     const long long nq = nframes * nsym;
     if (nq <= 0) return hipSuccess;
-    if (C >= 512 && hc_jofs == 0 && hc_ld == C && (hc_fstride % 2) == 0 &&
+    if (C >= 512 && (C % 2) == 0 && hc_jofs == 0 && hc_ld == C && (hc_fstride % 2) == 0 &&
         (sym_stride % 2) == 0 &&
         (frame_stride % 2) == 0 && ((uintptr_t)Hc % 16) == 0 && ((uintptr_t)Y % 16) == 0) {
-        const int bps = C / 2 / 256;
+        const int bps = (C / 2 + 255) / 256;  // C = 1200, 1536, ...: a partial last chunk
         // same-process A/B (profiles/r2_ab/abf_*): 8 symbols per lane at C <= 2048
         // (2 waves/SIMD, 32 KiB in flight per wave), 4 at C = 4096
         auto kern = C >= 4096 ? k_mrc_freq_frames<4, 4> : k_mrc_freq_frames<8, 4>;
@@ -227,6 +257,15 @@ hipError_t launch_mrc_freq(const float2 *Y, long long frame_stride, long long sy
         if (pxg * 8 > 0x7fffffffll) return hipErrorInvalidValue;
         hipLaunchKernelGGL(kern, dim3((unsigned)(pxg * 8)), dim3(256), 0, s, Y, frame_stride, sym_stride, nsym, R,
                            C, Hc, hc_fstride, P, p_fstride, p_jofs, out, mode, nbg, pxg, bps);
+        return hipGetLastError();
+    }
+    if (C & 1) {
+        const int bps = (C - 1 + 255) / 256;
+        const long long blocks = nq * bps;
+        if (blocks > 0x7fffffffll) return hipErrorInvalidValue;
+        const int hofs = (hc_jofs == 0 && hc_ld == C) ? 1 : hc_jofs;  // bin layout: subcarrier j at bin j + 1
+        hipLaunchKernelGGL(k_mrc_freq1, dim3((unsigned)blocks), dim3(256), 0, s, Y, frame_stride, sym_stride, nq,
+                           nsym, R, C, Hc, hc_fstride, hc_ld, hofs, P, p_fstride, p_jofs, out, mode);
         return hipGetLastError();
     }
     const int threads = C / 2 < 256 ? 64 * ((C / 2 + 63) / 64) : 256;
@@ -258,7 +297,7 @@ __global__ void __launch_bounds__(256) k_mrc_finalize(const float2 *__restrict__
         const long long f = q / nsym;
         const float p = P[f * K + j];
         const float2 v = num[i];
-        out[q * K + out_pos(j, K)] = float2{v.x / p, v.y / p};
+        out[q * K + out_pos_any(j, K)] = float2{v.x / p, v.y / p};
     }
 }
 

@@ -112,7 +112,7 @@ int ofdm_pipeline_create(int S, int R, int C, int cp_len, const ofdm_cf32 *X, in
     if (chunk_frames < 1 || depth < 1 || depth > 64)
         return err(OFDM_E_ARG, fn, "chunk_frames >= 1 and 1 <= depth <= 64 required");
     const size_t ws = ofdm_frame_workspace_bytes(chunk_frames, S, R, C);
-    if (ws == 0) return err(OFDM_E_UNSUPPORTED, fn, "bad frame geometry (S >= 2, R >= 1, C pow2 4..4096)");
+    if (ws == 0) return err(OFDM_E_UNSUPPORTED, fn, "bad frame geometry (S >= 2, R >= 1, 2 <= C <= 8192)");
     if (cp_len < 0 || cp_len > C) return err(OFDM_E_ARG, fn, "cp_len out of [0, C]");
     auto *p = new (std::nothrow) ofdm_pipeline;
     if (!p) return err(OFDM_E_ARG, fn, "out of host memory");

@@ -39,7 +39,7 @@ __global__ void __launch_bounds__(256) k_combine(const float2 *__restrict__ prod
         float2 acc = prod[s * R * K + j];
         for (int r = 1; r < R; ++r) acc = cadd(acc, prod[(s * R + r) * K + j]);
         const float p = P[j];
-        out[s * K + (rotate ? out_pos(j, K) : j)] = float2{acc.x / p, acc.y / p};
+        out[s * K + (rotate ? out_pos_any(j, K) : j)] = float2{acc.x / p, acc.y / p};
     }
 }
 
@@ -47,7 +47,7 @@ __global__ void __launch_bounds__(256) k_shift_rows(const float2 *__restrict__ i
                                                     float2 *__restrict__ out) {
     const long long row = blockIdx.y;
     for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < K; j += gridDim.x * blockDim.x)
-        out[row * K + out_pos(j, K)] = in[row * K + j];
+        out[row * K + out_pos_any(j, K)] = in[row * K + j];
 }
 
 __global__ void __launch_bounds__(256) k_dist_sqrd(const float2 *__restrict__ H, int R, int K,

@@ -8,8 +8,9 @@
 // the drivers build unchanged on a machine without FFTW: a plan records its
 // size, arrays and sign, and executing it runs ofdm_fft_rows (unnormalised
 // C2C, the FFTW sign convention: FFTW_FORWARD = e^{-2 pi i jk/n}) on the GPU
-// through the host staging engine.  Sizes are the library's: n a power of two
-// in [4, 4096]; any other n aborts with a message (no CPU fallback).
+// through the host staging engine.  Sizes are the library's: any n in
+// [2, 8192] (n = 1 is the identity); any other n aborts with a message (no CPU
+// fallback).
 // Planning never touches the arrays (FFTW_MEASURE's clobbering, which the
 // reference works around at cpuLS.hpp:262, does not happen).
 //
@@ -46,8 +47,8 @@ typedef ofdm_fftwf_plan_s *fftwf_plan;
 
 inline fftwf_plan fftwf_plan_dft_1d(int n, fftwf_complex *in, fftwf_complex *out, int sign,
                                     unsigned /*flags*/) {
-    if (n < 4 || n > 4096 || (n & (n - 1)) != 0) {
-        std::fprintf(stderr, "fftwf_plan_dft_1d: n=%d unsupported (power of two in [4, 4096])\n", n);
+    if (n < 1 || n > 8192) {
+        std::fprintf(stderr, "fftwf_plan_dft_1d: n=%d unsupported (1 <= n <= 8192)\n", n);
         std::abort();
     }
     return new ofdm_fftwf_plan_s{n, in, out, sign};
@@ -55,6 +56,7 @@ inline fftwf_plan fftwf_plan_dft_1d(int n, fftwf_complex *in, fftwf_complex *out
 
 inline void fftwf_execute(const fftwf_plan p) {
     if (p->out != p->in) std::memcpy(p->out, p->in, sizeof(fftwf_complex) * (size_t)p->n);
+    if (p->n == 1) return;  // the DFT of one sample is itself
     ofdm::HostEngine::get().fft_rows(p->out, 1, p->n, p->sign == FFTW_BACKWARD ? 1 : 0);
 }
 

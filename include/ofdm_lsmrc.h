@@ -8,8 +8,9 @@
  * GPU and returns an error if it cannot).
  *
  * Conventions (all cite the reference bhargav0410/gpu-accel-ofdm-ls-mrc):
- *   R  = RX antennas (numOfRows), C = FFT size / subcarriers (dimension, a
- *        power of two), K = C - 1 used subcarriers (the DC bin is dropped,
+ *   R  = RX antennas (numOfRows), C = FFT size / subcarriers (dimension:
+ *        any 2 <= C <= 8192, like the reference's FFTW / cuFFT plans; else
+ *        OFDM_E_UNSUPPORTED), K = C - 1 used subcarriers (the DC bin is dropped,
  *        cpuLS.hpp:290-292), S = symbols per frame (lenOfBuffer), symbol 0 of
  *        a frame is the pilot, symbols 1..S-1 carry data.
  *   ofdm_cf32 = {float re, im}, layout-identical to complexF
@@ -19,7 +20,9 @@
  *        symbols, batches are consecutive frames.
  *   Output of a data symbol: K values, shiftOneRow-rotated (cpuLS.hpp:135-149):
  *        out[k] = Z[(k + (K-1)/2) mod K], Z[j] = sum_r Y[r][j+1] conj(H[r][j])
- *        / sum_r |H[r][j]|^2.
+ *        / sum_r |H[r][j]|^2, for odd K (even C); for even K (odd C) the
+ *        three memmoves of shiftOneRow literally: out[k] = Z[k + K/2 - 1] for
+ *        k < K/2, Z[k - K/2] for K/2 <= k < K-1, and out[K-1] = Z[K-1].
  *   Pointers named d_* are device pointers; `stream` is a hipStream_t (NULL =
  *   the default stream).  Calls are asynchronous on that stream.
  *   Return value: 0 (OFDM_OK) or a negative OFDM_E_* code; ofdm_last_error()
@@ -69,7 +72,9 @@ int ofdm_read_pilots(const char *path, int K, float fill, ofdm_cf32 *X);
  * contiguous rows of C samples, in place or out of place.
  * Replaces gpuLS::batchedFFT (gpuLS.cu:343-349) / cufftPlan1d + cufftExecC2C
  * (gpuLS.cu:377-381, 441-445) and fftOneRow (cpuLS.hpp:165-174).
- * C in {4, 8, ..., 4096}. */
+ * Any 2 <= C <= 8192: powers of two up to 4096 by radix-4 Stockham stages,
+ * every other length by mixed-radix stages (radices 8, 4, 2, 3, 5, 7 and a
+ * direct stage with double accumulation for larger prime factors). */
 int ofdm_fft_rows(const ofdm_cf32 *d_in, ofdm_cf32 *d_out, long long nrows, int C, int inverse,
                   ofdm_stream_t stream);
 
@@ -160,8 +165,8 @@ int ofdm_workspace_release(const void *d_ws);
  * both run in ONE launch (estimator workgroups publish each frame's estimate
  * to the MRC workgroups through the workspace's flag words, agent-scope
  * release/acquire), except on a stream being captured into a graph, where
- * the two launches are used.  Other powers of two run FFT, LS and MRC as
- * stages through the workspace's staging buffer. */
+ * the two launches are used.  Every other C in [2, 8192] runs FFT, LS
+ * and MRC as stages through the workspace's staging buffer. */
 int ofdm_frame_demod(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, int cp_len,
                      const ofdm_cf32 *d_X, void *d_ws, size_t ws_bytes, ofdm_cf32 *d_out,
                      ofdm_stream_t stream);

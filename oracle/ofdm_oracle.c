@@ -102,7 +102,53 @@ static void fft_double(double *re, double *im, int C, int inverse) {
     }
 }
 
+/* Any other length (the sizes FFTW takes beyond powers of two, e.g. 1536,
+ * 600, odd and prime C): decimation in time by the smallest prime factor p
+ * of n, X[k] = sum_{r<p} W_n^{r k} S_r[k mod n/p] with S_r the DFTs of the p
+ * subsequences x[r + p i]; at prime n the direct sum.  Double precision,
+ * every twiddle from cos / sin of the exact angle 2 pi ((r k) mod n) / n. */
+static void dft_any(const double *xr, const double *xi, size_t stride, int n, double *yr, double *yi,
+                    double sgn) {
+    if (n == 1) { yr[0] = xr[0]; yi[0] = xi[0]; return; }
+    int p = 2;
+    while (p * p <= n && n % p) ++p;
+    if (n % p) p = n;
+    const int m = n / p;
+    double *sr = (double *)malloc((size_t)n * sizeof(double));
+    double *si = (double *)malloc((size_t)n * sizeof(double));
+    if (p == n) { /* prime: the subsequences are single samples */
+        for (int r = 0; r < n; ++r) { sr[r] = xr[r * stride]; si[r] = xi[r * stride]; }
+    } else {
+        for (int r = 0; r < p; ++r)
+            dft_any(xr + r * stride, xi + r * stride, stride * p, m, sr + (size_t)r * m, si + (size_t)r * m, sgn);
+    }
+    for (int k = 0; k < n; ++k) {
+        double ar = 0.0, ai = 0.0;
+        for (int r = 0; r < p; ++r) {
+            const double a = 2.0 * M_PI * (double)(((long long)r * k) % n) / (double)n;
+            const double wr = cos(a), wi = sgn * sin(a);
+            const double vr = sr[(size_t)r * m + k % m], vi = si[(size_t)r * m + k % m];
+            ar += vr * wr - vi * wi;
+            ai += vr * wi + vi * wr;
+        }
+        yr[k] = ar;
+        yi[k] = ai;
+    }
+    free(sr);
+    free(si);
+}
+
 void oracle_fft_row(oracle_cf32 *row, int C, int inverse) {
+    if (C < 1) return;
+    if (C & (C - 1)) { /* not a power of two */
+        double *xr = (double *)malloc((size_t)C * 4 * sizeof(double));
+        double *xi = xr + C, *yr = xr + 2 * (size_t)C, *yi = xr + 3 * (size_t)C;
+        for (int i = 0; i < C; ++i) { xr[i] = row[i].re; xi[i] = row[i].im; }
+        dft_any(xr, xi, 1, C, yr, yi, inverse ? 1.0 : -1.0);
+        for (int i = 0; i < C; ++i) { row[i].re = (float)yr[i]; row[i].im = (float)yi[i]; }
+        free(xr);
+        return;
+    }
     double stack_re[4096], stack_im[4096];
     double *re = stack_re, *im = stack_im;
     if (C > 4096) {
@@ -143,7 +189,7 @@ static const float *twiddles32(int log2c) {
 
 void oracle_fft_row_f32(oracle_cf32 *row, int C) {
     float re[4096], im[4096];
-    if (C > 4096) { oracle_fft_row(row, C, 0); return; }
+    if (C > 4096 || (C & (C - 1))) { oracle_fft_row(row, C, 0); return; }
     int log2c = 0;
     while ((1 << log2c) < C) ++log2c;
     for (int i = 0; i < C; ++i) { re[i] = row[i].re; im[i] = row[i].im; }

@@ -1,0 +1,113 @@
+"""FFT lengths beyond the powers of two (fft_any.hip): the reference transforms
+whatever `dimension` it is built with (ShMemSymBuff.hpp:47) through FFTW /
+cuFFT, so the library takes any C in [2, 8192] -- LTE's 1536, 600 and 1200,
+odd and prime lengths, 8192.  Checked through the C ABI against numpy
+(float64 FFT) and the oracle (its mixed-radix float64 DFT + the cpuLS.hpp
+LS / MRC restatement); tolerance helpers.RTOL = 1e-5 norm- and element-wise."""
+import numpy as np
+import pytest
+
+from helpers import parity
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [2, 3, 5, 6, 12, 15, 100, 243, 600, 1021, 1200, 1536, 2047, 3000, 4095, 6144, 8192]
+
+
+def to_dev(a, dev):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def host(t):
+    import torch
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+def qpsk(K, seed=7):
+    rng = np.random.default_rng(seed)
+    a = np.float32(0.70710678)
+    return (rng.choice([-a, a], K) + 1j * rng.choice([-a, a], K)).astype(np.complex64)
+
+
+@pytest.mark.parametrize("C", SIZES)
+def test_fft_rows_any_c_vs_numpy(ofdm, dev, C):
+    rng = np.random.default_rng(C)
+    n = 37
+    x = (rng.standard_normal((n, C)) + 1j * rng.standard_normal((n, C))).astype(np.complex64)
+    d = to_dev(x, dev)
+    out = ofdm.c64(x.shape, dev)
+    tol = 2e-6 * max(np.log2(C), 1.0)
+    got = host(ofdm.fft_rows(d, out))
+    ref = np.fft.fft(x.astype(np.complex128), axis=-1)
+    assert np.abs(got - ref).max() <= tol * np.abs(ref).max()
+    inv = host(ofdm.fft_rows(d, out, inverse=True))
+    refi = np.fft.ifft(x.astype(np.complex128), axis=-1) * C
+    assert np.abs(inv - refi).max() <= tol * np.abs(refi).max()
+    assert np.array_equal(host(ofdm.fft_rows(d)), got)  # in place
+
+
+def test_fft_rows_any_c_many_rows(ofdm, dev):
+    """More row groups than the persistent grid (2048 workgroups x G rows)."""
+    C = 12  # G = 341 rows per workgroup
+    rng = np.random.default_rng(5)
+    x = (rng.standard_normal((2048 * 341 + 77, C)) + 1j * rng.standard_normal((2048 * 341 + 77, C))).astype(
+        np.complex64)
+    got = host(ofdm.fft_rows(to_dev(x, dev)))
+    ref = np.fft.fft(x.astype(np.complex128), axis=-1)
+    assert np.abs(got - ref).max() <= 1e-5 * np.abs(ref).max()
+
+
+@pytest.mark.parametrize("C,R,prefix", [(6, 3, 0), (12, 1, 3), (600, 4, 44), (1021, 3, 0), (1200, 8, 84),
+                                        (1536, 8, 108), (1536, 64, 0), (3000, 2, 0), (6144, 4, 432),
+                                        (8192, 2, 512)])
+def test_frame_demod_any_c_vs_oracle(ofdm, oracle, dev, C, R, prefix):
+    F, S = 2, 4
+    X = to_dev(qpsk(C - 1), dev)
+    iq = ofdm.synth_frames(F, S, R, C, X, prefix=prefix, seed=C + R)
+    out = host(ofdm.frame_demod(iq, X, prefix))
+    ref = oracle.frames_demod(host(iq), host(X), prefix)
+    parity(out, ref)
+    # the synthetic frames decode to their own QPSK symbols
+    assert int(ofdm.count_symbol_errors(to_dev(out, dev), S, seed=C + R).item()) == 0
+    # estimate + combine (the staged two-call flow) gives the same bytes
+    ws = ofdm.workspace(F, S, R, C, dev)
+    ofdm.frame_estimate(iq, X, prefix, ws)
+    out2 = ofdm.c64(out.shape, dev)
+    ofdm.frame_combine(iq, prefix, ws, out2)
+    assert np.array_equal(host(out2), out)
+
+
+@pytest.mark.parametrize("C,R", [(7, 2), (601, 5), (1023, 8), (1535, 3)])
+def test_odd_c_freq_demod_vs_oracle(ofdm, oracle, dev, C, R):
+    """Odd C = even K: shiftOneRow's memmoves leave the last output in place
+    (cpuLS.hpp:135-149) -- the one-bin-per-lane combine and out_pos_any."""
+    F, S = 3, 5
+    X = to_dev(qpsk(C - 1), dev)
+    Y = ofdm.synth_frames(F, S, R, C, X, seed=C, freq_domain=True)
+    out = host(ofdm.frame_demod_freq(Y, X))
+    parity(out, oracle.frames_demod_freq(host(Y), host(X)))
+    assert int(ofdm.count_symbol_errors(to_dev(out, dev), S, seed=C).item()) == 0
+
+
+@pytest.mark.parametrize("C,R", [(7, 1), (12, 3), (1536, 16), (1023, 4)])
+def test_stages_any_c_vs_oracle(ofdm, oracle, dev, C, R):
+    rng = np.random.default_rng(C * R)
+    K = C - 1
+    X = qpsk(K)
+    Yp = (rng.standard_normal((R, C)) + 1j * rng.standard_normal((R, C))).astype(np.complex64)
+    Hc_ref, P_ref = oracle.ls(Yp, X)
+    Hc, P = ofdm.ls_estimate(to_dev(Yp, dev), to_dev(X, dev))
+    parity(host(Hc), Hc_ref)
+    parity(host(P), P_ref)
+    Yd = (rng.standard_normal((4, R, C)) + 1j * rng.standard_normal((4, R, C))).astype(np.complex64)
+    out = host(ofdm.mrc_demod(to_dev(Yd, dev), Hc, P))
+    parity(out, np.stack([oracle.mrc(Yd[s], Hc_ref, P_ref) for s in range(4)]))
+    # the per-stage gpuLS kernels: product, combine + rotate, shift
+    prod = ofdm.channel_conj_product(to_dev(Yd, dev), Hc)
+    comb = host(ofdm.combine_products(prod, P))
+    parity(comb, np.stack([oracle.mrc(Yd[s], Hc_ref, P_ref) for s in range(4)]))
+    rows = (rng.standard_normal((3, K)) + 1j * rng.standard_normal((3, K))).astype(np.complex64)
+    assert np.array_equal(host(ofdm.shift_rows(to_dev(rows, dev))),
+                          np.stack([oracle.shift_one_row(r) for r in rows]))

@@ -55,8 +55,10 @@ def test_argument_validation_without_device(ofdm):
     P = ctypes.c_void_p
     fake = P(4096)  # never dereferenced: validation rejects first
     # unsupported FFT size
-    assert L.ofdm_fft_rows(fake, fake, 1, 1000, 0, None) == -3
-    assert b"power of two" in L.ofdm_last_error()
+    assert L.ofdm_fft_rows(fake, fake, 1, 8193, 0, None) == -3
+    assert b"out of [2, 8192]" in L.ofdm_last_error()
+    assert L.ofdm_fft_rows(fake, fake, 1, 1, 0, None) == -3
+    assert L.ofdm_frame_demod(fake, 1, 2, 4, 16384, 0, fake, fake, 1 << 30, fake, None) == -3
     # null pointers
     assert L.ofdm_ls_estimate(None, fake, 4, 1024, fake, fake, None) == -1
     # frame shape errors
@@ -145,7 +147,10 @@ def test_workspace_sizes(ofdm):
     # non-fused C carries a bounded staging buffer (<= 256 MiB or one frame)
     b2 = ofdm.workspace_bytes(F, S, 64, 2048)
     assert b2 - (F * 64 * 2048 * 8 + F * 2048 * 4) <= max(256 << 20, S * 64 * 2048 * 8) + 512
-    assert ofdm.workspace_bytes(F, S, R, 1000) == 0
+    # any other C in [2, 8192] runs the staged path (mixed-radix row FFT)
+    for c in (2, 7, 1000, 1536, 8192):
+        assert ofdm.workspace_bytes(F, S, R, c) >= F * R * c * 8 + F * c * 4 + S * R * c * 8
+    assert ofdm.workspace_bytes(F, S, R, 1) == 0 and ofdm.workspace_bytes(F, S, R, 8193) == 0
 
 
 def test_pipeline_argument_validation_without_device(ofdm):
@@ -157,7 +162,7 @@ def test_pipeline_argument_validation_without_device(ofdm):
     assert L.ofdm_pipeline_create(101, 64, 1024, 0, None, 4, 3, ctypes.byref(h)) == -1
     assert L.ofdm_pipeline_create(101, 64, 1024, 0, X.ctypes.data_as(P), 0, 3, ctypes.byref(h)) == -1
     assert L.ofdm_pipeline_create(101, 64, 1024, 0, X.ctypes.data_as(P), 4, 0, ctypes.byref(h)) == -1
-    assert L.ofdm_pipeline_create(101, 64, 1000, 0, X.ctypes.data_as(P), 4, 3, ctypes.byref(h)) == -3
+    assert L.ofdm_pipeline_create(101, 64, 9000, 0, X.ctypes.data_as(P), 4, 3, ctypes.byref(h)) == -3
     assert L.ofdm_pipeline_create(1, 64, 1024, 0, X.ctypes.data_as(P), 4, 3, ctypes.byref(h)) == -3
     assert L.ofdm_pipeline_create(101, 64, 1024, 2000, X.ctypes.data_as(P), 4, 3,
                                   ctypes.byref(h)) == -1

@@ -56,9 +56,15 @@ def test_shift_closed_form(oracle):
     # shift undoes the pilot rotation
     z = np.arange(1023).astype(np.complex64)
     assert np.array_equal(oracle.shift_one_row(oracle.pilot_rotate(z)), z)
+    # even K (odd C): the three memmoves rotate the first K-1 values by K/2-1
+    # and leave the last in place (what the library's out_pos_any reproduces)
+    for K in (2, 6, 1022, 1534):
+        z = np.arange(K).astype(np.complex64)
+        exp = np.concatenate([(np.arange(K - 1) + K // 2 - 1) % (K - 1), [K - 1]])
+        assert np.array_equal(oracle.shift_one_row(z).real, exp)
 
 
-@pytest.mark.parametrize("C", [4, 8, 64, 256, 1024, 2048, 4096])
+@pytest.mark.parametrize("C", [4, 8, 64, 256, 1024, 2048, 4096, 2, 3, 6, 12, 600, 1021, 1200, 1536, 6144, 8192])
 def test_oracle_fft_matches_numpy(oracle, C):
     rng = np.random.default_rng(C)
     x = (rng.standard_normal((3, C)) + 1j * rng.standard_normal((3, C))).astype(np.complex64)
@@ -90,7 +96,8 @@ def test_oracle_f32_fft_for_cpu_baseline(oracle, C):
 
 
 @needs_ref
-@pytest.mark.parametrize("R,C", [(1, 4), (3, 64), (16, 1024), (64, 1024), (7, 2048)])
+@pytest.mark.parametrize("R,C", [(1, 4), (3, 64), (16, 1024), (64, 1024), (7, 2048), (2, 7), (3, 12), (4, 1536),
+                                 (2, 1023)])
 def test_oracle_bitexact_vs_reference_build(oracle, R, C):
     ref = Reference()
     rng = np.random.default_rng(R * C)
