@@ -196,44 +196,32 @@ int check_frame_args(const void *in, long long F, int S, int R, int C, int prefi
     return OFDM_OK;
 }
 
-// Generic (non-fused) time-domain frames: FFT rows of each chunk into the
-// staging buffer, then the frequency-domain LS / MRC kernels.
+// Generic (non-fused) time-domain frames.  LS: the pilot rows of each chunk
+// of frames FFT'd into the staging buffer (fft_any / k_fft_rows), then the
+// frequency-domain LS kernel (bin-layout Hc, P).  MRC: one fused pass over the
+// IQ (k_mrc_any: FFT + combine + normalise + rotate per symbol in LDS).
 // mode: 0 = full demod, 1 = MRC numerator only, 2 = LS only,
 //       3 = full demod against an estimate already in the workspace
 int td_staged(const float2 *iq, long long F, int S, int R, int C, int prefix, const float2 *X,
               const Workspace &w, float2 *out, int mode, hipStream_t s) {
-    const int K = C - 1;
     const long long frame_in = (long long)S * R * (C + prefix);
-    const long long frame_st = (long long)S * R * C;
-    for (long long f0 = 0; f0 < F; f0 += w.chunk) {
-        const long long n = F - f0 < w.chunk ? F - f0 : w.chunk;
-        const long long rows = mode == 2 ? 0 : n * S * R;
-        hipError_t e;
-        if (mode == 2) {  // only the pilot rows are needed
-            for (long long f = 0; f < n; ++f) {
-                e = ofdm::launch_fft_rows(iq + (f0 + f) * frame_in, C + prefix, prefix,
-                                          w.staging + f * frame_st, C, 0, R, C, false, 1.f, s);
-                if (e != hipSuccess) return hip_check(e, "fft (pilot rows)");
-            }
-        } else {
-            e = ofdm::launch_fft_rows(iq + f0 * frame_in, C + prefix, prefix, w.staging, C, 0, rows,
-                                      C, false, 1.f, s);
-            if (e != hipSuccess) return hip_check(e, "fft (frame rows)");
-        }
-        if (mode == 0 || mode == 2) {
-            e = ofdm::launch_ls_freq(w.staging, frame_st, n, R, C, X, w.Hc + f0 * R * C,
-                                     (long long)R * C, C, 1, w.P + f0 * C, C, 1, s);
+    hipError_t e;
+    if (mode == 0 || mode == 2) {
+        // the staging buffer holds w.chunk whole frames = w.chunk * S frames' pilot rows
+        const long long per = w.chunk * S, pilot = (long long)R * C;
+        for (long long f0 = 0; f0 < F; f0 += per) {
+            const long long n = F - f0 < per ? F - f0 : per;
+            e = ofdm::launch_fft_any_b(iq + f0 * frame_in, C + prefix, R, frame_in, prefix, w.staging, C, 0, n * R,
+                                       C, false, 1.f, s);
+            if (e != hipSuccess) return hip_check(e, "fft (pilot rows)");
+            e = ofdm::launch_ls_freq(w.staging, pilot, n, R, C, X, w.Hc + f0 * pilot, pilot, C, 1, w.P + f0 * C, C,
+                                     1, s);
             if (e != hipSuccess) return hip_check(e, "ls_freq");
         }
-        if (mode != 2) {
-            e = ofdm::launch_mrc_freq(w.staging + (long long)R * C, frame_st, (long long)R * C, n,
-                                      S - 1, R, C, w.Hc + f0 * R * C, (long long)R * C, C, 0,
-                                      w.P + f0 * C, C, 1, out + f0 * (S - 1) * K,
-                                      mode == 1 ? 1 : 0, s);
-            if (e != hipSuccess) return hip_check(e, "mrc_freq");
-        }
     }
-    return OFDM_OK;
+    if (mode == 2) return OFDM_OK;
+    return hip_check(ofdm::launch_mrc_any(iq, F, S, R, C, prefix, w.Hc, w.P, out, mode == 1 ? 1 : 0, s),
+                     "mrc_any");
 }
 
 }  // namespace

@@ -45,7 +45,18 @@ hipError_t launch_fft_rows(const float2 *in, long long in_stride, int in_off, fl
 hipError_t launch_fft_any(const float2 *in, long long in_stride, int in_off, float2 *out,
                           long long out_stride, int out_off, long long nrows, int C, bool inverse,
                           float scale, hipStream_t s);
+// ... with input row i at in + (i / in_rb) * in_bstride + (i % in_rb) * in_stride
+// + in_off (e.g. the R pilot rows of every frame of a batch in one launch).
+hipError_t launch_fft_any_b(const float2 *in, long long in_stride, long long in_rb, long long in_bstride,
+                            int in_off, float2 *out, long long out_stride, int out_off, long long nrows, int C,
+                            bool inverse, float scale, hipStream_t s);
 bool fft_any_supported(int C);
+// Fused any-C MRC (fft_any.hip k_mrc_any): data symbols of frames
+// iq + f*S*R*(C+prefix) (symbols 1..S-1) against the staged estimate in the
+// bin layout (Hc [F][R][C], P [F][C]); mode 0: out[q][out_pos_any(j)] =
+// sum_r Y*Hc / P, mode 1: out[q][j] = sum_r Y*Hc.
+hipError_t launch_mrc_any(const float2 *iq, long long nframes, int S, int R, int C, int prefix, const float2 *Hc,
+                          const float *P, float2 *out, int mode, hipStream_t s);
 
 // LS channel estimate on frequency-domain pilot symbols.
 // Pilot of frame f: Y + f*frame_stride, R rows of C bins.
