@@ -33,6 +33,7 @@
 // elements of a prefetched row group.
 #include "common.hpp"
 #include "launch.hpp"
+#include "pk.hpp"
 
 namespace ofdm {
 namespace fany {
@@ -96,24 +97,24 @@ __device__ __forceinline__ void fill_tables(float2 *lo, float2 *hi, unsigned C) 
 
 // radices 2, 4, 8: in-register FFT (compile-time twiddles);
 // 3, 5, 7: direct DFT with the roots r[j] = W_p^j in registers
+// (packed f32: pk.hpp; the inverse 2/4/8-point FFT as conj(FFT(conj(a))))
 template <int P, bool INV>
 __device__ __forceinline__ void dft_small(float2 (&a)[P], const float2 (&r)[P]) {
+    pk::v2f v[P];
+#pragma unroll
+    for (int t = 0; t < P; ++t) v[t] = pk::V(INV && (P == 2 || P == 4 || P == 8) ? float2{a[t].x, -a[t].y} : a[t]);
     if constexpr (P == 2 || P == 4 || P == 8) {
-        fft_reg<P, INV>(a);
+        pk::fft_reg<P>(v);
+#pragma unroll
+        for (int t = 0; t < P; ++t) a[t] = INV ? float2{v[t].x, -v[t].y} : pk::F(v[t]);
     } else {
-        float2 y[P];
 #pragma unroll
         for (int k = 0; k < P; ++k) {
-            float2 s = a[0];
+            pk::v2f s = v[0];
 #pragma unroll
-            for (int t = 1; t < P; ++t) {
-                const float2 w = r[(t * k) % P];
-                s = float2{s.x + (a[t].x * w.x - a[t].y * w.y), s.y + (a[t].x * w.y + a[t].y * w.x)};
-            }
-            y[k] = s;
+            for (int t = 1; t < P; ++t) pk::mac(s, v[t], pk::V(r[(t * k) % P]));
+            a[k] = pk::F(s);
         }
-#pragma unroll
-        for (int k = 0; k < P; ++k) a[k] = y[k];
     }
 }
 
@@ -123,8 +124,9 @@ __device__ __forceinline__ void dft_small(float2 (&a)[P], const float2 (&r)[P]) 
 template <int P, bool INV>
 __device__ __forceinline__ void twiddle_powers(float2 (&a)[P], const Tw &T, unsigned e) {
     if constexpr (P > 1) {
-        const float2 w1 = twv<INV>(T, e);
-        float2 w[8];
+        using pk::cmul;
+        const pk::v2f w1 = pk::V(twv<INV>(T, e));
+        pk::v2f w[8];
         w[1] = w1;
         if constexpr (P > 2) w[2] = cmul(w1, w1);
         if constexpr (P > 3) w[3] = cmul(w1, w[2]);
@@ -133,7 +135,7 @@ __device__ __forceinline__ void twiddle_powers(float2 (&a)[P], const Tw &T, unsi
         if constexpr (P > 6) w[6] = cmul(w[2], w[4]);
         if constexpr (P > 7) w[7] = cmul(w[3], w[4]);
 #pragma unroll
-        for (int t = 1; t < P; ++t) a[t] = cmul(a[t], w[t]);
+        for (int t = 1; t < P; ++t) a[t] = pk::F(cmul(pk::V(a[t]), w[t]));
     }
 }
 
@@ -145,7 +147,6 @@ __device__ __forceinline__ void stage_small(const float2 *src, float2 *dst, cons
     float2 r[P];
 #pragma unroll
     for (int j = 0; j < P; ++j) r[j] = (P == 3 || P == 5 || P == 7) ? twv<INV>(T, j * cp) : float2{1.f, 0.f};
-#pragma unroll 2
     for (unsigned bb = threadIdx.x; bb < nb; bb += NT) {
         const unsigned g = fdiv(bb, st.cp), b = bb - g * cp, m = fdiv(b, st.Lp), k1 = b - m * Lp;
         const unsigned s0 = g * C + b;
@@ -323,9 +324,9 @@ __device__ __forceinline__ void last_mac(const float2 *src, const Tw &T, unsigne
                 dft_small<P, false>(a, r);
 #pragma unroll
                 for (int k2 = 0; k2 < P; ++k2) {
-                    float2 &z = acc[j * P + k2];
-                    z = float2{z.x + (a[k2].x * h[k2].x - a[k2].y * h[k2].y),
-                               z.y + (a[k2].x * h[k2].y + a[k2].y * h[k2].x)};
+                    pk::v2f z = pk::V(acc[j * P + k2]);
+                    pk::mac(z, pk::V(a[k2]), pk::V(h[k2]));
+                    acc[j * P + k2] = pk::F(z);
                 }
             }
         }
@@ -483,33 +484,59 @@ k_mrc_any(const float2 *__restrict__ iq, long long nframes, int S, int R, int pr
     }
 }
 
-// radices in stage order: 8s, then 4, 2, then the odd primes ascending
+// Radices in stage order: primes above 8 first (their direct stages are
+// the slowest; never the fused last stage), then 8s, 7, 5, 4, 3, 2 -- the
+// smallest last, so that the fused last stage of k_mrc_any has the most
+// butterflies (C / p_last) to spread over the threads; a pure power of 8
+// ends in 4 x 2 instead of 8 for the same reason.
 bool make_plan(int C, Plan &pl) {
     if (C < 2 || C > FFT_ANY_MAX) return false;
     pl.C = C;
     pl.G = cap_of(C) / C;
     pl.ns = 0;
     pl.dC = make_fdiv((unsigned)C);
-    int n = C, Lp = 1;
-    auto push = [&](int p) {
-        if (pl.ns >= MAX_STAGES) return false;
+    int f[32], nf = 0, n = C;
+    int c2 = 0, c3 = 0, c5 = 0, c7 = 0;
+    while (n % 2 == 0) { n /= 2; ++c2; }
+    while (n % 3 == 0) { n /= 3; ++c3; }
+    while (n % 5 == 0) { n /= 5; ++c5; }
+    while (n % 7 == 0) { n /= 7; ++c7; }
+    int big[16], nbig = 0;  // prime factors above 7
+    for (int p = 11; n > 1; p += 2) {
+        if (p * p > n) p = n;
+        while (n % p == 0) {
+            if (nbig == 16) return false;
+            big[nbig++] = p;
+            n /= p;
+        }
+    }
+    for (int i = 0; i < nbig; ++i) f[nf++] = big[i];
+    int tail2 = 0;  // radices 4 / 2 that follow the 8s
+    if (c2 % 3 == 0 && c2 > 0 && c3 + c5 + c7 == 0) {  // pure power of 8 beside primes > 8 only
+        for (int i = 0; i < c2 / 3 - 1; ++i) f[nf++] = 8;
+        tail2 = 3;
+    } else {
+        for (int i = 0; i < c2 / 3; ++i) f[nf++] = 8;
+        tail2 = c2 % 3;
+    }
+    for (int i = 0; i < c7; ++i) f[nf++] = 7;
+    for (int i = 0; i < c5; ++i) f[nf++] = 5;
+    if (tail2 == 2) f[nf++] = 4;
+    if (tail2 == 3) f[nf++] = 4;
+    for (int i = 0; i < c3; ++i) f[nf++] = 3;
+    if (tail2 == 1 || tail2 == 3) f[nf++] = 2;
+    if (nf > MAX_STAGES) return false;
+    int Lp = 1;
+    for (int i = 0; i < nf; ++i) {
+        const int p = f[i];
         const FDiv d[3] = {make_fdiv((unsigned)(C / p)), make_fdiv((unsigned)Lp), make_fdiv((unsigned)(Lp * p))};
         for (int k = 0; k < 3; ++k) {
             pl.m[k][pl.ns] = d[k].m;
             pl.l[k][pl.ns] = d[k].l;
         }
         pl.p[pl.ns++] = p;
-        n /= p;
         Lp *= p;
-        return true;
-    };
-    while (n % 8 == 0)
-        if (!push(8)) return false;
-    if (n % 4 == 0 && !push(4)) return false;
-    if (n % 2 == 0 && !push(2)) return false;
-    for (int p = 3; n > 1; p += 2)
-        while (n % p == 0)
-            if (!push(p)) return false;
+    }
     return true;
 }
 
