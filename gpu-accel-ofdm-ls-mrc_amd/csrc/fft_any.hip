@@ -78,6 +78,12 @@ struct Tw {
     const float2 *lo, *hi;
 };
 
+// Workgroup barrier that orders LDS only.  __syncthreads() also drains every
+// outstanding global load (s_waitcnt vmcnt(0)), which would wait for the next
+// row group's prefetch at the first stage barrier: the prefetch would never
+// overlap the stages (measured: ~1 TB/s with it, all rows waiting on HBM).
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 template <bool INV>
 __device__ __forceinline__ float2 twv(const Tw &T, unsigned e) {
     const float2 w = cmul(T.lo[e & (TLO - 1)], T.hi[e / TLO]);
@@ -214,7 +220,7 @@ __device__ __forceinline__ float2 *run_stages(float2 *x0, float2 *x1, const Tw &
         case 8: stage_small<8, NT, INV>(a, b, T, C, G, Lp, st); break;
         default: stage_any<NT, INV>(a, b, T, C, G, Lp, p, st, plan.dC); break;
         }
-        __syncthreads();
+        lds_sync();
         float2 *t = a;
         a = b;
         b = t;
@@ -280,7 +286,7 @@ k_fft_any(const float2 *__restrict__ in, long long in_stride, long long in_rb, l
         const unsigned n = rows_of(grp);
 #pragma unroll
         for (int i = 0; i < MAXE; ++i) x0[threadIdx.x + i * NT] = pf[i];
-        __syncthreads();
+        lds_sync();
         const long long nxt = grp + gridDim.x;
         if (nxt < ngroups) load_rows_b<NT, MAXE>(pf, in, nxt * G, in_stride, in_rb, in_bstride, C, plan.dC, rows_of(nxt));
         const float2 *res = run_stages<NT, INV>(x0, x1, T, plan, n, plan.ns);
@@ -290,7 +296,7 @@ k_fft_any(const float2 *__restrict__ in, long long in_stride, long long in_rb, l
             const float2 v = res[e];
             dst[g * out_stride + (e - g * C)] = float2{v.x * scale, v.y * scale};
         }
-        __syncthreads();  // the next group's rows go into x0
+        lds_sync();  // the next group's rows go into x0
     }
 }
 
@@ -431,7 +437,7 @@ k_mrc_any(const float2 *__restrict__ iq, long long nframes, int S, int R, int pr
         const unsigned n = rows_in(gi);
 #pragma unroll
         for (int i = 0; i < MAXE; ++i) x0[threadIdx.x + i * NT] = pf[i];
-        __syncthreads();
+        lds_sync();
         long long qn = q, fn = f;
         int sn = s, gn = gi + 1;
         if (gn == ngr) {
@@ -456,7 +462,7 @@ k_mrc_any(const float2 *__restrict__ iq, long long nframes, int S, int R, int pr
         case 8: last_mac<8, NT>(y, T, Cl, n, H, acc); break;
         default: last_mac_any<NT>(y, T, Cl, n, (unsigned)pl, H, acc); break;
         }
-        __syncthreads();  // the next group's rows go into x0
+        lds_sync();  // the next group's rows go into x0
         if (gn == 0) {    // symbol q complete
             float2 *o = out + q * K;
             const float *Pf = P + f * C;
