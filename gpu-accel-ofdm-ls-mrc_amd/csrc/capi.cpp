@@ -49,6 +49,9 @@ size_t up256(size_t x) { return (x + 255) & ~size_t(255); }
 
 // fused one-pass kernels exist for these FFT sizes
 bool fused_c(int C) { return C == 1024 || C == 2048 || C == 4096; }
+// sizes whose workspace estimate is in a receiver's lane order: the fused
+// ones and C = 1536 (staged pilot FFT, then k_ls_1536 / k_mrc_td1536)
+bool lane_c(int C) { return fused_c(C) || C == 1536; }
 
 // fused time-domain kernels by C (fused_c(C) must hold)
 hipError_t ls_fused(const float2 *iq, long long F, int S, int R, int C, int prefix, const float2 *X,
@@ -214,12 +217,16 @@ int td_staged(const float2 *iq, long long F, int S, int R, int C, int prefix, co
             e = ofdm::launch_fft_any_b(iq + f0 * frame_in, C + prefix, R, frame_in, prefix, w.staging, C, 0, n * R,
                                        C, false, 1.f, s);
             if (e != hipSuccess) return hip_check(e, "fft (pilot rows)");
-            e = ofdm::launch_ls_freq(w.staging, pilot, n, R, C, X, w.Hc + f0 * pilot, pilot, C, 1, w.P + f0 * C, C,
-                                     1, s);
+            e = C == 1536 ? ofdm::launch_ls_1536(w.staging, n, R, X, w.Hc + f0 * pilot, w.P + f0 * C, s)
+                          : ofdm::launch_ls_freq(w.staging, pilot, n, R, C, X, w.Hc + f0 * pilot, pilot, C, 1,
+                                                 w.P + f0 * C, C, 1, s);
             if (e != hipSuccess) return hip_check(e, "ls_freq");
         }
     }
     if (mode == 2) return OFDM_OK;
+    if (C == 1536)
+        return hip_check(ofdm::launch_mrc_td1536(iq, F, S, R, prefix, w.Hc, w.P, out, mode == 1 ? 1 : 0, s),
+                         "mrc_td1536");
     return hip_check(ofdm::launch_mrc_any(iq, F, S, R, C, prefix, w.Hc, w.P, out, mode == 1 ? 1 : 0, s),
                      "mrc_any");
 }
@@ -383,7 +390,7 @@ int ofdm_frame_estimate(const ofdm_cf32 *d_iq, long long nframes, int S, int R, 
         rc = hip_check(ls_fused(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w.Hc, w.P, 0, s), "ls_fused");
     else
         rc = td_staged(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w, nullptr, 2, s);
-    if (rc == OFDM_OK) ws_record(d_ws, ws_bytes_, nframes, S, R, C, fused_c(C), false);
+    if (rc == OFDM_OK) ws_record(d_ws, ws_bytes_, nframes, S, R, C, lane_c(C), false);
     return rc;
 }
 
@@ -394,7 +401,7 @@ int ofdm_frame_combine(const ofdm_cf32 *d_iq, long long nframes, int S, int R, i
     if (nframes == 0) return OFDM_OK;
     WsTag tag;
     if ((rc = ws_check(d_ws, ws_bytes_, nframes, S, R, C, true, "ofdm_frame_combine", &tag))) return rc;
-    if (tag.lane_order != fused_c(C))
+    if (tag.lane_order != lane_c(C))
         return fail(OFDM_E_ARG, "ofdm_frame_combine: the workspace holds a frequency-domain estimate "
                                 "(use ofdm_frame_combine_freq)");
     Workspace w;
@@ -444,7 +451,7 @@ int ofdm_frame_demod_ex(const ofdm_cf32 *d_iq, long long nframes, int S, int R, 
         return hip_check(mrc_fused(F2(d_iq), nframes, S, R, C, prefix, w.Hc, w.P, F2(d_out), 0, s), "mrc_fused");
     }
     rc = td_staged(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w, F2(d_out), 0, s);
-    if (rc == OFDM_OK) ws_record(d_ws, ws_bytes_, nframes, S, R, C, false, false);
+    if (rc == OFDM_OK) ws_record(d_ws, ws_bytes_, nframes, S, R, C, lane_c(C), false);
     return rc;
 }
 
@@ -532,7 +539,7 @@ int ofdm_frame_ls_partial(const ofdm_cf32 *d_iq, long long nframes, int S, int R
     else
         rc = td_staged(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w, nullptr, 2, s);
     if (rc) return rc;
-    ws_record(d_ws, ws_bytes_, nframes, S, R, C, fused_c(C), true);
+    ws_record(d_ws, ws_bytes_, nframes, S, R, C, lane_c(C), true);
     // bins 1..C-1 of the bin-layout P -> [F][K]
     const int K = C - 1;
     return hip_check(hipMemcpy2DAsync(d_P, K * sizeof(float), w.P + 1, C * sizeof(float),
@@ -548,7 +555,7 @@ int ofdm_frame_mrc_partial(const ofdm_cf32 *d_iq, long long nframes, int S, int 
     if (nframes == 0) return OFDM_OK;
     WsTag tag;
     if ((rc = ws_check(d_ws, ws_bytes_, nframes, S, R, C, false, "ofdm_frame_mrc_partial", &tag))) return rc;
-    if (tag.lane_order != fused_c(C))
+    if (tag.lane_order != lane_c(C))
         return fail(OFDM_E_ARG, "ofdm_frame_mrc_partial: the workspace holds a frequency-domain estimate, "
                                 "not the time-domain one of ofdm_frame_ls_partial / ofdm_frame_estimate");
     Workspace w;

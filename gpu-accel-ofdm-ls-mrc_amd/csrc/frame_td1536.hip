@@ -1,0 +1,221 @@
+// frame_td1536.hip -- fused MRC for C = 1536 (LTE's 15 MHz FFT size, the most
+// common length that is not a power of two): one HBM pass over the IQ, as the
+// power-of-two receivers (demodOneFrameCUDA, gpuLS.cu:575-675, without its
+// cuFFT round trips), replacing the generic any-C kernel (fft_any.hip) at
+// this size.
+//
+// One 64-lane wave transforms one 1536-sample antenna row held in registers,
+// 24 samples per lane (lane t: x[t + 64 m'], m' < 24):
+//   * radix-3 decimation in frequency in registers: for n = t + 64 m (m < 8)
+//     u_j[n] = W1536^{n j} sum_i x[n + 512 i] W3^{i j},  j < 3,
+//     so that X[3 k + j] = FFT512(u_j)[k];
+//   * each FFT512 as 8 x 8 x 8 with two wave-local LDS transposes: pass A a
+//     DFT8 over m per lane (then W512^{t s}), transpose, pass B1 a DFT8 over b
+//     (t = a + 8 b; then W64^{a c}), transpose, pass B2 a DFT8 over a:
+//     lane L = 8 s + c ends with X512[s + 8 c + 64 d], d < 8;
+//   * packed f32 complex arithmetic (pk.hpp); the per-lane twiddles of passes
+//     A and B1 are row invariants held in registers, the DIF twiddles come
+//     from a W1536 table in LDS.
+// Lane L therefore owns the 24 bins 3 (s + 8 c + 64 d) + j, slot i = 8 j + d.
+// The channel estimate is kept in that "lane order" (k_ls_1536 writes it:
+// per (frame, antenna) slot i of lane L at i * 64 + L, one coalesced 512-B
+// wave load per slot); P stays bin-indexed [F][C].  A wave owns one data
+// symbol at a time and walks its R rows in order (matrixMultThenSum order,
+// cpuLS.hpp:187-208), the next row's 24 samples in flight during the current
+// row's transform; no workgroup barrier after the table fill.
+#include "common.hpp"
+#include "launch.hpp"
+#include "pk.hpp"
+
+namespace ofdm {
+namespace td1536 {
+
+using pk::v2f;
+constexpr int C = 1536, K = C - 1;
+constexpr int PA = 72;               // transpose image: 8 rows of 64 + 8 (conflict-free reads)
+constexpr int TS = 8 * PA;           // per-wave image, 4.5 KiB
+constexpr int WAVES = 4;
+constexpr int NT = 64 * WAVES;
+
+__device__ __forceinline__ void wsync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// bin of lane L's slot i (i = 8 j + d)
+__device__ __forceinline__ int bin_of(int L, int i) {
+    return 3 * ((L >> 3) + 8 * (L & 7) + 64 * (i & 7)) + (i >> 3);
+}
+
+// FFT512 of v (lane t: v[m] = u[t + 64 m]) -> v[d] = U[s + 8 c + 64 d], L = 8 s + c
+__device__ __forceinline__ void fft512(v2f (&v)[8], float2 *T, int L, const v2f (&twA)[7], const v2f (&twB)[7]) {
+    pk::fft_reg<8>(v);  // over m -> s
+#pragma unroll
+    for (int s = 1; s < 8; ++s) v[s] = pk::cmul(v[s], twA[s - 1]);
+    wsync();
+#pragma unroll
+    for (int s = 0; s < 8; ++s) T[s * PA + L] = pk::F(v[s]);
+    wsync();
+    const int s = L >> 3, a = L & 7;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) v[b] = pk::V(T[s * PA + a + 8 * b]);
+    pk::fft_reg<8>(v);  // over b -> c
+#pragma unroll
+    for (int c = 1; c < 8; ++c) v[c] = pk::cmul(v[c], twB[c - 1]);
+    wsync();
+#pragma unroll
+    for (int c = 0; c < 8; ++c) T[s * PA + 9 * c + a] = pk::F(v[c]);
+    wsync();
+    const int c = L & 7;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = pk::V(T[s * PA + 9 * c + q]);
+    pk::fft_reg<8>(v);  // over a -> d
+}
+
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
+k_mrc_td1536(const float2 *__restrict__ iq, long long nframes, int S, int R, int prefix, const float2 *__restrict__ Hl,
+             const float *__restrict__ P, float2 *__restrict__ out, int mode) {
+    __shared__ float2 tab[C];             // W1536^e
+    __shared__ float2 img[WAVES][TS];     // per-wave transpose images
+    for (int e = threadIdx.x; e < C; e += NT) {
+        double sn, cs;
+        sincospi(-2.0 * (double)e / (double)C, &sn, &cs);
+        tab[e] = float2{(float)cs, (float)sn};
+    }
+    __syncthreads();
+    const int w = threadIdx.x >> 6, L = threadIdx.x & 63;
+    float2 *T = img[w];
+    // row invariants: W512^{t s} = W1536^{3 t s} (t = L), W64^{a c} = W1536^{24 a c} (a = L & 7)
+    v2f twA[7], twB[7];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) {
+        twA[k - 1] = pk::V(tab[(3 * L * k) % C]);
+        twB[k - 1] = pk::V(tab[(24 * (L & 7) * k) % C]);
+    }
+    const int nsd = S - 1;
+    const long long Cp = C + prefix, nq = nframes * nsd, nw = (long long)gridDim.x * WAVES;
+    const float r3 = 0.86602540378443865f;  // sin(2 pi / 3)
+    auto row_ptr = [&](long long q, int r) {
+        const long long f = q / nsd, s = 1 + q % nsd;
+        return iq + ((f * S + s) * R + r) * Cp + prefix;
+    };
+    float2 x[24];
+    long long q = (long long)blockIdx.x * WAVES + w;
+    if (q < nq) {
+        const float2 *b = row_ptr(q, 0);
+#pragma unroll
+        for (int m = 0; m < 24; ++m) x[m] = b[L + 64 * m];
+    }
+    for (; q < nq; q += nw) {
+        const long long f = q / nsd;
+        v2f acc[24];
+#pragma unroll
+        for (int i = 0; i < 24; ++i) acc[i] = v2f{0.f, 0.f};
+        for (int r = 0; r < R; ++r) {
+            // radix-3 DIF in registers
+            v2f u[3][8];
+#pragma unroll
+            for (int m = 0; m < 8; ++m) {
+                const v2f a0 = pk::V(x[m]), a1 = pk::V(x[m + 8]), a2 = pk::V(x[m + 16]);
+                const v2f sm = a1 + a2, df = a1 - a2;
+                const v2f t0 = a0 - sm * (v2f){0.5f, 0.5f};
+                const v2f jd = v2f{df.y * r3, -df.x * r3};  // -i sin(2 pi/3) (a1 - a2)
+                const int n = L + 64 * m;
+                u[0][m] = a0 + sm;
+                u[1][m] = pk::cmul(t0 + jd, pk::V(tab[n]));
+                u[2][m] = pk::cmul(t0 - jd, pk::V(tab[2 * n]));
+            }
+            // the next row (or the next symbol's first) in flight during the transforms
+            {
+                const long long qn = r + 1 < R ? q : q + nw;
+                if (qn < nq) {
+                    const float2 *b = row_ptr(qn, r + 1 < R ? r + 1 : 0);
+#pragma unroll
+                    for (int m = 0; m < 24; ++m) x[m] = b[L + 64 * m];
+                }
+            }
+            const float2 *hrow = Hl + (f * R + r) * (long long)C;
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                v2f h[8];
+#pragma unroll
+                for (int d = 0; d < 8; ++d) h[d] = pk::V(hrow[(8 * j + d) * 64 + L]);
+                fft512(u[j], T, L, twA, twB);
+#pragma unroll
+                for (int d = 0; d < 8; ++d) pk::mac(acc[8 * j + d], u[j][d], h[d]);
+            }
+        }
+        float2 *o = out + q * K;
+        const float *Pf = P + f * C;
+#pragma unroll
+        for (int i = 0; i < 24; ++i) {
+            const int b = bin_of(L, i);
+            if (b == 0) continue;  // the DC bin carries no subcarrier
+            const float2 a = pk::F(acc[i]);
+            if (mode == 0) {
+                const float p = Pf[b];
+                o[out_pos(b - 1, K)] = float2{a.x / p, a.y / p};
+            } else {
+                o[b - 1] = a;
+            }
+        }
+    }
+}
+
+// LS from the FFT'd pilot rows (staging, bin order, frame stride R C):
+// Hc = conj(Y / X) in lane order, P = sum_r |Hc|^2 (rows in order, bin layout
+// with P[0] = 1 and a zero DC estimate), findHs + findDistSqrd
+// (gpuLS.cu:158-209, cpuLS.hpp:211-244) as k_ls_freq.
+__global__ void __launch_bounds__(256) k_ls_1536(const float2 *__restrict__ Y, int R, const float2 *__restrict__ X,
+                                                 float2 *__restrict__ Hl, float *__restrict__ P, int partial) {
+    const int b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= C) return;
+    const long long f = blockIdx.y;
+    const int k = b / 3, j = b - 3 * k, L = 8 * (k & 7) + ((k >> 3) & 7), i = 8 * j + (k >> 6);
+    const float2 *Yf = Y + f * (long long)R * C;
+    float2 *Hf = Hl + f * (long long)R * C + i * 64 + L;
+    float p = 0.f;
+    if (b == 0) {
+        for (int r = 0; r < R; ++r) Hf[(long long)r * C] = float2{0.f, 0.f};
+        p = 1.f;
+    } else {
+        const float2 x = X[b - 1];
+        for (int r = 0; r < R; ++r) {
+            const float2 h = ls_conj(Yf[(long long)r * C + b], x);
+            Hf[(long long)r * C] = h;
+            p = (r == 0) ? (h.x * h.x) + (h.y * h.y) : p + (h.x * h.x) + (h.y * h.y);
+        }
+    }
+    (void)partial;
+    P[f * C + b] = p;
+}
+
+}  // namespace td1536
+
+hipError_t launch_ls_1536(const float2 *Y, long long nframes, int R, const float2 *X, float2 *Hl, float *P,
+                          hipStream_t s) {
+    if (nframes <= 0) return hipSuccess;
+    for (long long f0 = 0; f0 < nframes; f0 += 65535) {
+        const long long n = nframes - f0 < 65535 ? nframes - f0 : 65535;
+        hipLaunchKernelGGL(td1536::k_ls_1536, dim3((td1536::C + 255) / 256, (unsigned)n), dim3(256), 0, s,
+                           Y + f0 * (long long)R * td1536::C, R, X, Hl + f0 * (long long)R * td1536::C,
+                           P + f0 * td1536::C, 0);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_mrc_td1536(const float2 *iq, long long nframes, int S, int R, int prefix, const float2 *Hl,
+                             const float *P, float2 *out, int mode, hipStream_t s) {
+    const long long nq = nframes * (S - 1);
+    if (nq <= 0) return hipSuccess;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
+    const long long res = 2ll * cus, need = (nq + td1536::WAVES - 1) / td1536::WAVES;
+    hipLaunchKernelGGL(td1536::k_mrc_td1536, dim3((unsigned)(need < res ? need : res)), dim3(td1536::NT), 0, s, iq,
+                       nframes, S, R, prefix, Hl, P, out, mode);
+    return hipGetLastError();
+}
+
+}  // namespace ofdm

@@ -51,6 +51,12 @@ hipError_t launch_fft_any_b(const float2 *in, long long in_stride, long long in_
                             int in_off, float2 *out, long long out_stride, int out_off, long long nrows, int C,
                             bool inverse, float scale, hipStream_t s);
 bool fft_any_supported(int C);
+// C = 1536 (frame_td1536.hip): LS from FFT'd pilot rows (staging, frame
+// stride R*C) into the lane-order Hc + bin-layout P, and the fused MRC.
+hipError_t launch_ls_1536(const float2 *Y, long long nframes, int R, const float2 *X, float2 *Hl, float *P,
+                          hipStream_t s);
+hipError_t launch_mrc_td1536(const float2 *iq, long long nframes, int S, int R, int prefix, const float2 *Hl,
+                             const float *P, float2 *out, int mode, hipStream_t s);
 // Fused any-C MRC (fft_any.hip k_mrc_any): data symbols of frames
 // iq + f*S*R*(C+prefix) (symbols 1..S-1) against the staged estimate in the
 // bin layout (Hc [F][R][C], P [F][C]); mode 0: out[q][out_pos_any(j)] =

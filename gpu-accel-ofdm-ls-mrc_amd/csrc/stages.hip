@@ -71,7 +71,7 @@ __device__ __forceinline__ int lane_of(int b, int &k) {  // b < 1024
     k = (b >> 4) & 15;
     return 4 * q + (((c & 1) << 1) | (c >> 1));
 }
-__device__ __forceinline__ int hc_pos(int b, int C) {  // C = 0: bin layout
+__device__ __forceinline__ int hc_pos(int b, int C) {  // C = 0: bin layout (b < C <= 4096)
     int k;
     if (C == 1024) {  // float4 (k >> 1) * 64 + t holds bins (k & ~1, k | 1) of lane t
         const int t = lane_of(b, k);
@@ -80,6 +80,10 @@ __device__ __forceinline__ int hc_pos(int b, int C) {  // C = 0: bin layout
     if (C == 2048) {  // float4 k * 64 + t = (Hc[2 b'], Hc[2 b' + 1]), b' = b0(t) + 16 k
         const int t = lane_of(b >> 1, k);
         return 2 * (k * 64 + t) + (b & 1);
+    }
+    if (C == 1536) {  // frame_td1536.hip: slot 8 j + d of lane 8 s + c holds bin 3 (s + 8 c + 64 d) + j
+        const int q = b / 3, j = b - 3 * q;
+        return (8 * j + (q >> 6)) * 64 + 8 * (q & 7) + ((q >> 3) & 7);
     }
     if (C == 4096) {  // float2 e * 2048 + h * 1024 + k * 64 + t = Hc[4 b' + 2 h + e]
         const int t = lane_of(b >> 2, k);

@@ -111,3 +111,35 @@ def test_stages_any_c_vs_oracle(ofdm, oracle, dev, C, R):
     rows = (rng.standard_normal((3, K)) + 1j * rng.standard_normal((3, K))).astype(np.complex64)
     assert np.array_equal(host(ofdm.shift_rows(to_dev(rows, dev))),
                           np.stack([oracle.shift_one_row(r) for r in rows]))
+
+
+@pytest.mark.parametrize("C,R,prefix", [(1536, 6, 16), (1200, 3, 0)])
+def test_estimate_export_and_antenna_partials_any_c(ofdm, oracle, dev, C, R, prefix):
+    """The estimate of a non-fused size (C = 1536: the lane order of
+    frame_td1536.hip; 1200: the bin layout) exported to the reference layout
+    matches the oracle's LS; the antenna-split partials (numerators + |H|^2)
+    summed over two shards and finalised give the full receiver's output."""
+    F, S = 2, 4
+    X = to_dev(qpsk(C - 1), dev)
+    iq = ofdm.synth_frames(F, S, R, C, X, prefix=prefix, seed=C + 3)
+    ws = ofdm.workspace(F, S, R, C, dev)
+    ofdm.frame_estimate(iq, X, prefix, ws)
+    H, P = ofdm.frame_export_estimate(ws, F, S, R, C, frame=1)
+    Y0 = oracle.fft_rows(host(iq)[1, 0, :, prefix:])
+    H_ref, P_ref = oracle.ls(Y0, host(X))
+    parity(host(H), H_ref)
+    parity(host(P), P_ref)
+    full = host(ofdm.frame_demod(iq, X, prefix))
+    import torch
+    num, psum = None, None
+    for r0, r1 in ((0, R // 2), (R // 2, R)):
+        part = iq[:, :, r0:r1].contiguous()
+        Pp, wsp = ofdm.frame_ls_partial(part, X, prefix)
+        n = ofdm.frame_mrc_partial(part, wsp, prefix)
+        num = n if num is None else num + n
+        psum = Pp if psum is None else psum + Pp
+    K = C - 1
+    out = ofdm.c64((F, S - 1, K), dev)
+    ofdm.mrc_finalize(num.reshape(-1), 0, S - 1, K, psum.reshape(-1).contiguous(), out)
+    torch.cuda.synchronize()
+    parity(host(out), full)
