@@ -50,8 +50,9 @@ size_t up256(size_t x) { return (x + 255) & ~size_t(255); }
 // fused one-pass kernels exist for these FFT sizes
 bool fused_c(int C) { return C == 1024 || C == 2048 || C == 4096; }
 // sizes whose workspace estimate is in a receiver's lane order: the fused
-// ones and C = 1536 (staged pilot FFT, then k_ls_1536 / k_mrc_td1536)
-bool lane_c(int C) { return fused_c(C) || C == 1536; }
+// ones and C = 1536 / 3072 (staged pilot FFT, then k_ls_1536 / k_mrc_td1536,
+// k_ls_3072 / k_mrc_td3072: frame_td1536.hip)
+bool lane_c(int C) { return fused_c(C) || C == 1536 || C == 3072; }
 
 // fused time-domain kernels by C (fused_c(C) must hold)
 hipError_t ls_fused(const float2 *iq, long long F, int S, int R, int C, int prefix, const float2 *X,
@@ -217,9 +218,10 @@ int td_staged(const float2 *iq, long long F, int S, int R, int C, int prefix, co
             e = ofdm::launch_fft_any_b(iq + f0 * frame_in, C + prefix, R, frame_in, prefix, w.staging, C, 0, n * R,
                                        C, false, 1.f, s);
             if (e != hipSuccess) return hip_check(e, "fft (pilot rows)");
-            e = C == 1536 ? ofdm::launch_ls_1536(w.staging, n, R, X, w.Hc + f0 * pilot, w.P + f0 * C, s)
-                          : ofdm::launch_ls_freq(w.staging, pilot, n, R, C, X, w.Hc + f0 * pilot, pilot, C, 1,
-                                                 w.P + f0 * C, C, 1, s);
+            e = C == 1536   ? ofdm::launch_ls_1536(w.staging, n, R, X, w.Hc + f0 * pilot, w.P + f0 * C, s)
+                : C == 3072 ? ofdm::launch_ls_3072(w.staging, n, R, X, w.Hc + f0 * pilot, w.P + f0 * C, s)
+                            : ofdm::launch_ls_freq(w.staging, pilot, n, R, C, X, w.Hc + f0 * pilot, pilot, C, 1,
+                                                   w.P + f0 * C, C, 1, s);
             if (e != hipSuccess) return hip_check(e, "ls_freq");
         }
     }
@@ -227,6 +229,9 @@ int td_staged(const float2 *iq, long long F, int S, int R, int C, int prefix, co
     if (C == 1536)
         return hip_check(ofdm::launch_mrc_td1536(iq, F, S, R, prefix, w.Hc, w.P, out, mode == 1 ? 1 : 0, s),
                          "mrc_td1536");
+    if (C == 3072)
+        return hip_check(ofdm::launch_mrc_td3072(iq, F, S, R, prefix, w.Hc, w.P, out, mode == 1 ? 1 : 0, s),
+                         "mrc_td3072");
     return hip_check(ofdm::launch_mrc_any(iq, F, S, R, C, prefix, w.Hc, w.P, out, mode == 1 ? 1 : 0, s),
                      "mrc_any");
 }

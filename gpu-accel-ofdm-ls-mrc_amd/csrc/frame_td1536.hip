@@ -193,6 +193,187 @@ __global__ void __launch_bounds__(256) k_ls_1536(const float2 *__restrict__ Y, i
 
 }  // namespace td1536
 
+// ---------------------------------------------------------------------------
+// C = 3072 (3 x 1024: NR's 3072-point FFT) on a wave PAIR per data symbol,
+// built from the same pieces: the radix-3 DIF in registers (each wave holds
+// n = t + 64 (m + 8 e), m < 8, of the first 1024 and its two partners n + 1024,
+// n + 2048: 24 samples per lane), then one radix-2 DIF step of the three
+// FFT1024s across the pair through LDS (v0 = u[n'] + u[n' + 512] on wave 0,
+// v1 = (u[n'] - u[n' + 512]) W1024^{n'} on wave 1), then three FFT512s per
+// wave (td1536::fft512).  Wave e, lane 8 s + c owns bins 3 (2 k' + e) + j,
+// k' = s + 8 c + 64 d, slot i = 8 j + d; the estimate in that lane order is
+// [e][slot][lane] per antenna row (k_ls_3072).  Two LDS barriers per row (the
+// exchange written / read); the exchange image of a wave doubles as its
+// transpose image once both have read it.
+namespace td3072 {
+
+using pk::v2f;
+constexpr int C = 3072, K = C - 1;
+constexpr int XS = 24 * 64;  // exchange image per wave (float2): [j][m][t]
+constexpr int NT = 128;      // one pair per workgroup
+static_assert(td1536::TS <= XS, "transpose image fits in the exchange image");
+
+__device__ __forceinline__ void pair_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__device__ __forceinline__ int bin_of(int e, int L, int i) {
+    return 3 * (2 * ((L >> 3) + 8 * (L & 7) + 64 * (i & 7)) + e) + (i >> 3);
+}
+
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
+k_mrc_td3072(const float2 *__restrict__ iq, long long nframes, int S, int R, int prefix, const float2 *__restrict__ Hl,
+             const float *__restrict__ P, float2 *__restrict__ out, int mode) {
+    __shared__ float2 tab[2048];   // W3072^e, e < 2048 (DIF twiddles n j, n < 1024, j <= 2)
+    __shared__ float2 xch[2][XS];  // per-wave exchange / transpose image
+    for (int e = threadIdx.x; e < 2048; e += NT) {
+        double sn, cs;
+        sincospi(-2.0 * (double)e / (double)C, &sn, &cs);
+        tab[e] = float2{(float)cs, (float)sn};
+    }
+    const int e = threadIdx.x >> 6, L = threadIdx.x & 63;
+    v2f twA[7], twB[7];  // W512^{t s}, W64^{a c}: the FFT512 row invariants
+#pragma unroll
+    for (int k = 1; k < 8; ++k) {
+        double sn, cs;
+        sincospi(-2.0 * (double)((L * k) % 512) / 512.0, &sn, &cs);
+        twA[k - 1] = v2f{(float)cs, (float)sn};
+        sincospi(-2.0 * (double)(((L & 7) * k) % 64) / 64.0, &sn, &cs);
+        twB[k - 1] = v2f{(float)cs, (float)sn};
+    }
+    __syncthreads();
+    float2 *own = xch[e], *oth = xch[e ^ 1];
+    const int nsd = S - 1;
+    const long long Cp = C + prefix, nq = nframes * nsd, np = gridDim.x;
+    const float r3 = 0.86602540378443865f;
+    auto row_ptr = [&](long long q, int r) {
+        const long long f = q / nsd, s = 1 + q % nsd;
+        return iq + ((f * S + s) * R + r) * Cp + prefix;
+    };
+    // lane L of wave e loads x[L + 64 (m + 8 e + 16 i)], m < 8, i < 3, into x[8 i + m]
+    auto load = [&](float2 (&x)[24], const float2 *b) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int m = 0; m < 8; ++m) x[8 * i + m] = b[L + 64 * (m + 8 * e + 16 * i)];
+    };
+    float2 x[24];
+    long long q = blockIdx.x;
+    if (q < nq) load(x, row_ptr(q, 0));
+    for (; q < nq; q += np) {
+        const long long f = q / nsd;
+        v2f acc[24];
+#pragma unroll
+        for (int i = 0; i < 24; ++i) acc[i] = v2f{0.f, 0.f};
+        for (int r = 0; r < R; ++r) {
+            v2f u[3][8];
+#pragma unroll
+            for (int m = 0; m < 8; ++m) {
+                const v2f a0 = pk::V(x[m]), a1 = pk::V(x[m + 8]), a2 = pk::V(x[m + 16]);
+                const v2f sm = a1 + a2, df = a1 - a2;
+                const v2f t0 = a0 - sm * (v2f){0.5f, 0.5f};
+                const v2f jd = v2f{df.y * r3, -df.x * r3};
+                const int n = L + 64 * (m + 8 * e);
+                u[0][m] = a0 + sm;
+                u[1][m] = pk::cmul(t0 + jd, pk::V(tab[n]));
+                u[2][m] = pk::cmul(t0 - jd, pk::V(tab[2 * n]));
+            }
+            {
+                const long long qn = r + 1 < R ? q : q + np;
+                if (qn < nq) load(x, row_ptr(qn, r + 1 < R ? r + 1 : 0));
+            }
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+#pragma unroll
+                for (int m = 0; m < 8; ++m) own[(8 * j + m) * 64 + L] = pk::F(u[j][m]);
+            pair_barrier();
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+#pragma unroll
+                for (int m = 0; m < 8; ++m) {
+                    const v2f p = pk::V(oth[(8 * j + m) * 64 + L]);
+                    // wave 0: u[n'] + u[n' + 512]; wave 1: (u[n'] - u[n' + 512]) W1024^{n'}, n' = L + 64 m
+                    u[j][m] = e == 0 ? u[j][m] + p : pk::cmul(p - u[j][m], pk::V(tab[3 * (L + 64 * m)]));
+                }
+            pair_barrier();  // both exchange images read: each becomes its wave's transpose image
+            const float2 *hrow = Hl + (f * R + r) * (long long)C + e * 1536;
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                v2f h[8];
+#pragma unroll
+                for (int d = 0; d < 8; ++d) h[d] = pk::V(hrow[(8 * j + d) * 64 + L]);
+                td1536::fft512(u[j], own, L, twA, twB);
+#pragma unroll
+                for (int d = 0; d < 8; ++d) pk::mac(acc[8 * j + d], u[j][d], h[d]);
+            }
+        }
+        float2 *o = out + q * K;
+        const float *Pf = P + f * C;
+#pragma unroll
+        for (int i = 0; i < 24; ++i) {
+            const int b = bin_of(e, L, i);
+            if (b == 0) continue;
+            const float2 a = pk::F(acc[i]);
+            if (mode == 0) {
+                const float p = Pf[b];
+                o[out_pos(b - 1, K)] = float2{a.x / p, a.y / p};
+            } else {
+                o[b - 1] = a;
+            }
+        }
+    }
+}
+
+// LS into the lane order of k_mrc_td3072 ([e][slot][lane] per antenna row)
+__global__ void __launch_bounds__(256) k_ls_3072(const float2 *__restrict__ Y, int R, const float2 *__restrict__ X,
+                                                 float2 *__restrict__ Hl, float *__restrict__ P) {
+    const int b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= C) return;
+    const long long f = blockIdx.y;
+    const int k = b / 3, j = b - 3 * k, kk = k >> 1, e = k & 1;
+    const int L = 8 * (kk & 7) + ((kk >> 3) & 7), i = 8 * j + (kk >> 6);
+    const float2 *Yf = Y + f * (long long)R * C;
+    float2 *Hf = Hl + f * (long long)R * C + e * 1536 + i * 64 + L;
+    float p = 0.f;
+    if (b == 0) {
+        for (int r = 0; r < R; ++r) Hf[(long long)r * C] = float2{0.f, 0.f};
+        p = 1.f;
+    } else {
+        const float2 x = X[b - 1];
+        for (int r = 0; r < R; ++r) {
+            const float2 h = ls_conj(Yf[(long long)r * C + b], x);
+            Hf[(long long)r * C] = h;
+            p = (r == 0) ? (h.x * h.x) + (h.y * h.y) : p + (h.x * h.x) + (h.y * h.y);
+        }
+    }
+    P[f * C + b] = p;
+}
+
+}  // namespace td3072
+
+hipError_t launch_ls_3072(const float2 *Y, long long nframes, int R, const float2 *X, float2 *Hl, float *P,
+                          hipStream_t s) {
+    if (nframes <= 0) return hipSuccess;
+    for (long long f0 = 0; f0 < nframes; f0 += 65535) {
+        const long long n = nframes - f0 < 65535 ? nframes - f0 : 65535;
+        hipLaunchKernelGGL(td3072::k_ls_3072, dim3((td3072::C + 255) / 256, (unsigned)n), dim3(256), 0, s,
+                           Y + f0 * (long long)R * td3072::C, R, X, Hl + f0 * (long long)R * td3072::C,
+                           P + f0 * td3072::C);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_mrc_td3072(const float2 *iq, long long nframes, int S, int R, int prefix, const float2 *Hl,
+                             const float *P, float2 *out, int mode, hipStream_t s) {
+    const long long nq = nframes * (S - 1);
+    if (nq <= 0) return hipSuccess;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
+    const long long res = 4ll * cus;  // 40 KiB of LDS and 2 waves per workgroup: 4 per CU
+    hipLaunchKernelGGL(td3072::k_mrc_td3072, dim3((unsigned)(nq < res ? nq : res)), dim3(td3072::NT), 0, s, iq,
+                       nframes, S, R, prefix, Hl, P, out, mode);
+    return hipGetLastError();
+}
+
 hipError_t launch_ls_1536(const float2 *Y, long long nframes, int R, const float2 *X, float2 *Hl, float *P,
                           hipStream_t s) {
     if (nframes <= 0) return hipSuccess;

@@ -85,6 +85,10 @@ __device__ __forceinline__ int hc_pos(int b, int C) {  // C = 0: bin layout (b <
         const int q = b / 3, j = b - 3 * q;
         return (8 * j + (q >> 6)) * 64 + 8 * (q & 7) + ((q >> 3) & 7);
     }
+    if (C == 3072) {  // wave e, slot 8 j + d of lane 8 s + c holds bin 3 (2 (s + 8 c + 64 d) + e) + j
+        const int q = b / 3, j = b - 3 * q, e = q & 1, kk = q >> 1;
+        return e * 1536 + (8 * j + (kk >> 6)) * 64 + 8 * (kk & 7) + ((kk >> 3) & 7);
+    }
     if (C == 4096) {  // float2 e * 2048 + h * 1024 + k * 64 + t = Hc[4 b' + 2 h + e]
         const int t = lane_of(b >> 2, k);
         return (b & 1) * 2048 + ((b >> 1) & 1) * 1024 + k * 64 + t;
