@@ -349,6 +349,163 @@ __global__ void __launch_bounds__(256) k_ls_3072(const float2 *__restrict__ Y, i
 
 }  // namespace td3072
 
+// ---------------------------------------------------------------------------
+// C = 6144 (3 x 2048) on a wave QUAD per data symbol: the radix-3 DIF in
+// registers (wave e holds n = t + 64 (m + 8 e) < 2048 and its partners
+// n + 2048, n + 4096), one radix-4 DIF step of the three FFT2048s across the
+// quad through LDS (wave e forms branch e: v_e[n'] = W2048^{n' e}
+// sum_h u[n' + 512 h] W4^{h e}, n' = t + 64 m), then three FFT512s per wave.
+// Wave e, lane 8 s + c owns bins 3 (4 k' + e) + j, k' = s + 8 c + 64 d; the
+// estimate is [e][slot][lane] per row (k_ls_6144).
+namespace td6144 {
+
+using pk::v2f;
+constexpr int C = 6144, K = C - 1;
+constexpr int XS = 24 * 64;
+constexpr int NT = 256;  // one quad per workgroup
+
+__device__ __forceinline__ int bin_of(int e, int L, int i) {
+    return 3 * (4 * ((L >> 3) + 8 * (L & 7) + 64 * (i & 7)) + e) + (i >> 3);
+}
+
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
+k_mrc_td6144(const float2 *__restrict__ iq, long long nframes, int S, int R, int prefix, const float2 *__restrict__ Hl,
+             const float *__restrict__ P, float2 *__restrict__ out, int mode) {
+    __shared__ float2 tab[2048];   // W6144^e, e < 2048
+    __shared__ float2 xch[4][XS];  // per-wave exchange / transpose image
+    for (int e = threadIdx.x; e < 2048; e += NT) {
+        double sn, cs;
+        sincospi(-2.0 * (double)e / (double)C, &sn, &cs);
+        tab[e] = float2{(float)cs, (float)sn};
+    }
+    const int e = threadIdx.x >> 6, L = threadIdx.x & 63;
+    v2f twA[7], twB[7];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) {
+        double sn, cs;
+        sincospi(-2.0 * (double)((L * k) % 512) / 512.0, &sn, &cs);
+        twA[k - 1] = v2f{(float)cs, (float)sn};
+        sincospi(-2.0 * (double)(((L & 7) * k) % 64) / 64.0, &sn, &cs);
+        twB[k - 1] = v2f{(float)cs, (float)sn};
+    }
+    __syncthreads();
+    float2 *own = xch[e];
+    const int nsd = S - 1;
+    const long long Cp = C + prefix, nq = nframes * nsd, np = gridDim.x;
+    const float r3 = 0.86602540378443865f;
+    auto row_ptr = [&](long long q, int r) {
+        const long long f = q / nsd, s = 1 + q % nsd;
+        return iq + ((f * S + s) * R + r) * Cp + prefix;
+    };
+    auto load = [&](float2 (&x)[24], const float2 *b) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int m = 0; m < 8; ++m) x[8 * i + m] = b[L + 64 * (m + 8 * e + 32 * i)];
+    };
+    float2 x[24];
+    long long q = blockIdx.x;
+    if (q < nq) load(x, row_ptr(q, 0));
+    for (; q < nq; q += np) {
+        const long long f = q / nsd;
+        v2f acc[24];
+#pragma unroll
+        for (int i = 0; i < 24; ++i) acc[i] = v2f{0.f, 0.f};
+        for (int r = 0; r < R; ++r) {
+            v2f u[3][8];
+#pragma unroll
+            for (int m = 0; m < 8; ++m) {
+                const v2f a0 = pk::V(x[m]), a1 = pk::V(x[m + 8]), a2 = pk::V(x[m + 16]);
+                const v2f sm = a1 + a2, df = a1 - a2;
+                const v2f t0 = a0 - sm * (v2f){0.5f, 0.5f};
+                const v2f jd = v2f{df.y * r3, -df.x * r3};
+                const int n = L + 64 * (m + 8 * e);
+                const v2f w1 = pk::V(tab[n]);
+                u[0][m] = a0 + sm;
+                u[1][m] = pk::cmul(t0 + jd, w1);
+                u[2][m] = pk::cmul(t0 - jd, pk::cmul(w1, w1));  // W6144^{2 n}
+            }
+            {
+                const long long qn = r + 1 < R ? q : q + np;
+                if (qn < nq) load(x, row_ptr(qn, r + 1 < R ? r + 1 : 0));
+            }
+#pragma unroll
+            for (int j = 0; j < 3; ++j)
+#pragma unroll
+                for (int m = 0; m < 8; ++m) own[(8 * j + m) * 64 + L] = pk::F(u[j][m]);
+            td3072::pair_barrier();
+#pragma unroll
+            for (int m = 0; m < 8; ++m) {
+                // W2048^{n' e} = W6144^{3 n' e}, n' = L + 64 m: from W2048^{n'} and its powers
+                const v2f w1 = pk::V(tab[3 * (L + 64 * m)]);
+                const v2f we = e == 0 ? v2f{1.f, 0.f} : e == 1 ? w1 : e == 2 ? pk::cmul(w1, w1)
+                                                                      : pk::cmul(w1, pk::cmul(w1, w1));
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    const v2f h0 = pk::V(xch[0][(8 * j + m) * 64 + L]), h1 = pk::V(xch[1][(8 * j + m) * 64 + L]);
+                    const v2f h2 = pk::V(xch[2][(8 * j + m) * 64 + L]), h3 = pk::V(xch[3][(8 * j + m) * 64 + L]);
+                    // sum_h u[n' + 512 h] W4^{h e}, W4 = -i
+                    const v2f s02 = h0 + h2, d02 = h0 - h2, s13 = h1 + h3, d13 = h1 - h3;
+                    const v2f md13 = v2f{d13.y, -d13.x};  // -i (h1 - h3)
+                    v2f v = e == 0 ? s02 + s13 : e == 1 ? d02 + md13 : e == 2 ? s02 - s13 : d02 - md13;
+                    u[j][m] = e == 0 ? v : pk::cmul(v, we);
+                }
+            }
+            td3072::pair_barrier();
+            const float2 *hrow = Hl + (f * R + r) * (long long)C + e * 1536;
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                v2f h[8];
+#pragma unroll
+                for (int d = 0; d < 8; ++d) h[d] = pk::V(hrow[(8 * j + d) * 64 + L]);
+                td1536::fft512(u[j], own, L, twA, twB);
+#pragma unroll
+                for (int d = 0; d < 8; ++d) pk::mac(acc[8 * j + d], u[j][d], h[d]);
+            }
+        }
+        float2 *o = out + q * K;
+        const float *Pf = P + f * C;
+#pragma unroll
+        for (int i = 0; i < 24; ++i) {
+            const int b = bin_of(e, L, i);
+            if (b == 0) continue;
+            const float2 a = pk::F(acc[i]);
+            if (mode == 0) {
+                const float p = Pf[b];
+                o[out_pos(b - 1, K)] = float2{a.x / p, a.y / p};
+            } else {
+                o[b - 1] = a;
+            }
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_ls_6144(const float2 *__restrict__ Y, int R, const float2 *__restrict__ X,
+                                                 float2 *__restrict__ Hl, float *__restrict__ P) {
+    const int b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= C) return;
+    const long long f = blockIdx.y;
+    const int k = b / 3, j = b - 3 * k, kk = k >> 2, e = k & 3;
+    const int L = 8 * (kk & 7) + ((kk >> 3) & 7), i = 8 * j + (kk >> 6);
+    const float2 *Yf = Y + f * (long long)R * C;
+    float2 *Hf = Hl + f * (long long)R * C + e * 1536 + i * 64 + L;
+    float p = 0.f;
+    if (b == 0) {
+        for (int r = 0; r < R; ++r) Hf[(long long)r * C] = float2{0.f, 0.f};
+        p = 1.f;
+    } else {
+        const float2 x = X[b - 1];
+        for (int r = 0; r < R; ++r) {
+            const float2 h = ls_conj(Yf[(long long)r * C + b], x);
+            Hf[(long long)r * C] = h;
+            p = (r == 0) ? (h.x * h.x) + (h.y * h.y) : p + (h.x * h.x) + (h.y * h.y);
+        }
+    }
+    P[f * C + b] = p;
+}
+
+}  // namespace td6144
+
 hipError_t launch_ls_3072(const float2 *Y, long long nframes, int R, const float2 *X, float2 *Hl, float *P,
                           hipStream_t s) {
     if (nframes <= 0) return hipSuccess;
@@ -395,6 +552,31 @@ hipError_t launch_mrc_td1536(const float2 *iq, long long nframes, int S, int R, 
         cus = 256;
     const long long res = 2ll * cus, need = (nq + td1536::WAVES - 1) / td1536::WAVES;
     hipLaunchKernelGGL(td1536::k_mrc_td1536, dim3((unsigned)(need < res ? need : res)), dim3(td1536::NT), 0, s, iq,
+                       nframes, S, R, prefix, Hl, P, out, mode);
+    return hipGetLastError();
+}
+
+hipError_t launch_ls_6144(const float2 *Y, long long nframes, int R, const float2 *X, float2 *Hl, float *P,
+                          hipStream_t s) {
+    if (nframes <= 0) return hipSuccess;
+    for (long long f0 = 0; f0 < nframes; f0 += 65535) {
+        const long long n = nframes - f0 < 65535 ? nframes - f0 : 65535;
+        hipLaunchKernelGGL(td6144::k_ls_6144, dim3((td6144::C + 255) / 256, (unsigned)n), dim3(256), 0, s,
+                           Y + f0 * (long long)R * td6144::C, R, X, Hl + f0 * (long long)R * td6144::C,
+                           P + f0 * td6144::C);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_mrc_td6144(const float2 *iq, long long nframes, int S, int R, int prefix, const float2 *Hl,
+                             const float *P, float2 *out, int mode, hipStream_t s) {
+    const long long nq = nframes * (S - 1);
+    if (nq <= 0) return hipSuccess;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
+    const long long res = 2ll * cus;  // 64 KiB of LDS and 4 waves per workgroup: 2 per CU
+    hipLaunchKernelGGL(td6144::k_mrc_td6144, dim3((unsigned)(nq < res ? nq : res)), dim3(td6144::NT), 0, s, iq,
                        nframes, S, R, prefix, Hl, P, out, mode);
     return hipGetLastError();
 }

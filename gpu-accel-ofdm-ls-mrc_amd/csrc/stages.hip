@@ -71,7 +71,7 @@ __device__ __forceinline__ int lane_of(int b, int &k) {  // b < 1024
     k = (b >> 4) & 15;
     return 4 * q + (((c & 1) << 1) | (c >> 1));
 }
-__device__ __forceinline__ int hc_pos(int b, int C) {  // C = 0: bin layout (b < C <= 4096)
+__device__ __forceinline__ int hc_pos(int b, int C) {  // C = 0: bin layout
     int k;
     if (C == 1024) {  // float4 (k >> 1) * 64 + t holds bins (k & ~1, k | 1) of lane t
         const int t = lane_of(b, k);
@@ -87,6 +87,10 @@ __device__ __forceinline__ int hc_pos(int b, int C) {  // C = 0: bin layout (b <
     }
     if (C == 3072) {  // wave e, slot 8 j + d of lane 8 s + c holds bin 3 (2 (s + 8 c + 64 d) + e) + j
         const int q = b / 3, j = b - 3 * q, e = q & 1, kk = q >> 1;
+        return e * 1536 + (8 * j + (kk >> 6)) * 64 + 8 * (kk & 7) + ((kk >> 3) & 7);
+    }
+    if (C == 6144) {  // wave e, slot 8 j + d of lane 8 s + c holds bin 3 (4 (s + 8 c + 64 d) + e) + j
+        const int q = b / 3, j = b - 3 * q, e = q & 3, kk = q >> 2;
         return e * 1536 + (8 * j + (kk >> 6)) * 64 + 8 * (kk & 7) + ((kk >> 3) & 7);
     }
     if (C == 4096) {  // float2 e * 2048 + h * 1024 + k * 64 + t = Hc[4 b' + 2 h + e]
