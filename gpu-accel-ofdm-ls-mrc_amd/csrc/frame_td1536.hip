@@ -506,6 +506,111 @@ __global__ void __launch_bounds__(256) k_ls_6144(const float2 *__restrict__ Y, i
 
 }  // namespace td6144
 
+// ---------------------------------------------------------------------------
+// C = 512 (LTE 5 MHz, and the FFT512 of the receivers above on its own): one
+// wave per data symbol, 8 samples per lane, td1536::fft512; lane 8 s + c owns
+// bins s + 8 c + 64 d (slot d); estimate [slot][lane] per row (k_ls_512).
+namespace td512 {
+
+using pk::v2f;
+constexpr int C = 512, K = C - 1;
+constexpr int WAVES = 4, NT = 64 * WAVES;
+
+__global__ void __launch_bounds__(NT) k_mrc_td512(const float2 *__restrict__ iq, long long nframes, int S, int R,
+                                                  int prefix, const float2 *__restrict__ Hl,
+                                                  const float *__restrict__ P, float2 *__restrict__ out, int mode) {
+    __shared__ float2 img[WAVES][td1536::TS];
+    const int w = threadIdx.x >> 6, L = threadIdx.x & 63;
+    float2 *T = img[w];
+    v2f twA[7], twB[7];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) {
+        double sn, cs;
+        sincospi(-2.0 * (double)((L * k) % 512) / 512.0, &sn, &cs);
+        twA[k - 1] = v2f{(float)cs, (float)sn};
+        sincospi(-2.0 * (double)(((L & 7) * k) % 64) / 64.0, &sn, &cs);
+        twB[k - 1] = v2f{(float)cs, (float)sn};
+    }
+    const int nsd = S - 1;
+    const long long Cp = C + prefix, nq = nframes * nsd, nw = (long long)gridDim.x * WAVES;
+    auto row_ptr = [&](long long q, int r) {
+        const long long f = q / nsd, s = 1 + q % nsd;
+        return iq + ((f * S + s) * R + r) * Cp + prefix;
+    };
+    float2 x[8];
+    long long q = (long long)blockIdx.x * WAVES + w;
+    if (q < nq) {
+        const float2 *b = row_ptr(q, 0);
+#pragma unroll
+        for (int m = 0; m < 8; ++m) x[m] = b[L + 64 * m];
+    }
+    for (; q < nq; q += nw) {
+        const long long f = q / nsd;
+        v2f acc[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i] = v2f{0.f, 0.f};
+        for (int r = 0; r < R; ++r) {
+            v2f u[8];
+#pragma unroll
+            for (int m = 0; m < 8; ++m) u[m] = pk::V(x[m]);
+            {
+                const long long qn = r + 1 < R ? q : q + nw;
+                if (qn < nq) {
+                    const float2 *b = row_ptr(qn, r + 1 < R ? r + 1 : 0);
+#pragma unroll
+                    for (int m = 0; m < 8; ++m) x[m] = b[L + 64 * m];
+                }
+            }
+            const float2 *hrow = Hl + (f * R + r) * (long long)C;
+            v2f h[8];
+#pragma unroll
+            for (int d = 0; d < 8; ++d) h[d] = pk::V(hrow[d * 64 + L]);
+            td1536::fft512(u, T, L, twA, twB);
+#pragma unroll
+            for (int d = 0; d < 8; ++d) pk::mac(acc[d], u[d], h[d]);
+        }
+        float2 *o = out + q * K;
+        const float *Pf = P + f * C;
+#pragma unroll
+        for (int d = 0; d < 8; ++d) {
+            const int b = (L >> 3) + 8 * (L & 7) + 64 * d;
+            if (b == 0) continue;
+            const float2 a = pk::F(acc[d]);
+            if (mode == 0) {
+                const float p = Pf[b];
+                o[out_pos(b - 1, K)] = float2{a.x / p, a.y / p};
+            } else {
+                o[b - 1] = a;
+            }
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_ls_512(const float2 *__restrict__ Y, int R, const float2 *__restrict__ X,
+                                                float2 *__restrict__ Hl, float *__restrict__ P) {
+    const int b = blockIdx.x * 256 + threadIdx.x;
+    if (b >= C) return;
+    const long long f = blockIdx.y;
+    const int L = 8 * (b & 7) + ((b >> 3) & 7), d = b >> 6;
+    const float2 *Yf = Y + f * (long long)R * C;
+    float2 *Hf = Hl + f * (long long)R * C + d * 64 + L;
+    float p = 0.f;
+    if (b == 0) {
+        for (int r = 0; r < R; ++r) Hf[(long long)r * C] = float2{0.f, 0.f};
+        p = 1.f;
+    } else {
+        const float2 x = X[b - 1];
+        for (int r = 0; r < R; ++r) {
+            const float2 h = ls_conj(Yf[(long long)r * C + b], x);
+            Hf[(long long)r * C] = h;
+            p = (r == 0) ? (h.x * h.x) + (h.y * h.y) : p + (h.x * h.x) + (h.y * h.y);
+        }
+    }
+    P[f * C + b] = p;
+}
+
+}  // namespace td512
+
 hipError_t launch_ls_3072(const float2 *Y, long long nframes, int R, const float2 *X, float2 *Hl, float *P,
                           hipStream_t s) {
     if (nframes <= 0) return hipSuccess;
@@ -577,6 +682,31 @@ hipError_t launch_mrc_td6144(const float2 *iq, long long nframes, int S, int R, 
         cus = 256;
     const long long res = 2ll * cus;  // 64 KiB of LDS and 4 waves per workgroup: 2 per CU
     hipLaunchKernelGGL(td6144::k_mrc_td6144, dim3((unsigned)(nq < res ? nq : res)), dim3(td6144::NT), 0, s, iq,
+                       nframes, S, R, prefix, Hl, P, out, mode);
+    return hipGetLastError();
+}
+
+hipError_t launch_ls_512(const float2 *Y, long long nframes, int R, const float2 *X, float2 *Hl, float *P,
+                         hipStream_t s) {
+    if (nframes <= 0) return hipSuccess;
+    for (long long f0 = 0; f0 < nframes; f0 += 65535) {
+        const long long n = nframes - f0 < 65535 ? nframes - f0 : 65535;
+        hipLaunchKernelGGL(td512::k_ls_512, dim3((td512::C + 255) / 256, (unsigned)n), dim3(256), 0, s,
+                           Y + f0 * (long long)R * td512::C, R, X, Hl + f0 * (long long)R * td512::C,
+                           P + f0 * td512::C);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_mrc_td512(const float2 *iq, long long nframes, int S, int R, int prefix, const float2 *Hl,
+                            const float *P, float2 *out, int mode, hipStream_t s) {
+    const long long nq = nframes * (S - 1);
+    if (nq <= 0) return hipSuccess;
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
+    const long long res = 4ll * cus, need = (nq + td512::WAVES - 1) / td512::WAVES;
+    hipLaunchKernelGGL(td512::k_mrc_td512, dim3((unsigned)(need < res ? need : res)), dim3(td512::NT), 0, s, iq,
                        nframes, S, R, prefix, Hl, P, out, mode);
     return hipGetLastError();
 }

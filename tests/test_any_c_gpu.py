@@ -59,7 +59,7 @@ def test_fft_rows_any_c_many_rows(ofdm, dev):
     assert np.abs(got - ref).max() <= 1e-5 * np.abs(ref).max()
 
 
-@pytest.mark.parametrize("C,R,prefix", [(6, 3, 0), (12, 1, 3), (600, 4, 44), (1021, 3, 0), (1200, 8, 84),
+@pytest.mark.parametrize("C,R,prefix", [(6, 3, 0), (12, 1, 3), (512, 1, 0), (512, 32, 36), (600, 4, 44), (1021, 3, 0), (1200, 8, 84),
                                         (1536, 8, 108), (1536, 64, 0), (3000, 2, 0), (3072, 3, 0), (3072, 16, 216),
                                         (6144, 4, 432), (6144, 12, 0),
                                         (8192, 2, 512)])
@@ -114,7 +114,7 @@ def test_stages_any_c_vs_oracle(ofdm, oracle, dev, C, R):
                           np.stack([oracle.shift_one_row(r) for r in rows]))
 
 
-@pytest.mark.parametrize("C,R,prefix", [(1536, 6, 16), (3072, 5, 24), (6144, 4, 40), (1200, 3, 0)])
+@pytest.mark.parametrize("C,R,prefix", [(512, 7, 36), (1536, 6, 16), (3072, 5, 24), (6144, 4, 40), (1200, 3, 0)])
 def test_estimate_export_and_antenna_partials_any_c(ofdm, oracle, dev, C, R, prefix):
     """The estimate of a non-fused size (C = 1536: the lane order of
     frame_td1536.hip; 1200: the bin layout) exported to the reference layout
