@@ -124,25 +124,13 @@ __device__ __forceinline__ void dft_small(float2 (&a)[P], const float2 (&r)[P]) 
     }
 }
 
-// a[t] *= W_C^{t e}, t = 1..P-1, from one table twiddle w = W_C^e and its
-// powers by products of depth <= 3 (w^2, w^4 = (w^2)^2, w^3 = w w^2, w^5 =
-// w w^4, w^6 = w^2 w^4, w^7 = w^3 w^4): within a few ulp of the table
+// a[t] *= W_C^{t e}, t = 1..P-1, each twiddle from the two-level table
+// (one rounding beyond the table's; powers by products of depth 3 instead
+// put single-antenna outputs at C = 6144 past the 1e-5 element-wise bound)
 template <int P, bool INV>
 __device__ __forceinline__ void twiddle_powers(float2 (&a)[P], const Tw &T, unsigned e) {
-    if constexpr (P > 1) {
-        using pk::cmul;
-        const pk::v2f w1 = pk::V(twv<INV>(T, e));
-        pk::v2f w[8];
-        w[1] = w1;
-        if constexpr (P > 2) w[2] = cmul(w1, w1);
-        if constexpr (P > 3) w[3] = cmul(w1, w[2]);
-        if constexpr (P > 4) w[4] = cmul(w[2], w[2]);
-        if constexpr (P > 5) w[5] = cmul(w1, w[4]);
-        if constexpr (P > 6) w[6] = cmul(w[2], w[4]);
-        if constexpr (P > 7) w[7] = cmul(w[3], w[4]);
 #pragma unroll
-        for (int t = 1; t < P; ++t) a[t] = pk::F(cmul(pk::V(a[t]), w[t]));
-    }
+    for (int t = 1; t < P; ++t) a[t] = pk::F(pk::cmul(pk::V(a[t]), pk::V(twv<INV>(T, t * e))));
 }
 
 // one radix-P stage over G rows, src -> dst (caller synchronises after)

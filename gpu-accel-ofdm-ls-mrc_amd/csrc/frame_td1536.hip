@@ -371,9 +371,9 @@ __device__ __forceinline__ int bin_of(int e, int L, int i) {
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
 k_mrc_td6144(const float2 *__restrict__ iq, long long nframes, int S, int R, int prefix, const float2 *__restrict__ Hl,
              const float *__restrict__ P, float2 *__restrict__ out, int mode) {
-    __shared__ float2 tab[2048];   // W6144^e, e < 2048
+    __shared__ float2 tab[4096];   // W6144^e, e < 4096 (e >= 4096: -W6144^{e - 3072}); every twiddle one table entry
     __shared__ float2 xch[4][XS];  // per-wave exchange / transpose image
-    for (int e = threadIdx.x; e < 2048; e += NT) {
+    for (int e = threadIdx.x; e < 4096; e += NT) {
         double sn, cs;
         sincospi(-2.0 * (double)e / (double)C, &sn, &cs);
         tab[e] = float2{(float)cs, (float)sn};
@@ -420,10 +420,9 @@ k_mrc_td6144(const float2 *__restrict__ iq, long long nframes, int S, int R, int
                 const v2f t0 = a0 - sm * (v2f){0.5f, 0.5f};
                 const v2f jd = v2f{df.y * r3, -df.x * r3};
                 const int n = L + 64 * (m + 8 * e);
-                const v2f w1 = pk::V(tab[n]);
                 u[0][m] = a0 + sm;
-                u[1][m] = pk::cmul(t0 + jd, w1);
-                u[2][m] = pk::cmul(t0 - jd, pk::cmul(w1, w1));  // W6144^{2 n}
+                u[1][m] = pk::cmul(t0 + jd, pk::V(tab[n]));
+                u[2][m] = pk::cmul(t0 - jd, pk::V(tab[2 * n]));  // 2 n < 4096
             }
             {
                 const long long qn = r + 1 < R ? q : q + np;
@@ -436,10 +435,9 @@ k_mrc_td6144(const float2 *__restrict__ iq, long long nframes, int S, int R, int
             td3072::pair_barrier();
 #pragma unroll
             for (int m = 0; m < 8; ++m) {
-                // W2048^{n' e} = W6144^{3 n' e}, n' = L + 64 m: from W2048^{n'} and its powers
-                const v2f w1 = pk::V(tab[3 * (L + 64 * m)]);
-                const v2f we = e == 0 ? v2f{1.f, 0.f} : e == 1 ? w1 : e == 2 ? pk::cmul(w1, w1)
-                                                                      : pk::cmul(w1, pk::cmul(w1, w1));
+                // W2048^{n' e} = W6144^{3 n' e}, n' = L + 64 m (3 n' e < 4608; W6144^{x + 3072} = -W6144^x)
+                const int x3 = 3 * (L + 64 * m) * e;
+                const v2f we = x3 < 4096 ? pk::V(tab[x3]) : -pk::V(tab[x3 - 3072]);
 #pragma unroll
                 for (int j = 0; j < 3; ++j) {
                     const v2f h0 = pk::V(xch[0][(8 * j + m) * 64 + L]), h1 = pk::V(xch[1][(8 * j + m) * 64 + L]);
@@ -485,7 +483,7 @@ __global__ void __launch_bounds__(256) k_ls_6144(const float2 *__restrict__ Y, i
     const int b = blockIdx.x * 256 + threadIdx.x;
     if (b >= C) return;
     const long long f = blockIdx.y;
-    const int k = b / 3, j = b - 3 * k, kk = k >> 2, e = k & 3;
+    const int k = b / 3, j = b - 3 * k, kk = k >> 2, e = k & 3;  // b = 3 (4 k' + e) + j
     const int L = 8 * (kk & 7) + ((kk >> 3) & 7), i = 8 * j + (kk >> 6);
     const float2 *Yf = Y + f * (long long)R * C;
     float2 *Hf = Hl + f * (long long)R * C + e * 1536 + i * 64 + L;
