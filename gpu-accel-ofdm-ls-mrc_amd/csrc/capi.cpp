@@ -51,7 +51,7 @@ size_t up256(size_t x) { return (x + 255) & ~size_t(255); }
 bool fused_c(int C) { return C == 1024 || C == 2048 || C == 4096; }
 // sizes whose workspace estimate is in a receiver's lane order: the fused
 // ones and C = 512 / 1536 / 3072 / 6144 (staged pilot FFT, then k_ls_* / k_mrc_td*
-// of frame_td1536.hip)
+// of frame_td_fft512.hip)
 bool lane_c(int C) { return fused_c(C) || C == 512 || C == 1536 || C == 3072 || C == 6144; }
 
 // fused time-domain kernels by C (fused_c(C) must hold)

@@ -1,10 +1,11 @@
-// frame_td1536.hip -- fused MRC for C = 1536 (LTE's 15 MHz FFT size, the most
-// common length that is not a power of two): one HBM pass over the IQ, as the
+// frame_td_fft512.hip -- fused receivers for the FFT sizes built on one
+// in-register FFT512 per wave: C = 1536 (LTE's 15 MHz size), 3072 (a wave
+// pair), 6144 (a wave quad) and 512 itself.  One HBM pass over the IQ, as the
 // power-of-two receivers (demodOneFrameCUDA, gpuLS.cu:575-675, without its
 // cuFFT round trips), replacing the generic any-C kernel (fft_any.hip) at
-// this size.
+// these sizes.
 //
-// One 64-lane wave transforms one 1536-sample antenna row held in registers,
+// C = 1536: one 64-lane wave transforms one antenna row held in registers,
 // 24 samples per lane (lane t: x[t + 64 m'], m' < 24):
 //   * radix-3 decimation in frequency in registers: for n = t + 64 m (m < 8)
 //     u_j[n] = W1536^{n j} sum_i x[n + 512 i] W3^{i j},  j < 3,
@@ -168,7 +169,7 @@ k_mrc_td1536(const float2 *__restrict__ iq, long long nframes, int S, int R, int
 // with P[0] = 1 and a zero DC estimate), findHs + findDistSqrd
 // (gpuLS.cu:158-209, cpuLS.hpp:211-244) as k_ls_freq.
 __global__ void __launch_bounds__(256) k_ls_1536(const float2 *__restrict__ Y, int R, const float2 *__restrict__ X,
-                                                 float2 *__restrict__ Hl, float *__restrict__ P, int partial) {
+                                                 float2 *__restrict__ Hl, float *__restrict__ P) {
     const int b = blockIdx.x * 256 + threadIdx.x;
     if (b >= C) return;
     const long long f = blockIdx.y;
@@ -187,7 +188,6 @@ __global__ void __launch_bounds__(256) k_ls_1536(const float2 *__restrict__ Y, i
             p = (r == 0) ? (h.x * h.x) + (h.y * h.y) : p + (h.x * h.x) + (h.y * h.y);
         }
     }
-    (void)partial;
     P[f * C + b] = p;
 }
 
@@ -609,104 +609,87 @@ __global__ void __launch_bounds__(256) k_ls_512(const float2 *__restrict__ Y, in
 
 }  // namespace td512
 
-hipError_t launch_ls_3072(const float2 *Y, long long nframes, int R, const float2 *X, float2 *Hl, float *P,
+namespace {
+
+int cu_count() {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
+    return cus;
+}
+
+// One workgroup column per 256 bins, one grid row per frame (65535 at a time).
+template <int CC, typename Kern>
+hipError_t launch_ls_lane(Kern kern, const float2 *Y, long long nframes, int R, const float2 *X, float2 *Hl, float *P,
                           hipStream_t s) {
     if (nframes <= 0) return hipSuccess;
     for (long long f0 = 0; f0 < nframes; f0 += 65535) {
         const long long n = nframes - f0 < 65535 ? nframes - f0 : 65535;
-        hipLaunchKernelGGL(td3072::k_ls_3072, dim3((td3072::C + 255) / 256, (unsigned)n), dim3(256), 0, s,
-                           Y + f0 * (long long)R * td3072::C, R, X, Hl + f0 * (long long)R * td3072::C,
-                           P + f0 * td3072::C);
+        hipLaunchKernelGGL(kern, dim3((CC + 255) / 256, (unsigned)n), dim3(256), 0, s, Y + f0 * (long long)R * CC, R,
+                           X, Hl + f0 * (long long)R * CC, P + f0 * CC);
     }
     return hipGetLastError();
 }
 
-hipError_t launch_mrc_td3072(const float2 *iq, long long nframes, int S, int R, int prefix, const float2 *Hl,
-                             const float *P, float2 *out, int mode, hipStream_t s) {
+// Persistent grid: min(workgroups needed, per_cu x CUs); each workgroup owns
+// `per_wg` data symbols at a time.
+template <typename Kern>
+hipError_t launch_mrc_lane(Kern kern, int nt, int per_cu, int per_wg, const float2 *iq, long long nframes, int S,
+                           int R, int prefix, const float2 *Hl, const float *P, float2 *out, int mode, hipStream_t s) {
     const long long nq = nframes * (S - 1);
     if (nq <= 0) return hipSuccess;
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        cus = 256;
-    const long long res = 4ll * cus;  // 40 KiB of LDS and 2 waves per workgroup: 4 per CU
-    hipLaunchKernelGGL(td3072::k_mrc_td3072, dim3((unsigned)(nq < res ? nq : res)), dim3(td3072::NT), 0, s, iq,
-                       nframes, S, R, prefix, Hl, P, out, mode);
+    const long long res = (long long)per_cu * cu_count(), need = (nq + per_wg - 1) / per_wg;
+    hipLaunchKernelGGL(kern, dim3((unsigned)(need < res ? need : res)), dim3(nt), 0, s, iq, nframes, S, R, prefix, Hl,
+                       P, out, mode);
     return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_ls_512(const float2 *Y, long long nframes, int R, const float2 *X, float2 *Hl, float *P,
+                         hipStream_t s) {
+    return launch_ls_lane<td512::C>(td512::k_ls_512, Y, nframes, R, X, Hl, P, s);
 }
 
 hipError_t launch_ls_1536(const float2 *Y, long long nframes, int R, const float2 *X, float2 *Hl, float *P,
                           hipStream_t s) {
-    if (nframes <= 0) return hipSuccess;
-    for (long long f0 = 0; f0 < nframes; f0 += 65535) {
-        const long long n = nframes - f0 < 65535 ? nframes - f0 : 65535;
-        hipLaunchKernelGGL(td1536::k_ls_1536, dim3((td1536::C + 255) / 256, (unsigned)n), dim3(256), 0, s,
-                           Y + f0 * (long long)R * td1536::C, R, X, Hl + f0 * (long long)R * td1536::C,
-                           P + f0 * td1536::C, 0);
-    }
-    return hipGetLastError();
+    return launch_ls_lane<td1536::C>(td1536::k_ls_1536, Y, nframes, R, X, Hl, P, s);
 }
 
-hipError_t launch_mrc_td1536(const float2 *iq, long long nframes, int S, int R, int prefix, const float2 *Hl,
-                             const float *P, float2 *out, int mode, hipStream_t s) {
-    const long long nq = nframes * (S - 1);
-    if (nq <= 0) return hipSuccess;
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        cus = 256;
-    const long long res = 2ll * cus, need = (nq + td1536::WAVES - 1) / td1536::WAVES;
-    hipLaunchKernelGGL(td1536::k_mrc_td1536, dim3((unsigned)(need < res ? need : res)), dim3(td1536::NT), 0, s, iq,
-                       nframes, S, R, prefix, Hl, P, out, mode);
-    return hipGetLastError();
+hipError_t launch_ls_3072(const float2 *Y, long long nframes, int R, const float2 *X, float2 *Hl, float *P,
+                          hipStream_t s) {
+    return launch_ls_lane<td3072::C>(td3072::k_ls_3072, Y, nframes, R, X, Hl, P, s);
 }
 
 hipError_t launch_ls_6144(const float2 *Y, long long nframes, int R, const float2 *X, float2 *Hl, float *P,
                           hipStream_t s) {
-    if (nframes <= 0) return hipSuccess;
-    for (long long f0 = 0; f0 < nframes; f0 += 65535) {
-        const long long n = nframes - f0 < 65535 ? nframes - f0 : 65535;
-        hipLaunchKernelGGL(td6144::k_ls_6144, dim3((td6144::C + 255) / 256, (unsigned)n), dim3(256), 0, s,
-                           Y + f0 * (long long)R * td6144::C, R, X, Hl + f0 * (long long)R * td6144::C,
-                           P + f0 * td6144::C);
-    }
-    return hipGetLastError();
+    return launch_ls_lane<td6144::C>(td6144::k_ls_6144, Y, nframes, R, X, Hl, P, s);
 }
 
-hipError_t launch_mrc_td6144(const float2 *iq, long long nframes, int S, int R, int prefix, const float2 *Hl,
-                             const float *P, float2 *out, int mode, hipStream_t s) {
-    const long long nq = nframes * (S - 1);
-    if (nq <= 0) return hipSuccess;
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        cus = 256;
-    const long long res = 2ll * cus;  // 64 KiB of LDS and 4 waves per workgroup: 2 per CU
-    hipLaunchKernelGGL(td6144::k_mrc_td6144, dim3((unsigned)(nq < res ? nq : res)), dim3(td6144::NT), 0, s, iq,
-                       nframes, S, R, prefix, Hl, P, out, mode);
-    return hipGetLastError();
-}
-
-hipError_t launch_ls_512(const float2 *Y, long long nframes, int R, const float2 *X, float2 *Hl, float *P,
-                         hipStream_t s) {
-    if (nframes <= 0) return hipSuccess;
-    for (long long f0 = 0; f0 < nframes; f0 += 65535) {
-        const long long n = nframes - f0 < 65535 ? nframes - f0 : 65535;
-        hipLaunchKernelGGL(td512::k_ls_512, dim3((td512::C + 255) / 256, (unsigned)n), dim3(256), 0, s,
-                           Y + f0 * (long long)R * td512::C, R, X, Hl + f0 * (long long)R * td512::C,
-                           P + f0 * td512::C);
-    }
-    return hipGetLastError();
-}
-
+// 512: 4 one-wave symbols per workgroup, 4 workgroups per CU.
 hipError_t launch_mrc_td512(const float2 *iq, long long nframes, int S, int R, int prefix, const float2 *Hl,
                             const float *P, float2 *out, int mode, hipStream_t s) {
-    const long long nq = nframes * (S - 1);
-    if (nq <= 0) return hipSuccess;
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        cus = 256;
-    const long long res = 4ll * cus, need = (nq + td512::WAVES - 1) / td512::WAVES;
-    hipLaunchKernelGGL(td512::k_mrc_td512, dim3((unsigned)(need < res ? need : res)), dim3(td512::NT), 0, s, iq,
-                       nframes, S, R, prefix, Hl, P, out, mode);
-    return hipGetLastError();
+    return launch_mrc_lane(td512::k_mrc_td512, td512::NT, 4, td512::WAVES, iq, nframes, S, R, prefix, Hl, P, out,
+                           mode, s);
+}
+
+// 1536: 4 one-wave symbols per workgroup, 2 workgroups per CU (2 waves / SIMD).
+hipError_t launch_mrc_td1536(const float2 *iq, long long nframes, int S, int R, int prefix, const float2 *Hl,
+                             const float *P, float2 *out, int mode, hipStream_t s) {
+    return launch_mrc_lane(td1536::k_mrc_td1536, td1536::NT, 2, td1536::WAVES, iq, nframes, S, R, prefix, Hl, P, out,
+                           mode, s);
+}
+
+// 3072: one wave pair (40 KiB of LDS) per workgroup, 4 per CU.
+hipError_t launch_mrc_td3072(const float2 *iq, long long nframes, int S, int R, int prefix, const float2 *Hl,
+                             const float *P, float2 *out, int mode, hipStream_t s) {
+    return launch_mrc_lane(td3072::k_mrc_td3072, td3072::NT, 4, 1, iq, nframes, S, R, prefix, Hl, P, out, mode, s);
+}
+
+// 6144: one wave quad (64 KiB of LDS) per workgroup, 2 per CU.
+hipError_t launch_mrc_td6144(const float2 *iq, long long nframes, int S, int R, int prefix, const float2 *Hl,
+                             const float *P, float2 *out, int mode, hipStream_t s) {
+    return launch_mrc_lane(td6144::k_mrc_td6144, td6144::NT, 2, 1, iq, nframes, S, R, prefix, Hl, P, out, mode, s);
 }
 
 }  // namespace ofdm

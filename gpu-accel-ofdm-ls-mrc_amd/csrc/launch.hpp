@@ -51,7 +51,7 @@ hipError_t launch_fft_any_b(const float2 *in, long long in_stride, long long in_
                             int in_off, float2 *out, long long out_stride, int out_off, long long nrows, int C,
                             bool inverse, float scale, hipStream_t s);
 bool fft_any_supported(int C);
-// C = 1536 (frame_td1536.hip): LS from FFT'd pilot rows (staging, frame
+// C = 1536 (frame_td_fft512.hip): LS from FFT'd pilot rows (staging, frame
 // stride R*C) into the lane-order Hc + bin-layout P, and the fused MRC.
 hipError_t launch_ls_1536(const float2 *Y, long long nframes, int R, const float2 *X, float2 *Hl, float *P,
                           hipStream_t s);

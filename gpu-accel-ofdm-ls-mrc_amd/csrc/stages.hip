@@ -81,7 +81,7 @@ __device__ __forceinline__ int hc_pos(int b, int C) {  // C = 0: bin layout
         const int t = lane_of(b >> 1, k);
         return 2 * (k * 64 + t) + (b & 1);
     }
-    if (C == 1536) {  // frame_td1536.hip: slot 8 j + d of lane 8 s + c holds bin 3 (s + 8 c + 64 d) + j
+    if (C == 1536) {  // frame_td_fft512.hip: slot 8 j + d of lane 8 s + c holds bin 3 (s + 8 c + 64 d) + j
         const int q = b / 3, j = b - 3 * q;
         return (8 * j + (q >> 6)) * 64 + 8 * (q & 7) + ((q >> 3) & 7);
     }

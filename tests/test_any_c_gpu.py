@@ -117,7 +117,7 @@ def test_stages_any_c_vs_oracle(ofdm, oracle, dev, C, R):
 @pytest.mark.parametrize("C,R,prefix", [(512, 7, 36), (1536, 6, 16), (3072, 5, 24), (6144, 4, 40), (1200, 3, 0)])
 def test_estimate_export_and_antenna_partials_any_c(ofdm, oracle, dev, C, R, prefix):
     """The estimate of a non-fused size (C = 1536: the lane order of
-    frame_td1536.hip; 1200: the bin layout) exported to the reference layout
+    frame_td_fft512.hip; 1200: the bin layout) exported to the reference layout
     matches the oracle's LS; the antenna-split partials (numerators + |H|^2)
     summed over two shards and finalised give the full receiver's output."""
     F, S = 2, 4
