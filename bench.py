@@ -385,7 +385,7 @@ def main():
            "flow": "one-launch" if one else "two-launch",
            "parallelism": f"frame-sharded x{world}, no collective"}
     b_sym = R * C * 8 + K * 8
-    kern = {1024: "k_mrc_td1024_hlds", 2048: "k_mrc_td2048", 4096: "k_mrc_td4096h", 1536: "k_mrc_td1536", 3072: "k_mrc_td3072", 6144: "k_mrc_td6144", 512: "k_mrc_td512"}.get(C)
+    kern = {1024: "k_mrc_td1024_hlds", 2048: "k_mrc_td2048", 4096: "k_mrc_td4096h", 1536: "k_mrc_td1536", 3072: "k_mrc_td3072", 6144: "k_mrc_td6144", 512: "k_mrc_td512", 256: "k_mrc_td256", 128: "k_mrc_td128"}.get(C)
     mrc_name = f"{kern} (FFT+MRC+normalise+rotate)" if kern else "k_mrc_any (mixed-radix FFT+MRC+normalise+rotate)"
     if freq:
         mrc_name = "k_mrc_freq_frames (MRC+normalise+rotate)" if C >= 512 else "k_mrc_freq (MRC+normalise+rotate)"
@@ -625,7 +625,7 @@ def bench_split(args, X, dev, world, rank, barrier):
     mrc_median = mrc_all[reps // 2]
     b_sym = R * C * 8 + K * 8
     achieved = Q * b_sym / (mrc_ms * 1e-3) / 1e9
-    kern = {1024: "k_mrc_td1024_hlds", 2048: "k_mrc_td2048", 4096: "k_mrc_td4096h", 1536: "k_mrc_td1536", 3072: "k_mrc_td3072", 6144: "k_mrc_td6144", 512: "k_mrc_td512"}.get(
+    kern = {1024: "k_mrc_td1024_hlds", 2048: "k_mrc_td2048", 4096: "k_mrc_td4096h", 1536: "k_mrc_td1536", 3072: "k_mrc_td3072", 6144: "k_mrc_td6144", 512: "k_mrc_td512", 256: "k_mrc_td256", 128: "k_mrc_td128"}.get(
         C, "k_mrc_any")
     result = {
         "metric": "OFDM symbols/s (LS+MRC) at 1024 subcarriers x 64 ant; achieved HBM GB/s vs peak",

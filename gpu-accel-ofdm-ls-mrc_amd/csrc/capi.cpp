@@ -50,9 +50,10 @@ size_t up256(size_t x) { return (x + 255) & ~size_t(255); }
 // fused one-pass kernels exist for these FFT sizes
 bool fused_c(int C) { return C == 1024 || C == 2048 || C == 4096; }
 // sizes whose workspace estimate is in a receiver's lane order: the fused
-// ones and C = 512 / 1536 / 3072 / 6144 (staged pilot FFT, then k_ls_* / k_mrc_td*
-// of frame_td_fft512.hip)
-bool lane_c(int C) { return fused_c(C) || C == 512 || C == 1536 || C == 3072 || C == 6144; }
+// ones and C = 128 / 256 / 512 / 1536 / 3072 / 6144 (staged pilot FFT, then
+// k_ls_* / k_mrc_td* of frame_td_fft512.hip)
+bool small_c(int C) { return C == 128 || C == 256 || C == 512; }
+bool lane_c(int C) { return fused_c(C) || small_c(C) || C == 1536 || C == 3072 || C == 6144; }
 
 // fused time-domain kernels by C (fused_c(C) must hold)
 hipError_t ls_fused(const float2 *iq, long long F, int S, int R, int C, int prefix, const float2 *X,
@@ -221,7 +222,7 @@ int td_staged(const float2 *iq, long long F, int S, int R, int C, int prefix, co
             e = C == 1536   ? ofdm::launch_ls_1536(w.staging, n, R, X, w.Hc + f0 * pilot, w.P + f0 * C, s)
                 : C == 3072 ? ofdm::launch_ls_3072(w.staging, n, R, X, w.Hc + f0 * pilot, w.P + f0 * C, s)
                 : C == 6144 ? ofdm::launch_ls_6144(w.staging, n, R, X, w.Hc + f0 * pilot, w.P + f0 * C, s)
-                : C == 512  ? ofdm::launch_ls_512(w.staging, n, R, X, w.Hc + f0 * pilot, w.P + f0 * C, s)
+                : small_c(C) ? ofdm::launch_ls_small(C, w.staging, n, R, X, w.Hc + f0 * pilot, w.P + f0 * C, s)
                             : ofdm::launch_ls_freq(w.staging, pilot, n, R, C, X, w.Hc + f0 * pilot, pilot, C, 1,
                                                    w.P + f0 * C, C, 1, s);
             if (e != hipSuccess) return hip_check(e, "ls_freq");
@@ -237,9 +238,9 @@ int td_staged(const float2 *iq, long long F, int S, int R, int C, int prefix, co
     if (C == 6144)
         return hip_check(ofdm::launch_mrc_td6144(iq, F, S, R, prefix, w.Hc, w.P, out, mode == 1 ? 1 : 0, s),
                          "mrc_td6144");
-    if (C == 512)
-        return hip_check(ofdm::launch_mrc_td512(iq, F, S, R, prefix, w.Hc, w.P, out, mode == 1 ? 1 : 0, s),
-                         "mrc_td512");
+    if (small_c(C))
+        return hip_check(ofdm::launch_mrc_small(C, iq, F, S, R, prefix, w.Hc, w.P, out, mode == 1 ? 1 : 0, s),
+                         "mrc_small");
     return hip_check(ofdm::launch_mrc_any(iq, F, S, R, C, prefix, w.Hc, w.P, out, mode == 1 ? 1 : 0, s),
                      "mrc_any");
 }

@@ -49,11 +49,9 @@ __device__ __forceinline__ int bin_of(int L, int i) {
     return 3 * ((L >> 3) + 8 * (L & 7) + 64 * (i & 7)) + (i >> 3);
 }
 
-// FFT512 of v (lane t: v[m] = u[t + 64 m]) -> v[d] = U[s + 8 c + 64 d], L = 8 s + c
-__device__ __forceinline__ void fft512(v2f (&v)[8], float2 *T, int L, const v2f (&twA)[7], const v2f (&twB)[7]) {
-    pk::fft_reg<8>(v);  // over m -> s
-#pragma unroll
-    for (int s = 1; s < 8; ++s) v[s] = pk::cmul(v[s], twA[s - 1]);
+// The two FFT64 passes of fft512: lane t holds v[s] = A_s[t] (8 sequences of
+// 64 over the lanes) -> lane L = 8 s + c holds v[d] = FFT64(A_s)[c + 8 d].
+__device__ __forceinline__ void fft64x8(v2f (&v)[8], float2 *T, int L, const v2f (&twB)[7]) {
     wsync();
 #pragma unroll
     for (int s = 0; s < 8; ++s) T[s * PA + L] = pk::F(v[s]);
@@ -72,6 +70,14 @@ __device__ __forceinline__ void fft512(v2f (&v)[8], float2 *T, int L, const v2f 
 #pragma unroll
     for (int q = 0; q < 8; ++q) v[q] = pk::V(T[s * PA + 9 * c + q]);
     pk::fft_reg<8>(v);  // over a -> d
+}
+
+// FFT512 of v (lane t: v[m] = u[t + 64 m]) -> v[d] = U[s + 8 c + 64 d], L = 8 s + c
+__device__ __forceinline__ void fft512(v2f (&v)[8], float2 *T, int L, const v2f (&twA)[7], const v2f (&twB)[7]) {
+    pk::fft_reg<8>(v);  // over m -> s
+#pragma unroll
+    for (int s = 1; s < 8; ++s) v[s] = pk::cmul(v[s], twA[s - 1]);
+    fft64x8(v, T, L, twB);
 }
 
 __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(2, 2)))
@@ -505,74 +511,102 @@ __global__ void __launch_bounds__(256) k_ls_6144(const float2 *__restrict__ Y, i
 }  // namespace td6144
 
 // ---------------------------------------------------------------------------
-// C = 512 (LTE 5 MHz, and the FFT512 of the receivers above on its own): one
-// wave per data symbol, 8 samples per lane, td1536::fft512; lane 8 s + c owns
-// bins s + 8 c + 64 d (slot d); estimate [slot][lane] per row (k_ls_512).
-namespace td512 {
+// C = 512, 256, 128 (LTE's 5, 3 and 1.4 MHz sizes; 512 is also the FFT of the
+// receivers above): one wave per data symbol, NR = 512 / C antenna rows per
+// pass, P = C / 64 samples of each per lane (lane t: v[rho P + m] =
+// x_{r0 + rho}[t + 64 m], m < P).  Pass A is a DFT_P per row with W_C^{t s'};
+// the NR P = 8 sequences then go through fft512's two FFT64 passes unchanged,
+// so lane L = 8 (rho P + s') + c ends with bins s' + P c + 8 P d (slot d) of
+// row r0 + rho.  Each lane accumulates its rows rho, rho + NR, ...; the NR
+// partial sums meet once per symbol (lane xor 8 P, 16 P).  Estimate per row:
+// [slot d][lane mod 8 P] (k_ls_small).  Rows past R enter as zeros.
+namespace tdsmall {
 
 using pk::v2f;
-constexpr int C = 512, K = C - 1;
 constexpr int WAVES = 4, NT = 64 * WAVES;
 
-__global__ void __launch_bounds__(NT) k_mrc_td512(const float2 *__restrict__ iq, long long nframes, int S, int R,
-                                                  int prefix, const float2 *__restrict__ Hl,
-                                                  const float *__restrict__ P, float2 *__restrict__ out, int mode) {
+template <int NR>
+__device__ __forceinline__ void mrc_small(const float2 *__restrict__ iq, long long nframes, int S, int R, int prefix,
+                                          const float2 *__restrict__ Hl, const float *__restrict__ P,
+                                          float2 *__restrict__ out, int mode) {
+    constexpr int NP = 8 / NR, C = 64 * NP, K = C - 1, LW = 8 * NP;
     __shared__ float2 img[WAVES][td1536::TS];
-    const int w = threadIdx.x >> 6, L = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6, L = threadIdx.x & 63, rho = L / LW, lw = L % LW;
     float2 *T = img[w];
-    v2f twA[7], twB[7];
+    v2f twA[NP > 1 ? NP - 1 : 1], twB[7];
+#pragma unroll
+    for (int k = 1; k < NP; ++k) {
+        double sn, cs;
+        sincospi(-2.0 * (double)((L * k) % C) / (double)C, &sn, &cs);
+        twA[k - 1] = v2f{(float)cs, (float)sn};
+    }
 #pragma unroll
     for (int k = 1; k < 8; ++k) {
         double sn, cs;
-        sincospi(-2.0 * (double)((L * k) % 512) / 512.0, &sn, &cs);
-        twA[k - 1] = v2f{(float)cs, (float)sn};
         sincospi(-2.0 * (double)(((L & 7) * k) % 64) / 64.0, &sn, &cs);
         twB[k - 1] = v2f{(float)cs, (float)sn};
     }
     const int nsd = S - 1;
     const long long Cp = C + prefix, nq = nframes * nsd, nw = (long long)gridDim.x * WAVES;
-    auto row_ptr = [&](long long q, int r) {
-        const long long f = q / nsd, s = 1 + q % nsd;
-        return iq + ((f * S + s) * R + r) * Cp + prefix;
-    };
     float2 x[8];
-    long long q = (long long)blockIdx.x * WAVES + w;
-    if (q < nq) {
-        const float2 *b = row_ptr(q, 0);
+    auto load = [&](long long qq, int r0) {  // rows r0 .. r0 + NR - 1 of symbol qq (wave-uniform)
+        const long long f = qq / nsd, s = 1 + qq % nsd;
+        const float2 *b = iq + ((f * S + s) * R + r0) * Cp + prefix;
 #pragma unroll
-        for (int m = 0; m < 8; ++m) x[m] = b[L + 64 * m];
-    }
+        for (int g = 0; g < NR; ++g)
+#pragma unroll
+            for (int m = 0; m < NP; ++m) x[g * NP + m] = r0 + g < R ? b[g * Cp + L + 64 * m] : float2{0.f, 0.f};
+    };
+    long long q = (long long)blockIdx.x * WAVES + w;
+    if (q < nq) load(q, 0);
     for (; q < nq; q += nw) {
         const long long f = q / nsd;
         v2f acc[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) acc[i] = v2f{0.f, 0.f};
-        for (int r = 0; r < R; ++r) {
+        for (int r0 = 0; r0 < R; r0 += NR) {
             v2f u[8];
 #pragma unroll
             for (int m = 0; m < 8; ++m) u[m] = pk::V(x[m]);
             {
-                const long long qn = r + 1 < R ? q : q + nw;
-                if (qn < nq) {
-                    const float2 *b = row_ptr(qn, r + 1 < R ? r + 1 : 0);
-#pragma unroll
-                    for (int m = 0; m < 8; ++m) x[m] = b[L + 64 * m];
-                }
+                const long long qn = r0 + NR < R ? q : q + nw;
+                if (qn < nq) load(qn, r0 + NR < R ? r0 + NR : 0);
             }
-            const float2 *hrow = Hl + (f * R + r) * (long long)C;
+            // this lane's row; a row past R has zero samples, its (clamped) estimate multiplies zeros
+            const int r = r0 + rho < R ? r0 + rho : R - 1;
+            const float2 *hrow = Hl + (f * R + r) * (long long)C + lw;
             v2f h[8];
 #pragma unroll
-            for (int d = 0; d < 8; ++d) h[d] = pk::V(hrow[d * 64 + L]);
-            td1536::fft512(u, T, L, twA, twB);
+            for (int d = 0; d < 8; ++d) h[d] = pk::V(hrow[d * LW]);
+#pragma unroll
+            for (int g = 0; g < NR; ++g) {  // pass A: DFT_P per row, then W_C^{t s'}
+                v2f a[NP];
+#pragma unroll
+                for (int m = 0; m < NP; ++m) a[m] = u[g * NP + m];
+                pk::fft_reg<NP>(a);
+#pragma unroll
+                for (int k = 1; k < NP; ++k) a[k] = pk::cmul(a[k], twA[k - 1]);
+#pragma unroll
+                for (int m = 0; m < NP; ++m) u[g * NP + m] = a[m];
+            }
+            td1536::fft64x8(u, T, L, twB);
 #pragma unroll
             for (int d = 0; d < 8; ++d) pk::mac(acc[d], u[d], h[d]);
         }
+#pragma unroll
+        for (int o = LW; o < 64; o <<= 1)
+#pragma unroll
+            for (int d = 0; d < 8; ++d) {
+                const float2 a = pk::F(acc[d]);
+                acc[d] += v2f{__shfl_xor(a.x, o), __shfl_xor(a.y, o)};
+            }
+        if (rho != 0) continue;
         float2 *o = out + q * K;
         const float *Pf = P + f * C;
 #pragma unroll
         for (int d = 0; d < 8; ++d) {
-            const int b = (L >> 3) + 8 * (L & 7) + 64 * d;
-            if (b == 0) continue;
+            const int b = (lw >> 3) + NP * (lw & 7) + LW * d;
+            if (b == 0) continue;  // the DC bin carries no subcarrier
             const float2 a = pk::F(acc[d]);
             if (mode == 0) {
                 const float p = Pf[b];
@@ -584,14 +618,17 @@ __global__ void __launch_bounds__(NT) k_mrc_td512(const float2 *__restrict__ iq,
     }
 }
 
-__global__ void __launch_bounds__(256) k_ls_512(const float2 *__restrict__ Y, int R, const float2 *__restrict__ X,
-                                                float2 *__restrict__ Hl, float *__restrict__ P) {
+// LS from the FFT'd pilot rows into the lane order above (as k_ls_1536).
+template <int NR>
+__device__ __forceinline__ void ls_small(const float2 *__restrict__ Y, int R, const float2 *__restrict__ X,
+                                         float2 *__restrict__ Hl, float *__restrict__ P) {
+    constexpr int NP = 8 / NR, C = 64 * NP, LW = 8 * NP;
     const int b = blockIdx.x * 256 + threadIdx.x;
     if (b >= C) return;
     const long long f = blockIdx.y;
-    const int L = 8 * (b & 7) + ((b >> 3) & 7), d = b >> 6;
+    const int pos = (b / LW) * LW + 8 * (b % NP) + ((b / NP) & 7);
     const float2 *Yf = Y + f * (long long)R * C;
-    float2 *Hf = Hl + f * (long long)R * C + d * 64 + L;
+    float2 *Hf = Hl + f * (long long)R * C + pos;
     float p = 0.f;
     if (b == 0) {
         for (int r = 0; r < R; ++r) Hf[(long long)r * C] = float2{0.f, 0.f};
@@ -607,7 +644,24 @@ __global__ void __launch_bounds__(256) k_ls_512(const float2 *__restrict__ Y, in
     P[f * C + b] = p;
 }
 
-}  // namespace td512
+#define OFDM_TD_SMALL(CC, NR)                                                                                          \
+    __global__ void __launch_bounds__(NT) k_mrc_td##CC(const float2 *__restrict__ iq, long long nframes, int S, int R, \
+                                                       int prefix, const float2 *__restrict__ Hl,                      \
+                                                       const float *__restrict__ P, float2 *__restrict__ out,          \
+                                                       int mode) {                                                     \
+        mrc_small<NR>(iq, nframes, S, R, prefix, Hl, P, out, mode);                                                    \
+    }                                                                                                                  \
+    __global__ void __launch_bounds__(256) k_ls_##CC(const float2 *__restrict__ Y, int R,                              \
+                                                     const float2 *__restrict__ X, float2 *__restrict__ Hl,            \
+                                                     float *__restrict__ P) {                                          \
+        ls_small<NR>(Y, R, X, Hl, P);                                                                                  \
+    }
+OFDM_TD_SMALL(512, 1)
+OFDM_TD_SMALL(256, 2)
+OFDM_TD_SMALL(128, 4)
+#undef OFDM_TD_SMALL
+
+}  // namespace tdsmall
 
 namespace {
 
@@ -646,9 +700,12 @@ hipError_t launch_mrc_lane(Kern kern, int nt, int per_cu, int per_wg, const floa
 
 }  // namespace
 
-hipError_t launch_ls_512(const float2 *Y, long long nframes, int R, const float2 *X, float2 *Hl, float *P,
-                         hipStream_t s) {
-    return launch_ls_lane<td512::C>(td512::k_ls_512, Y, nframes, R, X, Hl, P, s);
+hipError_t launch_ls_small(int C, const float2 *Y, long long nframes, int R, const float2 *X, float2 *Hl, float *P,
+                           hipStream_t s) {
+    return C == 512   ? launch_ls_lane<512>(tdsmall::k_ls_512, Y, nframes, R, X, Hl, P, s)
+           : C == 256 ? launch_ls_lane<256>(tdsmall::k_ls_256, Y, nframes, R, X, Hl, P, s)
+           : C == 128 ? launch_ls_lane<128>(tdsmall::k_ls_128, Y, nframes, R, X, Hl, P, s)
+                      : hipErrorInvalidValue;
 }
 
 hipError_t launch_ls_1536(const float2 *Y, long long nframes, int R, const float2 *X, float2 *Hl, float *P,
@@ -666,11 +723,13 @@ hipError_t launch_ls_6144(const float2 *Y, long long nframes, int R, const float
     return launch_ls_lane<td6144::C>(td6144::k_ls_6144, Y, nframes, R, X, Hl, P, s);
 }
 
-// 512: 4 one-wave symbols per workgroup, 4 workgroups per CU.
-hipError_t launch_mrc_td512(const float2 *iq, long long nframes, int S, int R, int prefix, const float2 *Hl,
+// 512 / 256 / 128: 4 one-wave symbols per workgroup, 4 workgroups per CU.
+hipError_t launch_mrc_small(int C, const float2 *iq, long long nframes, int S, int R, int prefix, const float2 *Hl,
                             const float *P, float2 *out, int mode, hipStream_t s) {
-    return launch_mrc_lane(td512::k_mrc_td512, td512::NT, 4, td512::WAVES, iq, nframes, S, R, prefix, Hl, P, out,
-                           mode, s);
+    using namespace tdsmall;
+    auto kern = C == 512 ? k_mrc_td512 : C == 256 ? k_mrc_td256 : C == 128 ? k_mrc_td128 : nullptr;
+    if (!kern) return hipErrorInvalidValue;
+    return launch_mrc_lane(kern, NT, 4, WAVES, iq, nframes, S, R, prefix, Hl, P, out, mode, s);
 }
 
 // 1536: 4 one-wave symbols per workgroup, 2 workgroups per CU (2 waves / SIMD).

@@ -62,10 +62,11 @@ hipError_t launch_ls_3072(const float2 *Y, long long nframes, int R, const float
                           hipStream_t s);
 hipError_t launch_mrc_td3072(const float2 *iq, long long nframes, int S, int R, int prefix, const float2 *Hl,
                              const float *P, float2 *out, int mode, hipStream_t s);
-// ... C = 512 on one wave per symbol (same file)
-hipError_t launch_ls_512(const float2 *Y, long long nframes, int R, const float2 *X, float2 *Hl, float *P,
-                         hipStream_t s);
-hipError_t launch_mrc_td512(const float2 *iq, long long nframes, int S, int R, int prefix, const float2 *Hl,
+// ... C = 512 / 256 / 128 on one wave per symbol (same file; other C:
+// hipErrorInvalidValue)
+hipError_t launch_ls_small(int C, const float2 *Y, long long nframes, int R, const float2 *X, float2 *Hl, float *P,
+                           hipStream_t s);
+hipError_t launch_mrc_small(int C, const float2 *iq, long long nframes, int S, int R, int prefix, const float2 *Hl,
                             const float *P, float2 *out, int mode, hipStream_t s);
 // ... and C = 6144 on a wave quad per symbol (same file)
 hipError_t launch_ls_6144(const float2 *Y, long long nframes, int R, const float2 *X, float2 *Hl, float *P,

@@ -89,8 +89,9 @@ __device__ __forceinline__ int hc_pos(int b, int C) {  // C = 0: bin layout
         const int q = b / 3, j = b - 3 * q, e = q & 1, kk = q >> 1;
         return e * 1536 + (8 * j + (kk >> 6)) * 64 + 8 * (kk & 7) + ((kk >> 3) & 7);
     }
-    if (C == 512) {  // slot d of lane 8 s + c holds bin s + 8 c + 64 d
-        return (b >> 6) * 64 + 8 * (b & 7) + ((b >> 3) & 7);
+    if (C == 512 || C == 256 || C == 128) {  // P = C / 64: slot d of lane 8 s + c holds bin s + P c + 8 P d
+        const int np = C >> 6, lw = 8 * np;
+        return (b / lw) * lw + 8 * (b % np) + ((b / np) & 7);
     }
     if (C == 6144) {  // wave e, slot 8 j + d of lane 8 s + c holds bin 3 (4 (s + 8 c + 64 d) + e) + j
         const int q = b / 3, j = b - 3 * q, e = q & 3, kk = q >> 2;

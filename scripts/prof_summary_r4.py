@@ -54,13 +54,13 @@ def dominant(bench):
     cfg = bench["config"]
     if "R_total" in cfg:  # split mode: the partial-numerator MRC
         return {1024: "k_mrc_td1024_hlds", 2048: "k_mrc_td2048", 4096: "k_mrc_td4096h",
-                1536: "k_mrc_td1536", 3072: "k_mrc_td3072", 6144: "k_mrc_td6144", 512: "k_mrc_td512"}.get(cfg["C"], "k_mrc_any")
+                1536: "k_mrc_td1536", 3072: "k_mrc_td3072", 6144: "k_mrc_td6144", 512: "k_mrc_td512", 256: "k_mrc_td256", 128: "k_mrc_td128"}.get(cfg["C"], "k_mrc_any")
     if cfg.get("domain") == "freq":
         return "k_mrc_freq"
     if cfg.get("flow") == "one-launch":
         return "k_demod_td"
     return {1024: "k_mrc_td1024_hlds", 2048: "k_mrc_td2048", 4096: "k_mrc_td4096h",
-            1536: "k_mrc_td1536", 3072: "k_mrc_td3072", 6144: "k_mrc_td6144", 512: "k_mrc_td512"}.get(cfg["C"], "k_mrc_any")
+            1536: "k_mrc_td1536", 3072: "k_mrc_td3072", 6144: "k_mrc_td6144", 512: "k_mrc_td512", 256: "k_mrc_td256", 128: "k_mrc_td128"}.get(cfg["C"], "k_mrc_any")
 
 
 def main():

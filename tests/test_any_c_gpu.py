@@ -59,7 +59,8 @@ def test_fft_rows_any_c_many_rows(ofdm, dev):
     assert np.abs(got - ref).max() <= 1e-5 * np.abs(ref).max()
 
 
-@pytest.mark.parametrize("C,R,prefix", [(6, 3, 0), (12, 1, 3), (512, 1, 0), (512, 32, 36), (600, 4, 44), (1021, 3, 0), (1200, 8, 84),
+@pytest.mark.parametrize("C,R,prefix", [(6, 3, 0), (12, 1, 3), (128, 5, 9), (128, 64, 32), (256, 7, 18), (256, 64, 0),
+                                        (512, 1, 0), (512, 32, 36), (600, 4, 44), (1021, 3, 0), (1200, 8, 84),
                                         (1536, 8, 108), (1536, 64, 0), (3000, 2, 0), (3072, 3, 0), (3072, 16, 216),
                                         (6144, 4, 432), (6144, 12, 0),
                                         (8192, 2, 512)])
@@ -114,9 +115,9 @@ def test_stages_any_c_vs_oracle(ofdm, oracle, dev, C, R):
                           np.stack([oracle.shift_one_row(r) for r in rows]))
 
 
-@pytest.mark.parametrize("C,R,prefix", [(512, 7, 36), (1536, 6, 16), (3072, 5, 24), (6144, 4, 40), (1200, 3, 0)])
+@pytest.mark.parametrize("C,R,prefix", [(128, 7, 9), (256, 10, 18), (512, 7, 36), (1536, 6, 16), (3072, 5, 24), (6144, 4, 40), (1200, 3, 0)])
 def test_estimate_export_and_antenna_partials_any_c(ofdm, oracle, dev, C, R, prefix):
-    """The estimate of a non-fused size (C = 1536: the lane order of
+    """The estimate of a non-fused size (C = 128 ... 6144: the lane orders of
     frame_td_fft512.hip; 1200: the bin layout) exported to the reference layout
     matches the oracle's LS; the antenna-split partials (numerators + |H|^2)
     summed over two shards and finalised give the full receiver's output."""
@@ -146,7 +147,7 @@ def test_estimate_export_and_antenna_partials_any_c(ofdm, oracle, dev, C, R, pre
     parity(host(out), full)
 
 
-@pytest.mark.parametrize("C", [512, 1536, 3072, 6144, 600])
+@pytest.mark.parametrize("C", [128, 256, 512, 1536, 3072, 6144, 600])
 @pytest.mark.parametrize("F,S,R,prefix", [(1, 2, 1, 0), (3, 2, 2, -1), (2, 9, 1, 7)])
 def test_small_batches_any_c_vs_oracle(ofdm, oracle, dev, C, F, S, R, prefix):
     """Edge shapes of the fused non-power-of-two receivers: one data symbol per
