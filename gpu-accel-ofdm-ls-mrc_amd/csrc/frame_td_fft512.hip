@@ -44,6 +44,12 @@ __device__ __forceinline__ void wsync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// IQ samples are streamed once: non-temporal loads keep the L2 for the
+// per-frame channel estimates every data symbol of the frame re-reads.
+__device__ __forceinline__ float2 ld_stream(const float2 *p) {
+    return __builtin_bit_cast(float2, __builtin_nontemporal_load(reinterpret_cast<const unsigned long long *>(p)));
+}
+
 // bin of lane L's slot i (i = 8 j + d)
 __device__ __forceinline__ int bin_of(int L, int i) {
     return 3 * ((L >> 3) + 8 * (L & 7) + 64 * (i & 7)) + (i >> 3);
@@ -112,7 +118,7 @@ k_mrc_td1536(const float2 *__restrict__ iq, long long nframes, int S, int R, int
     if (q < nq) {
         const float2 *b = row_ptr(q, 0);
 #pragma unroll
-        for (int m = 0; m < 24; ++m) x[m] = b[L + 64 * m];
+        for (int m = 0; m < 24; ++m) x[m] = ld_stream(b + L + 64 * m);
     }
     for (; q < nq; q += nw) {
         const long long f = q / nsd;
@@ -139,7 +145,7 @@ k_mrc_td1536(const float2 *__restrict__ iq, long long nframes, int S, int R, int
                 if (qn < nq) {
                     const float2 *b = row_ptr(qn, r + 1 < R ? r + 1 : 0);
 #pragma unroll
-                    for (int m = 0; m < 24; ++m) x[m] = b[L + 64 * m];
+                    for (int m = 0; m < 24; ++m) x[m] = ld_stream(b + L + 64 * m);
                 }
             }
             const float2 *hrow = Hl + (f * R + r) * (long long)C;
@@ -259,7 +265,7 @@ k_mrc_td3072(const float2 *__restrict__ iq, long long nframes, int S, int R, int
 #pragma unroll
         for (int i = 0; i < 3; ++i)
 #pragma unroll
-            for (int m = 0; m < 8; ++m) x[8 * i + m] = b[L + 64 * (m + 8 * e + 16 * i)];
+            for (int m = 0; m < 8; ++m) x[8 * i + m] = td1536::ld_stream(b + L + 64 * (m + 8 * e + 16 * i));
     };
     float2 x[24];
     long long q = blockIdx.x;
@@ -407,7 +413,7 @@ k_mrc_td6144(const float2 *__restrict__ iq, long long nframes, int S, int R, int
 #pragma unroll
         for (int i = 0; i < 3; ++i)
 #pragma unroll
-            for (int m = 0; m < 8; ++m) x[8 * i + m] = b[L + 64 * (m + 8 * e + 32 * i)];
+            for (int m = 0; m < 8; ++m) x[8 * i + m] = td1536::ld_stream(b + L + 64 * (m + 8 * e + 32 * i));
     };
     float2 x[24];
     long long q = blockIdx.x;
@@ -555,7 +561,7 @@ __device__ __forceinline__ void mrc_small(const float2 *__restrict__ iq, long lo
 #pragma unroll
         for (int g = 0; g < NR; ++g)
 #pragma unroll
-            for (int m = 0; m < NP; ++m) x[g * NP + m] = r0 + g < R ? b[g * Cp + L + 64 * m] : float2{0.f, 0.f};
+            for (int m = 0; m < NP; ++m) x[g * NP + m] = r0 + g < R ? td1536::ld_stream(b + g * Cp + L + 64 * m) : float2{0.f, 0.f};
     };
     long long q = (long long)blockIdx.x * WAVES + w;
     if (q < nq) load(q, 0);
