@@ -97,7 +97,7 @@ k_mrc_td1536(const float2 *__restrict__ iq, long long nframes, int S, int R, int
         tab[e] = float2{(float)cs, (float)sn};
     }
     __syncthreads();
-    const int w = threadIdx.x >> 6, L = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), L = threadIdx.x & 63;  // w uniform: q, f, row pointers scalar
     float2 *T = img[w];
     // row invariants: W512^{t s} = W1536^{3 t s} (t = L), W64^{a c} = W1536^{24 a c} (a = L & 7)
     v2f twA[7], twB[7];
@@ -122,6 +122,8 @@ k_mrc_td1536(const float2 *__restrict__ iq, long long nframes, int S, int R, int
     }
     for (; q < nq; q += nw) {
         const long long f = q / nsd;
+        // this symbol's antenna rows and the next symbol's first row: one division per symbol
+        const float2 *cur = row_ptr(q, 0), *nxt = q + nw < nq ? row_ptr(q + nw, 0) : nullptr;
         v2f acc[24];
 #pragma unroll
         for (int i = 0; i < 24; ++i) acc[i] = v2f{0.f, 0.f};
@@ -141,9 +143,8 @@ k_mrc_td1536(const float2 *__restrict__ iq, long long nframes, int S, int R, int
             }
             // the next row (or the next symbol's first) in flight during the transforms
             {
-                const long long qn = r + 1 < R ? q : q + nw;
-                if (qn < nq) {
-                    const float2 *b = row_ptr(qn, r + 1 < R ? r + 1 : 0);
+                const float2 *b = r + 1 < R ? cur + (r + 1) * Cp : nxt;
+                if (b) {
 #pragma unroll
                     for (int m = 0; m < 24; ++m) x[m] = ld_stream(b + L + 64 * m);
                 }
@@ -241,7 +242,7 @@ k_mrc_td3072(const float2 *__restrict__ iq, long long nframes, int S, int R, int
         sincospi(-2.0 * (double)e / (double)C, &sn, &cs);
         tab[e] = float2{(float)cs, (float)sn};
     }
-    const int e = threadIdx.x >> 6, L = threadIdx.x & 63;
+    const int e = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), L = threadIdx.x & 63;
     v2f twA[7], twB[7];  // W512^{t s}, W64^{a c}: the FFT512 row invariants
 #pragma unroll
     for (int k = 1; k < 8; ++k) {
@@ -272,6 +273,7 @@ k_mrc_td3072(const float2 *__restrict__ iq, long long nframes, int S, int R, int
     if (q < nq) load(x, row_ptr(q, 0));
     for (; q < nq; q += np) {
         const long long f = q / nsd;
+        const float2 *cur = row_ptr(q, 0), *nxt = q + np < nq ? row_ptr(q + np, 0) : nullptr;
         v2f acc[24];
 #pragma unroll
         for (int i = 0; i < 24; ++i) acc[i] = v2f{0.f, 0.f};
@@ -289,8 +291,8 @@ k_mrc_td3072(const float2 *__restrict__ iq, long long nframes, int S, int R, int
                 u[2][m] = pk::cmul(t0 - jd, pk::V(tab[2 * n]));
             }
             {
-                const long long qn = r + 1 < R ? q : q + np;
-                if (qn < nq) load(x, row_ptr(qn, r + 1 < R ? r + 1 : 0));
+                const float2 *b = r + 1 < R ? cur + (r + 1) * Cp : nxt;
+                if (b) load(x, b);
             }
 #pragma unroll
             for (int j = 0; j < 3; ++j)
@@ -537,7 +539,7 @@ __device__ __forceinline__ void mrc_small(const float2 *__restrict__ iq, long lo
                                           float2 *__restrict__ out, int mode) {
     constexpr int NP = 8 / NR, C = 64 * NP, K = C - 1, LW = 8 * NP;
     __shared__ float2 img[WAVES][td1536::TS];
-    const int w = threadIdx.x >> 6, L = threadIdx.x & 63, rho = L / LW, lw = L % LW;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), L = threadIdx.x & 63, rho = L / LW, lw = L % LW;
     float2 *T = img[w];
     v2f twA[NP > 1 ? NP - 1 : 1], twB[7];
 #pragma unroll
@@ -555,18 +557,21 @@ __device__ __forceinline__ void mrc_small(const float2 *__restrict__ iq, long lo
     const int nsd = S - 1;
     const long long Cp = C + prefix, nq = nframes * nsd, nw = (long long)gridDim.x * WAVES;
     float2 x[8];
-    auto load = [&](long long qq, int r0) {  // rows r0 .. r0 + NR - 1 of symbol qq (wave-uniform)
+    auto row_ptr = [&](long long qq) {  // antenna row 0 of data symbol qq
         const long long f = qq / nsd, s = 1 + qq % nsd;
-        const float2 *b = iq + ((f * S + s) * R + r0) * Cp + prefix;
+        return iq + (f * S + s) * R * Cp + prefix;
+    };
+    auto load = [&](const float2 *b, int r0) {  // rows r0 .. r0 + NR - 1 from row r0 at b (wave-uniform)
 #pragma unroll
         for (int g = 0; g < NR; ++g)
 #pragma unroll
             for (int m = 0; m < NP; ++m) x[g * NP + m] = r0 + g < R ? td1536::ld_stream(b + g * Cp + L + 64 * m) : float2{0.f, 0.f};
     };
     long long q = (long long)blockIdx.x * WAVES + w;
-    if (q < nq) load(q, 0);
+    if (q < nq) load(row_ptr(q), 0);
     for (; q < nq; q += nw) {
         const long long f = q / nsd;
+        const float2 *cur = row_ptr(q), *nxt = q + nw < nq ? row_ptr(q + nw) : nullptr;
         v2f acc[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) acc[i] = v2f{0.f, 0.f};
@@ -575,8 +580,8 @@ __device__ __forceinline__ void mrc_small(const float2 *__restrict__ iq, long lo
 #pragma unroll
             for (int m = 0; m < 8; ++m) u[m] = pk::V(x[m]);
             {
-                const long long qn = r0 + NR < R ? q : q + nw;
-                if (qn < nq) load(qn, r0 + NR < R ? r0 + NR : 0);
+                const float2 *b = r0 + NR < R ? cur + (r0 + NR) * Cp : nxt;
+                if (b) load(b, r0 + NR < R ? r0 + NR : 0);
             }
             // this lane's row; a row past R has zero samples, its (clamped) estimate multiplies zeros
             const int r = r0 + rho < R ? r0 + rho : R - 1;
