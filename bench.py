@@ -82,6 +82,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target wall time of the CPU-baseline sample")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-box", action="store_true",
+                    help="skip the same-box HBM probes and the diagnostic-build clock reading")
+    ap.add_argument("--stamps-out", default=None,
+                    help="save the diagnostic build's per-workgroup stamps (.npy) for scripts/wg_timeline.py")
     ap.add_argument("--no-mode-a", action="store_true",
                     help="skip the supplementary frequency-domain (mode A) measurement of the default mode")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
@@ -102,11 +106,8 @@ def cpu_baseline(args, X, ofdm, torch, dev):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from oracle_bindings import Oracle
     o = Oracle()
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    threads = max(1, min(16, cores))  # the box's CPU share is 16
+    share = host_cpu_share()
+    threads = share["threads"]
     Xh = X.cpu().numpy()
 
     def sample(nf):
@@ -147,11 +148,11 @@ def cpu_baseline(args, X, ofdm, torch, dev):
     d1 = time.perf_counter() - t0
     fft = "none (frequency-domain input)" if freq else \
         "float32 scalar radix-2 (oracle_fft_row_f32, twiddle table reused; FFTW's SIMD codelets are not available here)"
-    # cores = the threads the sample ran on (the bench contract); the host's
-    # own count (sched_getaffinity: on the GPU box the whole machine, of which
-    # this job's CPU share is 16) is reported beside it
+    # cores = the threads the sample ran on (the bench contract), i.e. the
+    # CPU share this job has on the box (cgroup quota, else the affinity
+    # mask, else os.cpu_count()); how that share was read is reported beside it
     return {"value": syms / dt, "unit": "symbols/s", "cores": threads, "threads": threads,
-            "host_cores_affinity": cores, "host_cpu_share": 16, "kind": "port", "fft": fft,
+            "cpu_share": share, "kind": "port", "fft": fft,
             "sample": f"{passes} x {nf} frames x {args.S} symbols (R={args.R}, C={args.C}, prefix="
                       f"{args.prefix}), {'LS+MRC+rotate (frequency domain)' if freq else 'FFT+LS+MRC+rotate'}, "
                       f"FFT: {'none' if freq else 'float32 scalar radix-2'}, OpenMP over frames, "
@@ -159,6 +160,133 @@ def cpu_baseline(args, X, ofdm, torch, dev):
             "configs0_single_thread": {"value": reps * 99 / d1, "unit": "symbols/s", "cores": 1, "fft": fft,
                                        "sample": f"R=4, C=1024, 1 frame x 100 symbols, {reps} repetitions, "
                                                  f"FFT float32 scalar radix-2, {d1:.2f} s wall"}}
+
+
+def host_cpu_share():
+    """The CPU share of this job, read from the box: the cgroup v2 quota
+    (cpu.max "quota period", or v1 cfs_quota_us / cfs_period_us), else the
+    affinity mask, else os.cpu_count().  threads = the share rounded down
+    (at least 1), capped by the affinity mask."""
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count() or 1
+    quota, src = None, None
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            with open(path) as fp:
+                q, per = fp.read().split()[:2]
+            if q != "max":
+                quota, src = int(q) / int(per), path
+        except (OSError, ValueError):
+            pass
+    if quota is None:
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as fp:
+                q = int(fp.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as fp:
+                per = int(fp.read())
+            if q > 0:
+                quota, src = q / per, "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"
+        except (OSError, ValueError):
+            pass
+    if quota is not None:
+        threads = max(1, min(affinity, int(quota)))
+    else:
+        threads, src = affinity, "sched_getaffinity"
+    return {"threads": threads, "cgroup_quota_cpus": quota, "affinity_cpus": affinity,
+            "os_cpu_count": os.cpu_count(), "source": src}
+
+
+def box_probe(ofdm, torch, dev, stream, gib=4, reps=5):
+    """Same-box HBM ceilings, timed in this process right after the timed
+    loop: a float4 copy of `gib` GiB (read + written bytes counted) and a
+    float4 read of the same source (ofdm_hbm_probe, plain 16-B accesses over
+    the whole chip).  Median of `reps` launches by HIP events."""
+    n = gib << 30
+    src = torch.empty(n, dtype=torch.uint8, device=dev)
+    src.view(torch.float32).uniform_()
+    dst = torch.empty(n, dtype=torch.uint8, device=dev)
+    res = {}
+    for mode, name, moved in ((0, "copy", 2 * n), (1, "read", n)):
+        sink = dst if mode == 0 else dst[: 8 << 20]
+        ofdm.hbm_probe(mode, src, sink, stream)  # warm
+        ts = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            ofdm.hbm_probe(mode, src, sink, stream)
+            e1.record(stream)
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        ts.sort()
+        res[name] = moved / (ts[len(ts) // 2] * 1e-3) / 1e9
+    del src, dst
+    torch.cuda.empty_cache()
+    return {"box_copy_GBps": res["copy"], "box_read_GBps": res["read"],
+            "box_probe": f"ofdm_hbm_probe float4 over {gib} GiB, median of {reps}; copy counts read + written bytes"}
+
+
+DIAG_LIB = os.path.join(ROOT, "gpu-accel-ofdm-ls-mrc_amd", "lib", "libofdm_lsmrc_diag.so")
+DIAG_TAG = {1024: "td1024", 2048: "td2048", 4096: "td4096"}
+
+
+def stamps_summary(rec):
+    """Per-workgroup records of the diagnostic build (csrc/diag.hpp): rt0,
+    rt_mark, rt_end (100 MHz), mt0, mt_end (shader clock), hw_id, xcc_id,
+    block.  Effective clock = d(memtime) / d(memrealtime) x 100 MHz."""
+    import numpy as np
+    rec = rec[rec[:, 2] > 0]
+    if not len(rec):
+        return None
+    drt = (rec[:, 2] - rec[:, 0]).astype(np.float64)
+    dmt = (rec[:, 4] - rec[:, 3]).astype(np.float64)
+    ok = drt > 0
+    ghz = dmt[ok] / drt[ok] * 0.1
+    span = (rec[:, 2].max() - rec[:, 0].min()) * 1e-5  # ms
+    return {"effective_GHz_median": float(np.median(ghz)), "effective_GHz_p10": float(np.percentile(ghz, 10)),
+            "effective_GHz_p90": float(np.percentile(ghz, 90)),
+            "busy_weighted_GHz": float(dmt[ok].sum() / drt[ok].sum() * 0.1),
+            "workgroups": int(len(rec)), "stamped_span_ms": float(span)}
+
+
+def clock_probe(step_diag, tag, ofdm, torch, stream, reps=3, save=None):
+    """Effective clock of the timed kernel: the diagnostic build of the SAME
+    kernel (make diag; per-workgroup s_memtime / s_memrealtime stamps, no
+    other change) run `reps` times right after the timed loop on the same
+    batch; the stamps of the last launch give the clock per workgroup."""
+    import ctypes
+    import numpy as np
+    if not os.path.exists(DIAG_LIB) or tag is None:
+        return None
+    L = ofdm.load_library(DIAG_LIB)
+    clear, read = getattr(L, f"ofdm_diag_clear_{tag}"), getattr(L, f"ofdm_diag_read_{tag}")
+    read.argtypes = [ctypes.c_void_p, ctypes.c_longlong]
+    ts = []
+    with ofdm.using(L):
+        for i in range(reps):
+            torch.cuda.synchronize()
+            if i == reps - 1:
+                clear()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            step_diag()
+            e1.record(stream)
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1))
+    nwg = 1 << 17
+    rec = np.zeros((nwg, 8), dtype=np.uint64)
+    if read(rec.ctypes.data, nwg) != 0:
+        return None
+    if save:
+        np.save(save, rec[rec[:, 2] > 0])
+    out = stamps_summary(rec)
+    if out is None:
+        return None
+    out.update({"diag_launch_ms": ts, "source": f"lib/libofdm_lsmrc_diag.so (the same kernel with per-workgroup "
+                                                f"s_memtime/s_memrealtime stamps, csrc/diag.hpp), {reps} launches "
+                                                f"right after the timed loop, stamps of the last"})
+    return out
 
 
 def pmc_traffic(path, cfg):
@@ -365,15 +493,49 @@ def main():
     errs = int(ofdm.count_symbol_errors(out, S, seed=args.seed, frame0=rank * F).item())
     same = bool(torch.equal(out, out_w))
     del out_w
+    torch.cuda.empty_cache()
+
+    # same-box context, after the timed loop (never inside it): the HBM copy /
+    # read ceilings of this box, and the effective clock of the timed kernel
+    # from its diagnostic build on the same batch
+    box = box_probe(ofdm, torch, dev, stream) if not args.no_box else None
+    clock = None
+    if not args.no_box:
+        ws_d = ofdm.workspace(F, S, R, C, dev)
+        out_d = ofdm.c64((F, S - 1, K), dev)
+
+        def step_diag():
+            if one:
+                ofdm.frame_demod(iq, X, prefix, ws=ws_d, out=out_d, stream=stream)
+            else:
+                ofdm.frame_estimate(iq, X, prefix, ws_d, stream)
+                ofdm.frame_combine(iq, prefix, ws_d, out_d, stream)
+        clock = clock_probe(step_diag, None if freq else DIAG_TAG.get(C), ofdm, torch, stream,
+                            save=args.stamps_out)
+        del ws_d, out_d
+        torch.cuda.empty_cache()
+
+    # per-rank spread (a SCALE shortfall points at a slow rank or at skew)
+    rank_vals = [elapsed, mrc_ms, box["box_copy_GBps"] if box else float("nan"),
+                 clock["effective_GHz_median"] if clock else float("nan")]
     stats = torch.tensor([elapsed, float(errs), float(errs_warm), 0.0 if same else 1.0],
                          dtype=torch.float64, device=dev)
+    per_rank = None
     if world > 1:
         mx = stats.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         tot = stats.clone()
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         elapsed, errs, errs_warm, same = float(mx[0]), int(tot[1]), int(tot[2]), float(tot[3]) == 0.0
-    if not same or errs:
+        rv = torch.tensor(rank_vals, dtype=torch.float64, device=dev)
+        lo, hi = rv.clone(), rv.clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        names = ["step_ms", "kernel_ms", "box_copy_GBps", "effective_GHz"]
+        scale = [1e3 / args.steps, 1.0, 1.0, 1.0]
+        per_rank = {n: {"min": float(lo[i]) * scale[i], "max": float(hi[i]) * scale[i]} for i, n in enumerate(names)}
+    failed = not same or errs > 0
+    if failed:
         log(f"CHECK FAILURE: timed output equals warm-up: {same}, QPSK errors on the timed output: {errs}")
 
     dom = "frequency-domain symbols (FFT upstream)" if freq else "time-domain IQ"
@@ -415,14 +577,29 @@ def main():
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                      "traffic_source": tsrc,
                      "bytes_per_launch": bytes_launch, "avg_launch_ms": mrc_ms,
-                     "median_launch_ms": mrc_median},
+                     "median_launch_ms": mrc_median,
+                     "box_copy_GBps": box["box_copy_GBps"] if box else None,
+                     "frac_of_box_copy": achieved / box["box_copy_GBps"] if box else None,
+                     "box_read_GBps": box["box_read_GBps"] if box else None,
+                     "frac_of_box_read": achieved / box["box_read_GBps"] if box else None,
+                     "box_probe": box["box_probe"] if box else None},
+        "clock": clock,
         "stages_ms": {"demod_one_launch": mrc_ms} if one else {"estimate_ls": ls_ms, "combine_mrc": mrc_ms},
         "step_algorithmic_GBps": step_bytes / (elapsed / args.steps) / 1e9,
+        "per_rank": per_rank,
         "check": {"qpsk_symbol_errors": errs, "timed_equals_warmup": same,
                   "qpsk_symbol_errors_warmup": errs_warm,
                   "checked_output": "the last timed step's (its buffer NaN-filled before the warm-up)"},
         "cpu_baseline": None,
     }
+    if failed:  # a broken run never yields a throughput that counts
+        result["status"] = "CHECK_FAILED"
+        result["value"] = None
+        if rank == 0:
+            print(json.dumps(result), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        sys.exit(1)
     if world == 1 and not freq and not args.no_mode_a:
         del iq
         torch.cuda.empty_cache()
@@ -607,6 +784,18 @@ def bench_split(args, X, dev, world, rank, barrier):
     if rank == 0:
         check["vs_full_receiver"] = split_vs_full(ofdm, torch, X, out, F, S, R * world, C, prefix, args)
 
+    # stage times of one more (untimed) step, per rank, then max over ranks:
+    # partial LS / partial FFT+MRC / finalise on the compute stream, the
+    # communication the overlap left exposed, and the collectives alone
+    barrier()
+    stages = pipe.profile_step(iq, X, out, stream=torch.cuda.current_stream())
+    keys = sorted(k for k, v in stages.items() if isinstance(v, float))
+    if world > 1:
+        v = torch.tensor([stages[k] for k in keys], dtype=torch.float64, device=dev)
+        dist.all_reduce(v, op=dist.ReduceOp.MAX)
+        stages.update({k: float(v[i]) for i, k in enumerate(keys)})
+    stages["reduction"] = "max over ranks" if world > 1 else "one rank"
+
     # roofline of the dominant kernel: the partial FFT+MRC over the whole
     # local batch, HIP events on its stream (outside the timed region)
     stream = torch.cuda.current_stream()
@@ -651,6 +840,7 @@ def bench_split(args, X, dev, world, rank, barrier):
                      "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
                      "bytes_per_launch": Q * b_sym, "avg_launch_ms": mrc_ms,
                      "median_launch_ms": mrc_median},
+        "stages_ms": stages,
         "check": check,
         "cpu_baseline": None,
     }

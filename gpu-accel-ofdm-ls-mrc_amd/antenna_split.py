@@ -123,29 +123,100 @@ class SplitPipeline:
         # synchronously.  RCCL (the product backend) never takes this branch.
         self.host_coll = (dist.get_backend(group) == "gloo" and torch.device(device).type == "cuda")
 
-    def run(self, shard, X, out, stream=None):
+    def run(self, shard, X, out, stream=None, timing=None):
         """shard: (F, S, R_local, C + prefix) on this rank; out: (F, S-1, K).
         stream: a torch.cuda.Stream to run on (default: the current stream).
         The whole step -- kernels, collectives and their waits -- is issued
         with `stream` as torch's current stream, because the async
         collectives and work.wait() order themselves against the current
-        stream: kernels on any other stream could race them."""
+        stream: kernels on any other stream could race them.
+        timing: a dict to receive HIP events of the step's stages on that
+        stream (profile_step; never in a timed step)."""
         if stream is not None and self.ops is HipOps:
             import torch
             with torch.cuda.stream(stream):
-                return self._run(shard, X, out)
-        return self._run(shard, X, out)
+                return self._run(shard, X, out, timing=timing)
+        return self._run(shard, X, out, timing=timing)
 
-    def _run(self, shard, X, out, stream=None):
+    def profile_step(self, shard, X, out, stream=None):
+        """Stage times of ONE step (ms, HIP events on the compute stream), for
+        a SCALE run that falls short: the partial LS, the partial FFT+MRC and
+        the finalise summed over chunks; `exposed_comm` = the time the
+        compute stream spent blocked in the waits for the collectives (what
+        the overlap did not hide); and the two collectives timed alone
+        (issued and waited one by one on the last chunk's buffers), so
+        exposed can be read against what they cost."""
+        import time
+        import torch
+        import torch.distributed as dist
+        if stream is None:
+            stream = torch.cuda.current_stream() if torch.cuda.is_available() and self.ops is HipOps else None
+        ev = {}
+        if stream is not None:
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        self.run(shard, X, out, stream=stream, timing=ev)
+        if stream is not None:
+            torch.cuda.synchronize()
+        wall = (time.perf_counter() - t0) * 1e3
+
+        def span(a, b):
+            return sum(x.elapsed_time(y) for x, y in zip(ev.get(a, []), ev.get(b, [])))
+        st = {"step_wall_ms": wall}
+        if ev:
+            st.update({"ls_partial": span("ls0", "ls1"), "mrc_partial": span("ls1", "mrc1"),
+                       "exposed_comm": span("w0", "w1"), "finalize": span("w1", "fin1"),
+                       "step_events_ms": ev["ls0"][0].elapsed_time(ev["fin1"][-1])})
+        # the collectives alone, on the last buffers used
+        b = 0
+        fc = min(self.chunk, self.F)
+        iso = {}
+        for name in ("all_reduce", "reduce_scatter"):
+            if stream is not None:
+                torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            if name == "all_reduce":
+                if self.host_coll:
+                    Ph = self.P[b][:fc].cpu()
+                    dist.all_reduce(Ph, group=self.group)
+                else:
+                    dist.all_reduce(self.P[b][:fc], group=self.group)
+            else:
+                if self.host_coll:
+                    mine_h = torch_real(self.mine[b]).cpu()
+                    dist.reduce_scatter_tensor(mine_h, torch_real(self.num[b]).cpu(), group=self.group)
+                else:
+                    dist.reduce_scatter_tensor(torch_real(self.mine[b]), torch_real(self.num[b]),
+                                               group=self.group)
+            if stream is not None:
+                torch.cuda.synchronize()
+            iso[name] = (time.perf_counter() - t0) * 1e3
+        nchunks = -(-self.F // self.chunk)
+        st.update({"all_reduce_alone_per_chunk": iso["all_reduce"],
+                   "reduce_scatter_alone_per_chunk": iso["reduce_scatter"],
+                   "chunks": nchunks,
+                   "collectives_alone_step": (iso["all_reduce"] + iso["reduce_scatter"]) * nchunks,
+                   "collective_path": "host-staged (gloo rehearsal)" if self.host_coll else "device (RCCL)"})
+        return st
+
+    def _run(self, shard, X, out, stream=None, timing=None):
         import torch
         import torch.distributed as dist
         F, S, K = self.F, self.S, self.K
         pending = []
 
+        def mark(name):  # HIP events on the current stream (kernel stand-ins of the CPU tests: none)
+            if timing is not None and self.ops is HipOps:
+                e = torch.cuda.Event(enable_timing=True)
+                e.record()
+                timing.setdefault(name, []).append(e)
+
         def finalize(c, b, wp, wn):
+            mark("w0")
             if wp is not None:
                 wp.wait()
                 wn.wait()
+            mark("w1")
             f0 = c * self.chunk
             fc = min(self.chunk, F - f0)
             n = fc * (S - 1) * K
@@ -154,6 +225,7 @@ class SplitPipeline:
             if count:
                 self.ops.mrc_finalize(self.mine[b][:count], e0, S - 1, K, self.P[b][:fc],
                                       out[f0:f0 + fc], stream=stream)
+            mark("fin1")
 
         nchunks = -(-F // self.chunk)
         for c in range(nchunks):
@@ -162,7 +234,9 @@ class SplitPipeline:
             fc = min(self.chunk, F - f0)
             part = shard[f0:f0 + fc]
             P = self.P[b][:fc]
+            mark("ls0")
             _, self.ws[b] = self.ops.ls_partial(part, X, self.prefix, ws=self.ws[b], P=P, stream=stream)
+            mark("ls1")
             if self.host_coll:
                 Ph = P.cpu()
                 dist.all_reduce(Ph, group=self.group)
@@ -172,6 +246,7 @@ class SplitPipeline:
             n = fc * (S - 1) * K
             num = self.num[b][:n].view(fc, S - 1, K)
             self.ops.mrc_partial(part, self.ws[b], self.prefix, num=num, stream=stream)
+            mark("mrc1")
             flat = self.num[b] if n == self.per * self.world else self._padded(b, n)
             if self.host_coll:
                 mine_h = torch_real(self.mine[b]).cpu()

@@ -659,6 +659,15 @@ int ofdm_count_symbol_errors(const ofdm_cf32 *d_out, long long nframes, int S, i
                      "ofdm_count_symbol_errors");
 }
 
+int ofdm_hbm_probe(int mode, const void *d_src, void *d_dst, size_t bytes, ofdm_stream_t stream) {
+    if ((mode != 0 && mode != 1) || !d_src || !d_dst)
+        return fail(OFDM_E_ARG, "ofdm_hbm_probe: mode 0 (copy) or 1 (read) and non-null buffers");
+    if ((reinterpret_cast<size_t>(d_src) | reinterpret_cast<size_t>(d_dst) | bytes) % 16)
+        return fail(OFDM_E_ARG, "ofdm_hbm_probe: 16-B aligned buffers and a multiple of 16 bytes");
+    return hip_check(ofdm::launch_hbm_probe(mode, d_src, d_dst, (long long)(bytes / 16), hs(stream)),
+                     "ofdm_hbm_probe");
+}
+
 int ofdm_pn_correlate(const ofdm_cf32 *d_buf, int R, long long N, const ofdm_cf32 *d_pn, int L,
                       float thres, long long *d_pos, float *d_mag, ofdm_stream_t stream) {
     if (!d_pos) return fail(OFDM_E_ARG, "ofdm_pn_correlate: null d_pos");

@@ -1,0 +1,67 @@
+// diag.hpp -- per-workgroup clock stamps of the diagnostic build.
+//
+// The product library (make) compiles every macro below to nothing.  The
+// diagnostic build (make diag -> lib/libofdm_lsmrc_diag.so, OFDM_DIAG_STAMPS=1)
+// compiles the SAME kernels with three stamps per workgroup: thread 0 reads
+// s_memrealtime (100 MHz wall clock) and s_memtime (shader clock) at the
+// workgroup's start, at one mark (the receivers: the estimate hand-off done)
+// and at its end (after a workgroup barrier), and stores them with vector
+// stores into a buffer of their own (g_diag_<tag>) that no kernel reads and
+// no output is computed from (MI355X_MICROARCH.md "DVFS give-back" (6)).
+// bench.py reads them after the timed loop: the effective clock of the timed
+// kernel = delta s_memtime / delta s_memrealtime x 100 MHz, median over
+// workgroups, and the workgroup timeline (start, hand-off, end, XCC, CU).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#if defined(OFDM_DIAG_STAMPS) && OFDM_DIAG_STAMPS
+namespace ofdm {
+namespace diag {
+constexpr long long MAX_WG = 1 << 17;  // workgroups stamped per launch (later ones are not)
+constexpr int WORDS = 8;               // u64 per workgroup record
+// record: rt_start, rt_mark, rt_end, mt_start, mt_end, hw_id, xcc_id, blockIdx
+__device__ __forceinline__ unsigned long long rt() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ unsigned long long mt() { return __builtin_amdgcn_s_memtime(); }
+constexpr int HWREG_HW_ID = (31 << 11) | 4;   // s_getreg_b32 HW_REG_HW_ID, 32 bits
+constexpr int HWREG_XCC_ID = (31 << 11) | 20; // s_getreg_b32 HW_REG_XCC_ID, 32 bits
+}  // namespace diag
+}  // namespace ofdm
+
+// one per translation unit: the stamp buffer and its host reader/clearer
+#define OFDM_DIAG_TU(tag)                                                                                   \
+    namespace ofdm { namespace diag {                                                                       \
+    __device__ unsigned long long g_diag_##tag[MAX_WG * WORDS];                                             \
+    } }                                                                                                     \
+    extern "C" int ofdm_diag_read_##tag(void *host, long long nwg) {                                        \
+        if (nwg > ofdm::diag::MAX_WG) nwg = ofdm::diag::MAX_WG;                                             \
+        return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(ofdm::diag::g_diag_##tag),                         \
+                                        (size_t)nwg * ofdm::diag::WORDS * 8, 0, hipMemcpyDeviceToHost);     \
+    }                                                                                                       \
+    extern "C" int ofdm_diag_clear_##tag() {                                                                \
+        void *p = nullptr;                                                                                  \
+        if (hipGetSymbolAddress(&p, HIP_SYMBOL(ofdm::diag::g_diag_##tag)) != hipSuccess) return -1;         \
+        return (int)hipMemset(p, 0, sizeof(ofdm::diag::g_diag_##tag));                                      \
+    }
+#define OFDM_DIAG_BEGIN()                                                                                   \
+    const unsigned long long dg_rt0 = ofdm::diag::rt(), dg_mt0 = ofdm::diag::mt();                         \
+    unsigned long long dg_rt1 = 0;
+#define OFDM_DIAG_MARK() dg_rt1 = ofdm::diag::rt();
+// every thread of the workgroup reaches this point (it holds a barrier)
+#define OFDM_DIAG_END(tag)                                                                                  \
+    do {                                                                                                    \
+        __syncthreads();                                                                                    \
+        if (threadIdx.x == 0 && (long long)blockIdx.x < ofdm::diag::MAX_WG) {                               \
+            const unsigned long long rt2 = ofdm::diag::rt(), mt2 = ofdm::diag::mt();                        \
+            unsigned long long *d = ofdm::diag::g_diag_##tag + (long long)blockIdx.x * ofdm::diag::WORDS;  \
+            d[0] = dg_rt0; d[1] = dg_rt1 ? dg_rt1 : dg_rt0; d[2] = rt2; d[3] = dg_mt0; d[4] = mt2;          \
+            d[5] = (unsigned)__builtin_amdgcn_s_getreg(ofdm::diag::HWREG_HW_ID);                            \
+            d[6] = (unsigned)__builtin_amdgcn_s_getreg(ofdm::diag::HWREG_XCC_ID);                           \
+            d[7] = blockIdx.x;                                                                              \
+        }                                                                                                   \
+    } while (0)
+#else
+#define OFDM_DIAG_TU(tag)
+#define OFDM_DIAG_BEGIN()
+#define OFDM_DIAG_MARK()
+#define OFDM_DIAG_END(tag) do { } while (0)
+#endif

@@ -279,4 +279,59 @@ hipError_t launch_count_errors(const float2 *out, long long nframes, int S, int 
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// HBM probes of the box (bench.py's roofline.box_*): a float4 copy and a
+// float4 read (summed, one float per thread written so the loads are kept)
+// over `n4` float4s, grid-stride, 4 independent 16-B loads per lane per step.
+// Plain loads and stores: the guide's "float4 copy" ceiling
+// (MI355X_MICROARCH.md: 6.29 TB/s measured against the 8 TB/s spec).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_hbm_copy(const float4 *__restrict__ src, float4 *__restrict__ dst,
+                                                  long long n4) {
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n4; i += 4 * stride) {
+        const float4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+        dst[i] = a;
+        dst[i + stride] = b;
+        dst[i + 2 * stride] = c;
+        dst[i + 3 * stride] = d;
+    }
+    for (; i < n4; i += stride) dst[i] = src[i];
+}
+
+__global__ void __launch_bounds__(256) k_hbm_read(const float4 *__restrict__ src, float *__restrict__ sink,
+                                                  long long n4) {
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    float4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (; i + 3 * stride < n4; i += 4 * stride) {
+        const float4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+        acc.x += (a.x + b.x) + (c.x + d.x);
+        acc.y += (a.y + b.y) + (c.y + d.y);
+        acc.z += (a.z + b.z) + (c.z + d.z);
+        acc.w += (a.w + b.w) + (c.w + d.w);
+    }
+    for (; i < n4; i += stride) {
+        const float4 a = src[i];
+        acc.x += a.x;
+        acc.y += a.y;
+        acc.z += a.z;
+        acc.w += a.w;
+    }
+    sink[(long long)blockIdx.x * blockDim.x + threadIdx.x] = (acc.x + acc.y) + (acc.z + acc.w);
+}
+
+hipError_t launch_hbm_probe(int mode, const void *src, void *dst, long long n4, hipStream_t s) {
+    if (n4 <= 0) return hipSuccess;
+    const int blocks = 256 * 8;  // 8 workgroups of 256 threads per CU
+    if (mode == 0)
+        hipLaunchKernelGGL(k_hbm_copy, dim3(blocks), dim3(256), 0, s, static_cast<const float4 *>(src),
+                           static_cast<float4 *>(dst), n4);
+    else
+        hipLaunchKernelGGL(k_hbm_read, dim3(blocks), dim3(256), 0, s, static_cast<const float4 *>(src),
+                           static_cast<float *>(dst), n4);
+    return hipGetLastError();
+}
+
 }  // namespace ofdm

@@ -27,6 +27,9 @@
 // (q, a) finally owns bins b = q + 256 c(a) + 16 k', c(a) = (a >> 1) + 2 (a & 1).
 #include "launch.hpp"
 #include "wave_fft1024.hpp"
+#include "diag.hpp"
+
+OFDM_DIAG_TU(td1024)
 
 
 namespace ofdm {
@@ -399,6 +402,7 @@ k_demod_td1024(const float2 *__restrict__ iq, int S, int R, int prefix, const fl
     float2 *T = lds + TW1S + TW2S + w * TS;
     float2 *T0 = lds + TW1S + TW2S;
     float4 *hfree = reinterpret_cast<float4 *>(T0 + HW * TS);
+    OFDM_DIAG_BEGIN()
 
     // Frames this workgroup estimates itself, [e0, e1]: an estimator
     // workgroup its own frame; an MRC workgroup none, or -- when a flag it
@@ -434,10 +438,13 @@ k_demod_td1024(const float2 *__restrict__ iq, int S, int R, int prefix, const fl
     }
     for (long long ff = e0; ff <= e1; ++ff) hlds_ls_frame(iq, S, R, prefix, X, Hc, P, ff, w, t, T, T0, tw1, tw2);
     if (estimator) {
+        OFDM_DIAG_MARK()
         publish_flag(flags + e0, epoch);
+        OFDM_DIAG_END(td1024);
         return;
     }
     if (e0 <= e1) acquire_all();
+    OFDM_DIAG_MARK()
 
     const long long lb = mrc_block();
     const int nsym = S - 1;
@@ -456,8 +463,8 @@ k_demod_td1024(const float2 *__restrict__ iq, int S, int R, int prefix, const fl
     else
         hlds_rows<false, false>(sym, Cp, R, reinterpret_cast<const float4 *>(Hc + f * (long long)R * C), t, T,
                                 tw1, tw2, T0, hfree, acc);
-    if (!store) return;
-    hlds_epilogue(acc, P, f, q, t, T, out, 0);
+    if (store) hlds_epilogue(acc, P, f, q, t, T, out, 0);
+    OFDM_DIAG_END(td1024);
 }
 
 }  // namespace td1024

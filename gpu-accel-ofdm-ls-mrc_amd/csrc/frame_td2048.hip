@@ -15,6 +15,9 @@
 // dwordx4 wave loads per row.  P stays bin-indexed [F][C].
 #include "launch.hpp"
 #include "wave_fft1024.hpp"
+#include "diag.hpp"
+
+OFDM_DIAG_TU(td2048)
 
 namespace ofdm {
 namespace td2048 {
@@ -260,11 +263,12 @@ k_mrc_td2048(const float2 *__restrict__ iq, int S, int R, int prefix, const floa
     const long long pb = blockIdx.x;
     const long long lb = (pb & 7) * per_xcd + (pb >> 3);
     if (lb >= nblocks) return;
+    OFDM_DIAG_BEGIN()
     fill_tables(lds);
     __syncthreads();
     const long long q = lb * MRC_WAVES + w;
-    if (q >= nq) return;  // no block-level sync follows
-    mrc2048_symbol(iq, S, R, prefix, Hc, P, out, q, t, T, lds, mode);
+    if (q < nq) mrc2048_symbol(iq, S, R, prefix, Hc, P, out, q, t, T, lds, mode);  // no block-level sync inside
+    OFDM_DIAG_END(td2048);
 
 }
 

@@ -28,6 +28,9 @@
 // z3 = (b + i d) W^(3 n0).  Same bin ownership as above.
 #include "launch.hpp"
 #include "wave_fft1024.hpp"
+#include "diag.hpp"
+
+OFDM_DIAG_TU(td4096)
 
 namespace ofdm {
 namespace td4096 {
@@ -428,6 +431,7 @@ k_mrc_td4096h(const float2 *__restrict__ iq, int S, int R, int prefix, const flo
     const long long pb = blockIdx.x;
     const long long lb = (pb & 7) * per_xcd + (pb >> 3);  // XCD-grouped: a frame's blocks share an L2
     if (lb >= nblocks) return;  // whole workgroup
+    OFDM_DIAG_BEGIN()
     const int nsym = S - 1;
     const long long bpf = (nsym + H_PAIRS - 1) / H_PAIRS;
     const long long f = lb / bpf;
@@ -435,6 +439,7 @@ k_mrc_td4096h(const float2 *__restrict__ iq, int S, int R, int prefix, const flo
     const bool store = j < nsym;
     const int s = 1 + (store ? j : nsym - 1);
     mrc4096_block(iq, S, R, prefix, Hc, P, out, f, j, store, s, lds, mode);
+    OFDM_DIAG_END(td4096);
 }
 
 

@@ -75,6 +75,7 @@ _SIGS = {
     "ofdm_zf_transpose": (_I, [_P, _I, _I, _I, _P, _P]),
     "ofdm_zf_apply": (_I, [_P, _P, _I, _I, _I, _LL, _P, _P]),
     "ofdm_zf_detect": (_I, [_P, _P, _I, _I, _I, _LL, _P, _P]),
+    "ofdm_hbm_probe": (_I, [_I, _P, _P, _c.c_size_t, _P]),
 }
 
 _lib = None
@@ -103,6 +104,47 @@ def lib():
             fn.argtypes = args
         _lib = L
     return _lib
+
+
+def load_library(path):
+    """Another build of this library (the diagnostic build, lib/
+    libofdm_lsmrc_diag.so, or an A/B variant) loaded beside the product one,
+    with the same signatures; call it through `using(L)`.  Its device state
+    (workspace registry, flag epochs, twiddle tables) is its own."""
+    import torch  # noqa: F401  (same HIP runtime as torch, see lib())
+    L = _c.CDLL(path)
+    for name, (res, args) in _SIGS.items():
+        if hasattr(L, name):
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+    return L
+
+
+class using:
+    """with using(L): ... -- the binding's calls go to library L."""
+
+    def __init__(self, L):
+        self.L = L
+
+    def __enter__(self):
+        global _lib
+        lib()
+        self.prev, _lib = _lib, self.L
+        return self.L
+
+    def __exit__(self, *exc):
+        global _lib
+        _lib = self.prev
+        return False
+
+
+def hbm_probe(mode, src, dst, stream=None):
+    """Box probe: mode 0 copies src -> dst (float4), mode 1 reads src (dst:
+    >= 2 MiB of partial sums).  Byte tensors on the device, 16-B multiples."""
+    nbytes = src.numel() * src.element_size()
+    _check(lib().ofdm_hbm_probe(mode, _dptr(src, "src"), _dptr(dst, "dst"), nbytes, _stream(stream)),
+           "ofdm_hbm_probe")
 
 
 def _check(rc, fn):

@@ -384,6 +384,12 @@ int ofdm_count_symbol_errors(const ofdm_cf32 *d_out, long long nframes, int S, i
                              unsigned long long seed, long long frame0,
                              unsigned long long *d_errors, ofdm_stream_t stream);
 
+/* Box probe for bench.py (no reference counterpart): mode 0 copies `bytes`
+ * from d_src to d_dst as float4s, mode 1 reads them (d_dst receives
+ * 2048 x 256 float partial sums, 2 MiB).  Plain 16-B loads/stores over the
+ * whole chip; `bytes` and both pointers 16-B aligned. */
+int ofdm_hbm_probe(int mode, const void *d_src, void *d_dst, size_t bytes, ofdm_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,43 @@
+#!/usr/bin/env bash
+# One GPU session of named steps, each under its own time limit, stopping at
+# the first failure (no retries).  Outputs under gpurun_out/<tag>/.
+# usage: bash scripts/gpu_session.sh <tag> step [step ...]
+# steps:
+#   suite      pytest -m gpu (the driver's form)          smoke    __graft_entry__.smoke()
+#   default    bench.py (driver form: 20 steps, 3 warm-up, CPU baseline) + stamps
+#   cfg1       configs[1]: --R 16 --frames 100 --steps 20 --warmup 5 + stamps
+#   cfg2       configs[2]: --R 64 --C 2048 --frames 1000 --steps 10
+#   c4096      configs[4] per-GPU slice: --R 32 --C 4096 --frames 400 --steps 20 + stamps
+#   split      bench.py --mode split (RCCL, world 1) with stages_ms
+#   freq       bench.py --mode freq (mode A line)
+#   prof_default / prof_cfg1 / prof_c4096   scripts/gpu_prof_r4.sh of that command
+#   abx:<args> python scripts/abx.py <args, ':' for spaces>
+set -o pipefail
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$ROOT"
+TAG=$1; shift
+OUT=gpurun_out/$TAG; mkdir -p $OUT
+bench() { name=$1; lim=$2; shift 2
+  timeout -k 10 $lim python -u bench.py "$@" > $OUT/$name.json 2> $OUT/$name.err
+  rc=$?; echo "$name rc=$rc"; tail -c 3000 $OUT/$name.json; return $rc; }
+for st in "$@"; do
+  case $st in
+    suite) timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1
+           rc=$?; echo "suite rc=$rc"; tail -3 $OUT/pytest.log ;;
+    smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
+           rc=$?; echo "smoke rc=$rc"; tail -2 $OUT/smoke.log ;;
+    default) bench default 600 --stamps-out $OUT/stamps_default.npy; rc=$? ;;
+    cfg1) bench cfg1 300 --R 16 --frames 100 --steps 20 --warmup 5 --no-cpu --stamps-out $OUT/stamps_cfg1.npy; rc=$? ;;
+    cfg2) bench cfg2 300 --R 64 --C 2048 --frames 1000 --steps 10 --no-cpu --stamps-out $OUT/stamps_cfg2.npy; rc=$? ;;
+    c4096) bench c4096 300 --R 32 --C 4096 --frames 400 --steps 20 --no-cpu --stamps-out $OUT/stamps_c4096.npy; rc=$? ;;
+    split) bench split 300 --mode split --no-cpu; rc=$? ;;
+    freq) bench freq 300 --mode freq --no-cpu; rc=$? ;;
+    prof_default) timeout -k 10 1000 bash scripts/gpu_prof_r4.sh ${TAG}_default > $OUT/prof_default.log 2>&1; rc=$?; echo "prof_default rc=$rc"; tail -3 $OUT/prof_default.log ;;
+    prof_cfg1) timeout -k 10 600 bash scripts/gpu_prof_r4.sh ${TAG}_cfg1 --gpus 1 --steps 20 --warmup 5 --R 16 --frames 100 --no-box > $OUT/prof_cfg1.log 2>&1; rc=$?; echo "prof_cfg1 rc=$rc"; tail -3 $OUT/prof_cfg1.log ;;
+    prof_c4096) timeout -k 10 800 bash scripts/gpu_prof_r4.sh ${TAG}_c4096 --gpus 1 --steps 20 --warmup 5 --R 32 --C 4096 --frames 400 --no-box > $OUT/prof_c4096.log 2>&1; rc=$?; echo "prof_c4096 rc=$rc"; tail -3 $OUT/prof_c4096.log ;;
+    abx:*) a=${st#abx:}; timeout -k 10 600 python -u scripts/abx.py ${a//:/ } > $OUT/abx_$(echo $a | tr -c 'a-zA-Z0-9' _).jsonl 2> $OUT/abx.err; rc=$?; echo "abx $a rc=$rc"; tail -8 $OUT/abx_$(echo $a | tr -c 'a-zA-Z0-9' _).jsonl ;;
+    *) echo "unknown step $st"; rc=2 ;;
+  esac
+  [ $rc -eq 0 ] || exit $rc
+done
+echo "session $TAG done"

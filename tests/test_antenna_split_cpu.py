@@ -7,6 +7,7 @@ are replaced by a numpy stand-in with the HIP library's signatures (NumpyOps
 below, test-only).  The gathered result must match the oracle run on ALL
 antennas within helpers.RTOL, and the ranks' finalised
 slices must tile the output exactly once."""
+import json
 import os
 import socket
 import tempfile
@@ -88,6 +89,11 @@ def _worker(rank, world, port, tmp, splits, prefix, gather, chunk=0):
             for _ in range(2):  # buffers reused across steps
                 out.zero_()
                 pipe.run(shard, X, out)
+            # bench.py --mode split's stages_ms: one more step (rewrites the
+            # same slices) and the collectives alone
+            stages = pipe.profile_step(shard, X, out)
+            with open(os.path.join(tmp, f"stages{rank}.json"), "w") as fp:
+                json.dump(stages, fp)
             if gather:
                 dist.all_reduce(torch.view_as_real(out))
             e0, count = 0, int((out != 0).sum())
@@ -126,6 +132,14 @@ def test_antenna_split_gloo(oracle, world, R, F, S, C, prefix, gather, chunk):
         mp.spawn(_worker, args=(world, _free_port(), tmp, splits, prefix, gather, chunk),
                  nprocs=world)
         res = [np.load(os.path.join(tmp, f"out{r}.npz")) for r in range(world)]
+        if chunk:
+            for r in range(world):
+                with open(os.path.join(tmp, f"stages{r}.json")) as fp:
+                    st = json.load(fp)
+                for k in ("step_wall_ms", "all_reduce_alone_per_chunk", "reduce_scatter_alone_per_chunk",
+                          "collectives_alone_step", "chunks"):
+                    assert k in st and st[k] >= 0, (k, st)
+                assert st["chunks"] == -(-F // chunk)
     n = F * (S - 1) * K
     if not (chunk and gather):
         assert sum(int(r["count"]) for r in res) == n

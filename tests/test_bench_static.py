@@ -36,3 +36,58 @@ def test_functions_reference_only_defined_names(rel):
     bad = []
     _walk(top, module_names, bad)
     assert not bad, f"undefined names in {rel}: {bad}"
+
+
+def _src(rel):
+    with open(os.path.join(ROOT, rel)) as fp:
+        return fp.read()
+
+
+def test_bench_line_carries_box_and_clock_fields():
+    """the line shows the box it ran on (same-process HBM
+    copy / read ceilings and the effective clock of the timed kernel)."""
+    src = _src("bench.py")
+    for key in ('"box_copy_GBps"', '"frac_of_box_copy"', '"box_read_GBps"', '"frac_of_box_read"',
+                '"clock"', '"effective_GHz_median"', '"per_rank"', '"stages_ms": stages'):
+        assert key in src, key
+
+
+def test_cpu_share_read_from_the_box():
+    """no literal CPU share in bench.py."""
+    import re
+    src = _src("bench.py")
+    assert not re.search(r"min\(\s*16\s*,", src)
+    assert '"host_cpu_share": 16' not in src
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    share = bench.host_cpu_share()
+    assert share["threads"] >= 1 and share["threads"] <= share["affinity_cpus"]
+    assert share["source"]
+
+
+def test_check_failure_invalidates_the_line():
+    """a run whose timed output differs from the warm-up's or has
+    QPSK errors prints value null with status CHECK_FAILED and exits 1."""
+    src = _src("bench.py")
+    i = src.index("if failed:  # a broken run")
+    block = src[i:i + 400]
+    assert '"CHECK_FAILED"' in block and 'result["value"] = None' in block and "sys.exit(1)" in block
+
+
+def test_stamps_summary_clock():
+    """The diagnostic-build stamp records -> effective clock: 2.0 GHz when
+    memtime advances 20 ticks per memrealtime tick (100 MHz)."""
+    import importlib.util
+    import numpy as np
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    rec = np.zeros((4, 8), dtype=np.uint64)
+    for i in range(3):
+        rec[i] = [1000 + i, 1100 + i, 2000 + i, 50000, 50000 + 20 * 1000, 0, i, i]
+    st = bench.stamps_summary(rec)  # the empty 4th record is ignored
+    assert st["workgroups"] == 3
+    assert abs(st["effective_GHz_median"] - 2.0) < 1e-9
+    assert abs(st["stamped_span_ms"] - 1002 * 1e-5) < 1e-12
