@@ -659,6 +659,13 @@ int ofdm_count_symbol_errors(const ofdm_cf32 *d_out, long long nframes, int S, i
                      "ofdm_count_symbol_errors");
 }
 
+int ofdm_buffer_hash(const void *d_buf, size_t bytes, unsigned long long *d_hash, ofdm_stream_t stream) {
+    if (!d_hash || (bytes && !d_buf) || bytes % 4 || !aligned(d_buf, 4))
+        return fail(OFDM_E_ARG, "ofdm_buffer_hash: a 4-B aligned buffer of whole 32-bit words and a hash slot");
+    return hip_check(ofdm::launch_hash_words(d_buf, (long long)(bytes / 4), d_hash, hs(stream)),
+                     "ofdm_buffer_hash");
+}
+
 int ofdm_hbm_probe(int mode, const void *d_src, void *d_dst, size_t bytes, ofdm_stream_t stream) {
     if ((mode != 0 && mode != 1) || !d_src || !d_dst)
         return fail(OFDM_E_ARG, "ofdm_hbm_probe: mode 0 (copy) or 1 (read) and non-null buffers");

@@ -387,6 +387,7 @@ k_mrc_td6144(const float2 *__restrict__ iq, long long nframes, int S, int R, int
              const float *__restrict__ P, float2 *__restrict__ out, int mode) {
     __shared__ float2 tab[4096];   // W6144^e, e < 4096 (e >= 4096: -W6144^{e - 3072}); every twiddle one table entry
     __shared__ float2 xch[4][XS];  // per-wave exchange / transpose image
+    static_assert((4096 + 4 * XS) * sizeof(float2) <= 80 * 1024, "two workgroups per CU (160 KiB of LDS)");
     for (int e = threadIdx.x; e < 4096; e += NT) {
         double sn, cs;
         sincospi(-2.0 * (double)e / (double)C, &sn, &cs);
@@ -703,6 +704,14 @@ hipError_t launch_mrc_lane(Kern kern, int nt, int per_cu, int per_wg, const floa
                            int R, int prefix, const float2 *Hl, const float *P, float2 *out, int mode, hipStream_t s) {
     const long long nq = nframes * (S - 1);
     if (nq <= 0) return hipSuccess;
+    // the resident count from the occupancy query (LDS, registers), capped by
+    // the hint: a kernel that outgrows its LDS budget shrinks the grid
+    // instead of queueing workgroups behind a persistent one
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void *>(kern), nt, 0) ==
+            hipSuccess &&
+        occ > 0 && occ < per_cu)
+        per_cu = occ;
     const long long res = (long long)per_cu * cu_count(), need = (nq + per_wg - 1) / per_wg;
     hipLaunchKernelGGL(kern, dim3((unsigned)(need < res ? need : res)), dim3(nt), 0, s, iq, nframes, S, R, prefix, Hl,
                        P, out, mode);
@@ -756,7 +765,9 @@ hipError_t launch_mrc_td3072(const float2 *iq, long long nframes, int S, int R, 
     return launch_mrc_lane(td3072::k_mrc_td3072, td3072::NT, 4, 1, iq, nframes, S, R, prefix, Hl, P, out, mode, s);
 }
 
-// 6144: one wave quad (64 KiB of LDS) per workgroup, 2 per CU.
+// 6144: one wave quad (80 KiB of static LDS: the 32 KiB twiddle table and
+// four 12 KiB exchange images) per workgroup, 2 per CU (static_assert in
+// k_mrc_td6144; the occupancy query in launch_mrc_lane has the last word).
 hipError_t launch_mrc_td6144(const float2 *iq, long long nframes, int S, int R, int prefix, const float2 *Hl,
                              const float *P, float2 *out, int mode, hipStream_t s) {
     return launch_mrc_lane(td6144::k_mrc_td6144, td6144::NT, 2, 1, iq, nframes, S, R, prefix, Hl, P, out, mode, s);

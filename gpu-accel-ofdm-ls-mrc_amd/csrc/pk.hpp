@@ -76,11 +76,13 @@ __device__ __forceinline__ v2f cmul_s_v(v2f a, v2f w) {
                  : "=&v"(r) : "v"(a), "s"(w));
     return r;
 }
-// acc += x * h
+// acc += x * h.  Two instructions in one statement: the second reads x and h
+// after the first has written acc, so acc is early-clobber ("+&v") and can
+// never share a register with x or h (e.g. mac(a, a, h)).
 __device__ __forceinline__ void mac(v2f &acc, v2f x, v2f h) {
     asm("v_pk_fma_f32 %0, %1, %2, %0 op_sel_hi:[0,1,1]\n\t"
         "v_pk_fma_f32 %0, %1, %2, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[0,1,0]"
-        : "+v"(acc) : "v"(x), "v"(h));
+        : "+&v"(acc) : "v"(x), "v"(h));
 }
 // v * (a * b): the twiddle a * b formed and applied in one statement
 // (twiddle generation chains: no pad between the product and its use)

@@ -167,4 +167,29 @@ hipError_t launch_dist_sqrd(const float2 *H, int R, int K, float *P, hipStream_t
     return hipGetLastError();
 }
 
+// Order-sensitive 64-bit hash of a buffer's 32-bit words (sum over i of
+// mix(w_i) * (2 i + 1) mod 2^64, one 64-bit atomic add per wave into *h,
+// which the launcher zeroes first): gpuLS::demodOneSymbol's check that the
+// caller's Hconj / Hsqrd still hold what firstVector exported.
+__global__ void __launch_bounds__(256) k_hash_words(const unsigned *__restrict__ w, long long n,
+                                                    unsigned long long *h) {
+    unsigned long long acc = 0;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x)
+        acc += ((unsigned long long)w[i] * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull) *
+               (unsigned long long)(2 * i + 1);
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if ((threadIdx.x & 63) == 0) atomicAdd(h, acc);
+}
+
+hipError_t launch_hash_words(const void *d, long long nwords, unsigned long long *h, hipStream_t s) {
+    if (hipError_t e = hipMemsetAsync(h, 0, sizeof(*h), s); e != hipSuccess) return e;
+    if (nwords <= 0) return hipSuccess;
+    long long blocks = (nwords + 255) / 256;
+    if (blocks > 1024) blocks = 1024;
+    hipLaunchKernelGGL(k_hash_words, dim3((unsigned)blocks), dim3(256), 0, s, static_cast<const unsigned *>(d),
+                       nwords, h);
+    return hipGetLastError();
+}
+
 }  // namespace ofdm

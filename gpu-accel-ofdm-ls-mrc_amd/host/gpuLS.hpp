@@ -168,6 +168,7 @@ class gpuLS {
             est_rows_ = rows;
             est_cols_ = cols;
             est_wsb_ = wsb;
+            est_hash_ = estimate_hash(dH, Hsqrd, rows, cols);
             return;
         }
         batchedFFT(Y, rows, cols, nullptr);
@@ -185,12 +186,15 @@ class gpuLS {
     // MRC + normalise + rotate launch (ofdm_symbols_demod) on the staging
     // buffer against the kept estimate, one synchronising copy of the K
     // outputs.  Otherwise FFT rows in Y, then MRC from Hconj / Hsqrd.
-    // Contract of the fused path: it demodulates against the workspace copy
-    // of the estimate firstVector exported, NOT what Hconj / Hsqrd hold now.
-    // A caller that edits them in place after firstVector (smoothing,
-    // interpolation, another estimate copied in) calls estimateChanged()
-    // first; the next demodOneSymbol then reads Hconj / Hsqrd as the
-    // reference does (gpuLS.cu:410-473).
+    // The fused path demodulates against the workspace copy of the estimate
+    // firstVector exported, so it is taken only while Hconj / Hsqrd still
+    // hold exactly those bytes: their device hash (ofdm_buffer_hash, one
+    // small kernel + an 16-B read-back per symbol) must equal the one taken
+    // at export.  A caller that edits them in place after firstVector
+    // (smoothing, interpolation, another estimate copied in) -- as reference
+    // callers may, without telling anyone -- therefore gets the reference's
+    // behaviour, Hconj / Hsqrd read afresh (gpuLS.cu:410-473).
+    // estimateChanged() drops the kept estimate outright.
     void estimateChanged() {
         est_H_ = nullptr;
         est_P_ = nullptr;
@@ -199,7 +203,7 @@ class gpuLS {
                         float *Hsqrd, int rows1, int cols1, int it) {
         const int K = cols1 - 1;
         const bool use_est = fused(cols1) && Hconj == est_H_ && Hsqrd == est_P_ && rows1 == est_rows_ &&
-                             cols1 == est_cols_;
+                             cols1 == est_cols_ && estimate_hash(Hconj, Hsqrd, rows1, cols1) == est_hash_;
         int pfx = 0;
         const hipFloatComplex *src = read_symbol(dY, Y, rows1, cols1, it, it == numberOfSymbolsToTest - 1,
                                                  use_est ? &pfx : nullptr);
@@ -369,7 +373,22 @@ class gpuLS {
         return Y;
     }
 
-    ofdm::DevBuf scratch_, scratchP_, ws_, ws1_;
+    // hash of the caller's Hconj [rows][cols-1] and Hsqrd [cols-1] (device)
+    struct EstHash {
+        unsigned long long h, p;
+        bool operator==(const EstHash &o) const { return h == o.h && p == o.p; }
+    };
+    EstHash estimate_hash(const hipFloatComplex *H, const float *P, int rows, int cols) {
+        auto *d = hash_.get<unsigned long long>(2 * sizeof(unsigned long long));
+        const size_t K = (size_t)cols - 1;
+        ofdm::check(ofdm_buffer_hash(H, (size_t)rows * K * sizeof(hipFloatComplex), d, nullptr), "ofdm_buffer_hash");
+        ofdm::check(ofdm_buffer_hash(P, K * sizeof(float), d + 1, nullptr), "ofdm_buffer_hash");
+        EstHash e;
+        ofdm::copy_any(&e, d, sizeof(e));
+        return e;
+    }
+    ofdm::DevBuf scratch_, scratchP_, ws_, ws1_, hash_;
+    EstHash est_hash_{0, 0};
     // the estimate firstVector keeps in ws1_ and the buffers it exported to
     const hipFloatComplex *est_H_ = nullptr;
     const float *est_P_ = nullptr;

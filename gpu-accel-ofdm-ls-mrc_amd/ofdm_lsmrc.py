@@ -76,6 +76,7 @@ _SIGS = {
     "ofdm_zf_apply": (_I, [_P, _P, _I, _I, _I, _LL, _P, _P]),
     "ofdm_zf_detect": (_I, [_P, _P, _I, _I, _I, _LL, _P, _P]),
     "ofdm_hbm_probe": (_I, [_I, _P, _P, _c.c_size_t, _P]),
+    "ofdm_buffer_hash": (_I, [_P, _c.c_size_t, _P, _P]),
 }
 
 _lib = None

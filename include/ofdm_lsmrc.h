@@ -234,10 +234,14 @@ int ofdm_frame_demod_freq(const ofdm_cf32 *d_Y, long long nframes, int S, int R,
 
 /* Its two stages (as ofdm_frame_estimate / ofdm_frame_combine): the LS
  * estimate of every frame's pilot symbol into d_ws, then the MRC of the data
- * symbols against it.  ofdm_frame_combine_freq refuses a workspace filled by
- * the time-domain ofdm_frame_estimate for C in {1024, 2048, 4096} (whose
- * estimate is in the fused kernels' lane order), and ofdm_frame_combine one
- * filled here, with OFDM_E_ARG. */
+ * symbols against it.  At every C that has a fused time-domain receiver --
+ * 128, 256, 512, 1024, 1536, 2048, 3072, 4096, 6144 -- the time-domain
+ * ofdm_frame_estimate leaves its estimate in that receiver's lane order:
+ * ofdm_frame_combine_freq refuses such a workspace and ofdm_frame_combine
+ * refuses one filled here, with OFDM_E_ARG.  (Until round 4, C = 128 / 256 /
+ * 512 had no fused receiver and their time-domain estimates were in the bin
+ * layout, which ofdm_frame_combine_freq accepted.)  At every other C both
+ * estimators write the bin layout, and each combine accepts either one. */
 int ofdm_frame_estimate_freq(const ofdm_cf32 *d_Y, long long nframes, int S, int R, int C,
                              const ofdm_cf32 *d_X, void *d_ws, size_t ws_bytes, ofdm_stream_t stream);
 int ofdm_frame_combine_freq(const ofdm_cf32 *d_Y, long long nframes, int S, int R, int C, void *d_ws,
@@ -383,6 +387,13 @@ int ofdm_synth_frames(ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, i
 int ofdm_count_symbol_errors(const ofdm_cf32 *d_out, long long nframes, int S, int C,
                              unsigned long long seed, long long frame0,
                              unsigned long long *d_errors, ofdm_stream_t stream);
+
+/* Host-mirror helper (no reference counterpart): an order-sensitive 64-bit
+ * hash of `bytes` (a multiple of 4) of device memory into *d_hash (device).
+ * gpuLS::demodOneSymbol hashes the caller's Hconj / Hsqrd to tell whether
+ * they still hold the estimate firstVector exported (gpuLS.cu:410-473 reads
+ * them afresh for every symbol). */
+int ofdm_buffer_hash(const void *d_buf, size_t bytes, unsigned long long *d_hash, ofdm_stream_t stream);
 
 /* Box probe for bench.py (no reference counterpart): mode 0 copies `bytes`
  * from d_src to d_dst as float4s, mode 1 reads them (d_dst receives

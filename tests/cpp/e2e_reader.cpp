@@ -5,6 +5,8 @@
 //   symbol  gpuLS firstVector + demodOneSymbol x (S-1)  -> Output_gpu.dat
 //   frame   gpuLS demodOneFrame                          -> Output_gpu.dat
 //   symbolcuda  as symbol, with a device staging buffer (readNextSymbolCUDA)
+//   symboledit  as symbol, the caller doubling Hsqrd in place after firstVector
+//           (no estimateChanged(): the outputs must follow the edit, x 1/2)
 //   frames N [chunk depth]  gpuLS demodFrames: N frames through the pipelined
 //           ring reader and ofdm_pipeline (page-locked output) -> Output_gpu.dat,
 //           and the ingest rate on stdout
@@ -34,7 +36,7 @@ static int run_cpuls() {
     return 0;
 }
 
-static int run_gpuls(bool frame, bool dev_staging) {
+static int run_gpuls(bool frame, bool dev_staging, bool edit = false) {
     const int rows = numOfRows, cols = dimension, K = cols - 1;
     gpuLS g;
     hipFloatComplex *Y, *dH, *dX;
@@ -59,6 +61,12 @@ static int run_gpuls(bool frame, bool dev_staging) {
         hipFloatComplex *dY = hY.data();
         if (dev_staging) ofdm::hcheck(hipMalloc(&dY, hY.size() * sizeof(hipFloatComplex)), "hipMalloc");
         g.firstVector(dY, Y, dH, dX, Hsqrd, rows, cols, 0);
+        if (edit) {  // a caller's in-place edit of the estimate, without estimateChanged(): Hsqrd x 2
+            std::vector<float> p(K);
+            ofdm::copy_any(p.data(), Hsqrd, p.size() * sizeof(float));
+            for (float &v : p) v *= 2.f;
+            ofdm::copy_any(Hsqrd, p.data(), p.size() * sizeof(float));
+        }
         for (int i = 1; i < numberOfSymbolsToTest; i++) {
             g.demodOneSymbol(dY, Y, dH, Hsqrd, rows, cols, i);
             ofdm::copy_any(o.data(), dY, (size_t)K * sizeof(hipFloatComplex));
@@ -110,6 +118,7 @@ int main(int argc, char **argv) {
     if (m == "cpuls") return run_cpuls();
     if (m == "symbol") return run_gpuls(false, false);
     if (m == "symbolcuda") return run_gpuls(false, true);
+    if (m == "symboledit") return run_gpuls(false, false, true);
     if (m == "frame") return run_gpuls(true, false);
     if (m == "frames" && argc > 2)
         return run_frames(std::atoi(argv[2]), argc > 3 ? std::atoi(argv[3]) : 4,

@@ -163,3 +163,32 @@ def test_small_batches_any_c_vs_oracle(ofdm, oracle, dev, C, F, S, R, prefix):
     parity(out, oracle.frames_demod(host(iq), host(X), prefix), erel_tol=1e-4 if R == 1 else None)
     if R > 1:  # one antenna has no diversity: a deep fade under the noise flips a decision (so does the oracle)
         assert int(ofdm.count_symbol_errors(to_dev(out, dev), S, seed=C + F + R).item()) == 0
+
+
+@pytest.mark.parametrize("C,lane", [(512, True), (600, False), (1024, True)])
+def test_combine_freq_and_estimate_layouts(ofdm, dev, C, lane):
+    """at the sizes with a fused receiver (lane-order estimates)
+    the time- and frequency-domain stage pairs refuse each other's
+    workspaces; at other sizes (600) both estimates are in the bin layout
+    and each combine accepts the other's estimate with the same result."""
+    F, S, R = 2, 3, 4
+    X = to_dev(qpsk(C - 1), dev)
+    iq = ofdm.synth_frames(F, S, R, C, X, seed=3, noise_std=0.02)
+    Y = ofdm.fft_rows(iq.clone())
+    ref = host(ofdm.frame_demod(iq, X, 0))
+    ws = ofdm.workspace(F, S, R, C, dev)
+    out = ofdm.c64((F, S - 1, C - 1), dev)
+    ofdm.frame_estimate(iq, X, 0, ws)
+    if lane:
+        with pytest.raises(ofdm.OfdmError, match="lane order"):
+            ofdm.frame_combine_freq(Y, ws, out)
+    else:
+        ofdm.frame_combine_freq(Y, ws, out)
+        parity(host(out), ref)
+    ofdm.frame_estimate_freq(Y, X, ws)
+    if lane:
+        with pytest.raises(ofdm.OfdmError, match="frequency-domain estimate"):
+            ofdm.frame_combine(iq, 0, ws, out)
+    else:
+        ofdm.frame_combine(iq, 0, ws, out)
+        parity(host(out), ref)
