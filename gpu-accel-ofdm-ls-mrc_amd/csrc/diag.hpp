@@ -17,7 +17,12 @@
 #if defined(OFDM_DIAG_STAMPS) && OFDM_DIAG_STAMPS
 namespace ofdm {
 namespace diag {
-constexpr long long MAX_WG = 1 << 17;  // workgroups stamped per launch (later ones are not)
+constexpr long long MAX_WG = 1 << 20;  // records in the buffer (64 MiB); later workgroups are not stamped
+// kernels that know a per-launch counter (k_demod_td1024: the low bits of its
+// flag epoch) stamp into slot (counter % SLOTS) of SLOT_WG records, so the
+// last SLOTS launches of a back-to-back run can be read at once
+constexpr int SLOTS = 32;
+constexpr long long SLOT_WG = MAX_WG / SLOTS;
 constexpr int WORDS = 8;               // u64 per workgroup record
 // record: rt_start, rt_mark, rt_end, mt_start, mt_end, hw_id, xcc_id, blockIdx
 __device__ __forceinline__ unsigned long long rt() { return __builtin_amdgcn_s_memrealtime(); }
@@ -47,12 +52,15 @@ constexpr int HWREG_XCC_ID = (31 << 11) | 20; // s_getreg_b32 HW_REG_XCC_ID, 32 
     unsigned long long dg_rt1 = 0;
 #define OFDM_DIAG_MARK() dg_rt1 = ofdm::diag::rt();
 // every thread of the workgroup reaches this point (it holds a barrier)
-#define OFDM_DIAG_END(tag)                                                                                  \
+#define OFDM_DIAG_END(tag) OFDM_DIAG_END_AT(tag, 0, ofdm::diag::MAX_WG)
+#define OFDM_DIAG_END_SLOT(tag, counter)                                                                    \
+    OFDM_DIAG_END_AT(tag, (long long)((counter) % ofdm::diag::SLOTS) * ofdm::diag::SLOT_WG, ofdm::diag::SLOT_WG)
+#define OFDM_DIAG_END_AT(tag, base, cap)                                                                    \
     do {                                                                                                    \
         __syncthreads();                                                                                    \
-        if (threadIdx.x == 0 && (long long)blockIdx.x < ofdm::diag::MAX_WG) {                               \
+        if (threadIdx.x == 0 && (long long)blockIdx.x < (cap)) {                                            \
             const unsigned long long rt2 = ofdm::diag::rt(), mt2 = ofdm::diag::mt();                        \
-            unsigned long long *d = ofdm::diag::g_diag_##tag + (long long)blockIdx.x * ofdm::diag::WORDS;  \
+            unsigned long long *d = ofdm::diag::g_diag_##tag + ((base) + (long long)blockIdx.x) * ofdm::diag::WORDS; \
             d[0] = dg_rt0; d[1] = dg_rt1 ? dg_rt1 : dg_rt0; d[2] = rt2; d[3] = dg_mt0; d[4] = mt2;          \
             d[5] = (unsigned)__builtin_amdgcn_s_getreg(ofdm::diag::HWREG_HW_ID);                            \
             d[6] = (unsigned)__builtin_amdgcn_s_getreg(ofdm::diag::HWREG_XCC_ID);                           \
@@ -64,4 +72,5 @@ constexpr int HWREG_XCC_ID = (31 << 11) | 20; // s_getreg_b32 HW_REG_XCC_ID, 32 
 #define OFDM_DIAG_BEGIN()
 #define OFDM_DIAG_MARK()
 #define OFDM_DIAG_END(tag) do { } while (0)
+#define OFDM_DIAG_END_SLOT(tag, counter) do { } while (0)
 #endif

@@ -440,7 +440,7 @@ k_demod_td1024(const float2 *__restrict__ iq, int S, int R, int prefix, const fl
     if (estimator) {
         OFDM_DIAG_MARK()
         publish_flag(flags + e0, epoch);
-        OFDM_DIAG_END(td1024);
+        OFDM_DIAG_END_SLOT(td1024, epoch);
         return;
     }
     if (e0 <= e1) acquire_all();
@@ -464,7 +464,7 @@ k_demod_td1024(const float2 *__restrict__ iq, int S, int R, int prefix, const fl
         hlds_rows<false, false>(sym, Cp, R, reinterpret_cast<const float4 *>(Hc + f * (long long)R * C), t, T,
                                 tw1, tw2, T0, hfree, acc);
     if (store) hlds_epilogue(acc, P, f, q, t, T, out, 0);
-    OFDM_DIAG_END(td1024);
+    OFDM_DIAG_END_SLOT(td1024, epoch);
 }
 
 }  // namespace td1024
