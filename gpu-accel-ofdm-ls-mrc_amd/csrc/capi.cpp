@@ -62,11 +62,20 @@ hipError_t ls_fused(const float2 *iq, long long F, int S, int R, int C, int pref
     if (C == 2048) return ofdm::launch_ls_td2048(iq, F, S, R, prefix, X, Hc, P, partial, s);
     return ofdm::launch_ls_td4096(iq, F, S, R, prefix, X, Hc, P, partial, s);
 }
+hipError_t tickets_next(const void *ws, unsigned long long *tickets, hipStream_t s, int *par);
+void tickets_forget(const void *ws);
+// ws / tickets: the frame workspace and its ticket area (work-ticketed
+// kernels: C = 2048 and 4096)
 hipError_t mrc_fused(const float2 *iq, long long F, int S, int R, int C, int prefix, const float2 *Hc,
-                     const float *P, float2 *out, int mode, hipStream_t s) {
+                     const float *P, float2 *out, int mode, hipStream_t s, const void *ws,
+                     unsigned long long *tickets) {
     if (C == 1024) return ofdm::launch_mrc_td1024(iq, F, S, R, prefix, Hc, P, out, mode, s);
-    if (C == 2048) return ofdm::launch_mrc_td2048(iq, F, S, R, prefix, Hc, P, out, mode, s);
-    return ofdm::launch_mrc_td4096(iq, F, S, R, prefix, Hc, P, out, mode, s);
+    int par = 0;
+    if (hipError_t e = tickets_next(ws, tickets, s, &par); e != hipSuccess) return e;
+    hipError_t e = C == 2048 ? ofdm::launch_mrc_td2048(iq, F, S, R, prefix, Hc, P, out, mode, tickets, par, s)
+                             : ofdm::launch_mrc_td4096(iq, F, S, R, prefix, Hc, P, out, mode, tickets, par, s);
+    if (e != hipSuccess) tickets_forget(ws);  // no kernel zeroed the next set
+    return e;
 }
 
 // ofdm_frame_demod at C = 1024 runs LS and MRC as ONE launch (k_demod_td1024)
@@ -108,13 +117,42 @@ struct Workspace {
     float2 *Hc;                 // [F][R][C] bin layout
     float *P;                   // [F][C]   bin layout
     unsigned long long *flags;  // [F] per-frame estimate flags of the one-launch demod
+    unsigned long long *tickets;  // 8 work-ticket counters, 128 B apart (wave_fft1024.hpp take_block)
     float2 *staging;            // [chunk][S][R][C] (non-fused C only)
     long long chunk;
 };
 
+constexpr size_t TICKET_BYTES = 2 * 8 * 128;  // two sets of 8 counters, one 128-B line each
+
+// Work-ticket counter sets of a workspace (wave_fft1024.hpp, take_block): a
+// launch counts in set `par` and zeroes the other set for the next launch on
+// the same workspace; the host keeps `par` per workspace, flips it per
+// launch, and zeroes both sets the first time it meets the workspace (and
+// again after ofdm_workspace_release).  Launches on one workspace are
+// ordered (one stream, as the estimate they share already requires).  A
+// workspace used by two library instances in turn must be released by one
+// before the other uses it, as for its estimate.
+std::mutex g_tk_mu;
+std::map<const void *, int> g_tk_par;
+hipError_t tickets_next(const void *ws, unsigned long long *tickets, hipStream_t s, int *par) {
+    std::lock_guard<std::mutex> lock(g_tk_mu);
+    auto it = g_tk_par.find(ws);
+    if (it == g_tk_par.end()) {
+        if (hipError_t e = hipMemsetAsync(tickets, 0, TICKET_BYTES, s); e != hipSuccess) return e;
+        it = g_tk_par.emplace(ws, 1).first;
+    }
+    it->second ^= 1;
+    *par = it->second;
+    return hipSuccess;
+}
+void tickets_forget(const void *ws) {
+    std::lock_guard<std::mutex> lock(g_tk_mu);
+    g_tk_par.erase(ws);
+}
+
 size_t ws_bytes(long long F, int S, int R, int C, bool need_staging) {
     size_t b = up256((size_t)F * R * C * sizeof(float2)) + up256((size_t)F * C * sizeof(float)) +
-               up256((size_t)F * sizeof(unsigned long long));
+               up256((size_t)F * sizeof(unsigned long long)) + TICKET_BYTES;
     if (need_staging) b += up256((size_t)staging_frames(F, S, R, C) * S * R * C * sizeof(float2));
     return b;
 }
@@ -132,6 +170,8 @@ int carve(void *d_ws, size_t bytes, long long F, int S, int R, int C, bool need_
     p += up256((size_t)F * C * sizeof(float));
     w.flags = reinterpret_cast<unsigned long long *>(p);
     p += up256((size_t)F * sizeof(unsigned long long));
+    w.tickets = reinterpret_cast<unsigned long long *>(p);
+    p += TICKET_BYTES;
     w.staging = need_staging ? reinterpret_cast<float2 *>(p) : nullptr;
     w.chunk = need_staging ? staging_frames(F, S, R, C) : F;
     return OFDM_OK;
@@ -387,6 +427,7 @@ size_t ofdm_frame_workspace_bytes(long long nframes, int S, int R, int C) {
 
 int ofdm_workspace_release(const void *d_ws) {
     ws_forget(d_ws);
+    tickets_forget(d_ws);
     return OFDM_OK;
 }
 
@@ -423,7 +464,7 @@ int ofdm_frame_combine(const ofdm_cf32 *d_iq, long long nframes, int S, int R, i
     hipStream_t s = hs(stream);
     if (fused_c(C))
         return hip_check(mrc_fused(F2(d_iq), nframes, S, R, C, prefix, w.Hc, w.P,
-                                                 F2(d_out), 0, s),
+                                                 F2(d_out), 0, s, d_ws, w.tickets),
                          "mrc_fused");
     // staged path: the FFT of every chunk is redone here (estimate kept only Hc/P)
     return td_staged(F2(d_iq), nframes, S, R, C, prefix, nullptr, w, F2(d_out), 3, s);
@@ -450,10 +491,15 @@ int ofdm_frame_demod_ex(const ofdm_cf32 *d_iq, long long nframes, int S, int R, 
     hipStream_t s = hs(stream);
     ws_forget(d_ws);
     if (flow == OFDM_FLOW_AUTO && one_launch_demod(C, s)) {
+        int par = 0;
+        if ((rc = hip_check(tickets_next(d_ws, w.tickets, s, &par), "work tickets"))) return rc;
         rc = hip_check(ofdm::launch_demod_td1024(F2(d_iq), nframes, S, R, prefix, F2(d_X), w.Hc, w.P, F2(d_out),
-                                                 w.flags, next_epoch(), spin_ticks, s),
+                                                 w.tickets, par, w.flags, next_epoch(), spin_ticks, s),
                        "launch_demod_td");
-        if (rc == OFDM_OK) ws_record(d_ws, ws_bytes_, nframes, S, R, C, true, false);
+        if (rc == OFDM_OK)
+            ws_record(d_ws, ws_bytes_, nframes, S, R, C, true, false);
+        else
+            tickets_forget(d_ws);  // no kernel zeroed the next set: start over at the next use
         return rc;
     }
     if (fused_c(C)) {
@@ -462,7 +508,8 @@ int ofdm_frame_demod_ex(const ofdm_cf32 *d_iq, long long nframes, int S, int R, 
         if (rc) return rc;
         // the estimate is in the workspace once the LS launch is enqueued
         ws_record(d_ws, ws_bytes_, nframes, S, R, C, true, false);
-        return hip_check(mrc_fused(F2(d_iq), nframes, S, R, C, prefix, w.Hc, w.P, F2(d_out), 0, s), "mrc_fused");
+        return hip_check(mrc_fused(F2(d_iq), nframes, S, R, C, prefix, w.Hc, w.P, F2(d_out), 0, s, d_ws, w.tickets),
+                         "mrc_fused");
     }
     rc = td_staged(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w, F2(d_out), 0, s);
     if (rc == OFDM_OK) ws_record(d_ws, ws_bytes_, nframes, S, R, C, lane_c(C), false);
@@ -577,7 +624,7 @@ int ofdm_frame_mrc_partial(const ofdm_cf32 *d_iq, long long nframes, int S, int 
     hipStream_t s = hs(stream);
     if (fused_c(C))
         return hip_check(mrc_fused(F2(d_iq), nframes, S, R, C, prefix, w.Hc, w.P,
-                                                 F2(d_num), 1, s),
+                                                 F2(d_num), 1, s, d_ws, w.tickets),
                          "mrc_fused");
     return td_staged(F2(d_iq), nframes, S, R, C, prefix, nullptr, w, F2(d_num), 1, s);
 }
@@ -618,7 +665,7 @@ int ofdm_symbols_demod(const ofdm_cf32 *d_sym, long long nsym, int R, int C, int
     const long long row = (long long)R * (C + prefix);
     const float2 *iq = reinterpret_cast<const float2 *>(reinterpret_cast<uintptr_t>(d_sym) - (uintptr_t)(row * 8));
     return hip_check(mrc_fused(iq, 1, (int)(nsym + 1), R, C, prefix, w.Hc + frame * (long long)R * C,
-                               w.P + frame * C, F2(d_out), 0, hs(stream)),
+                               w.P + frame * C, F2(d_out), 0, hs(stream), d_ws, w.tickets),
                      fn);
 }
 

@@ -391,9 +391,9 @@ __device__ __forceinline__ void hlds_ls_frame(const float2 *__restrict__ iq, int
 // DESIGN.md 4.6).
 __global__ void __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 4)))
 k_demod_td1024(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ X, float2 *Hc,
-               float *P, float2 *__restrict__ out, long long nq, long long nblocks, long long per_xcd,
-               unsigned long long *flags, unsigned long long epoch, int nls, long long nframes,
-               long long spin_ticks) {
+               float *P, float2 *__restrict__ out, long long nq, long long nblocks, unsigned long long *tickets,
+               int par, long long k0, unsigned long long *flags, unsigned long long epoch, int nls,
+               long long nframes, long long spin_ticks) {
     using namespace hlds;
     constexpr int HW = WAVES;
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
@@ -411,20 +411,21 @@ k_demod_td1024(const float2 *__restrict__ iq, int S, int R, int prefix, const fl
     // inlined code and write the same bytes (two inlined copies
     // could contract differently).
     const bool estimator = (int)blockIdx.x < nls;
-    // MRC block map (XCD-grouped logical block; a pure function of blockIdx,
-    // recomputed after the LS loop rather than held across it)
-    auto mrc_block = [&]() { const long long pb = blockIdx.x - nls; return (pb & 7) * per_xcd + (pb >> 3); };
+    // MRC workgroups: the logical block (8 consecutive data symbols) is a
+    // work ticket (take_block: own XCD's range first, then the others'),
+    // kept in SGPRs
     auto first_frame = [&](long long lb) { return (lb * HW) / (S - 1); };
     auto last_frame = [&](long long lb) { return ((lb * HW + HW - 1 < nq ? lb * HW + HW - 1 : nq - 1)) / (S - 1); };
-    long long e0 = 1, e1 = 0;
+    long long e0 = 1, e1 = 0, lb = 0;
     if (estimator) {
         e0 = e1 = blockIdx.x;
         if (e0 >= nframes) return;
         fill(tw1, tw2);
         __syncthreads();
     } else {
-        const long long lb = mrc_block();
-        if (lb >= nblocks) return;
+        lb = wg_take_block(tickets, par, nblocks, k0, (long long)blockIdx.x - nls,
+                           reinterpret_cast<long long *>(hfree + 255));
+        if (lb < 0) return;  // every block taken
         fill(tw1, tw2);
         // wait for the estimates of frames f0 .. fl (hfree, not used before
         // the rows, carries the outcome); not published in time: estimate
@@ -446,7 +447,6 @@ k_demod_td1024(const float2 *__restrict__ iq, int S, int R, int prefix, const fl
     if (e0 <= e1) acquire_all();
     OFDM_DIAG_MARK()
 
-    const long long lb = mrc_block();
     const int nsym = S - 1;
     const long long qw = lb * HW + w;
     const bool store = qw < nq;
@@ -518,17 +518,18 @@ hipError_t launch_mrc_td1024(const float2 *iq, long long nframes, int S, int R, 
 // spin_ticks: how long (100 MHz ticks) an MRC workgroup waits for a frame's
 // flag before it estimates the frame itself (< 0: SPIN_TICKS).
 hipError_t launch_demod_td1024(const float2 *iq, long long nframes, int S, int R, int prefix, const float2 *X,
-                               float2 *Hc, float *P, float2 *out, unsigned long long *flags,
-                               unsigned long long epoch, long long spin_ticks, hipStream_t s) {
+                               float2 *Hc, float *P, float2 *out, unsigned long long *tickets, int par,
+                               unsigned long long *flags, unsigned long long epoch, long long spin_ticks,
+                               hipStream_t s) {
     using namespace td1024;
     const long long nq = nframes * (S - 1);
     if (nq <= 0) return hipSuccess;
     const long long nb = (nq + hlds::WAVES - 1) / hlds::WAVES;
-    const long long pxcd = (nb + 7) / 8;
     const long long nls = (nframes + 7) / 8 * 8;
-    if (pxcd * 8 + nls > 0x7fffffffll) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_demod_td1024, dim3((unsigned)(nls + pxcd * 8)), dim3(64 * hlds::WAVES), hlds::LDS_BYTES,
-                       s, iq, S, R, prefix, X, Hc, P, out, nq, nb, pxcd, flags, epoch, (int)nls, nframes,
+    const long long g = ticket_grid(nb);
+    if (g + nls > 0x7fffffffll) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_demod_td1024, dim3((unsigned)(nls + g)), dim3(64 * hlds::WAVES), hlds::LDS_BYTES, s, iq,
+                       S, R, prefix, X, Hc, P, out, nq, nb, tickets, par, ticket_k0(2), flags, epoch, (int)nls, nframes,
                        spin_ticks < 0 ? SPIN_TICKS : spin_ticks);
     return hipGetLastError();
 }

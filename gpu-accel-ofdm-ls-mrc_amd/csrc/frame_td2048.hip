@@ -256,14 +256,17 @@ __device__ __forceinline__ void mrc2048_symbol(const float2 *__restrict__ iq, in
 __global__ void __attribute__((amdgpu_flat_work_group_size(256, 256), amdgpu_waves_per_eu(2, 2)))
 k_mrc_td2048(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
              const float *__restrict__ P, float2 *__restrict__ out, long long nq, long long nblocks,
-             long long per_xcd, int mode) {
+             unsigned long long *tickets, int par, long long k0, int mode) {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     const int w = threadIdx.x >> 6, t = threadIdx.x & 63;
     float2 *T = lds + TAB + w * hl::TS;
-    const long long pb = blockIdx.x;
-    const long long lb = (pb & 7) * per_xcd + (pb >> 3);
-    if (lb >= nblocks) return;
     OFDM_DIAG_BEGIN()
+    // the logical block (4 consecutive data symbols) is a work ticket
+    // (wave_fft1024.hpp take_block); the slot is wave 0's transpose image,
+    // first written after the table barrier
+    const long long lb = td1024::wg_take_block(tickets, par, nblocks, k0, blockIdx.x,
+                                               reinterpret_cast<long long *>(lds + TAB));
+    if (lb < 0) return;
     fill_tables(lds);
     __syncthreads();
     const long long q = lb * MRC_WAVES + w;
@@ -285,17 +288,17 @@ hipError_t launch_ls_td2048(const float2 *iq, long long nframes, int S, int R, i
 }
 
 hipError_t launch_mrc_td2048(const float2 *iq, long long nframes, int S, int R, int prefix,
-                             const float2 *Hc, const float *P, float2 *out, int mode, hipStream_t s) {
+                             const float2 *Hc, const float *P, float2 *out, int mode, unsigned long long *tickets,
+                             int par, hipStream_t s) {
     using namespace td2048;
     const long long nq = nframes * (S - 1);
     if (nq <= 0) return hipSuccess;
     const long long nblocks = (nq + MRC_WAVES - 1) / MRC_WAVES;
-    const long long per_xcd = (nblocks + 7) / 8;
-    const long long grid = per_xcd * 8;
+    const long long grid = td1024::ticket_grid(nblocks);
     if (grid > 0x7fffffffll) return hipErrorInvalidValue;
     auto kern = k_mrc_td2048;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * MRC_WAVES), lds_bytes(MRC_WAVES), s, iq, S,
-                       R, prefix, Hc, P, out, nq, nblocks, per_xcd, mode);
+                       R, prefix, Hc, P, out, nq, nblocks, tickets, par, td1024::ticket_k0(2), mode);
     return hipGetLastError();
 }
 

@@ -197,6 +197,7 @@ __device__ __forceinline__ pk::v2f dif_tw(pk::v2f base) {  // base * W64^(CM * M
 
 using td1024::dma16;
 using td1024::lds_addr;
+using td1024::wg_take_block;
 
 // One 32 KiB Hc row (4096 float2) into LDS by an NW-wave workgroup: 32 / NW
 // wave-instructions of 1 KiB per wave, natural order.
@@ -425,13 +426,16 @@ __device__ __forceinline__ void mrc4096_block(const float2 *__restrict__ iq, int
 __global__ void __attribute__((amdgpu_flat_work_group_size(128 * H_PAIRS, 128 * H_PAIRS), amdgpu_waves_per_eu(2, 2)))
 k_mrc_td4096h(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
               const float *__restrict__ P, float2 *__restrict__ out, long long nframes, long long nblocks,
-              long long per_xcd, int mode) {
+              unsigned long long *tickets, int par, long long k0, int mode) {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     const int pair = __builtin_amdgcn_readfirstlane(threadIdx.x >> 7);
-    const long long pb = blockIdx.x;
-    const long long lb = (pb & 7) * per_xcd + (pb >> 3);  // XCD-grouped: a frame's blocks share an L2
-    if (lb >= nblocks) return;  // whole workgroup
     OFDM_DIAG_BEGIN()
+    // the logical block is a work ticket (wave_fft1024.hpp take_block: own
+    // XCD's range of consecutive blocks first -- a frame's blocks share an
+    // L2 -- then the others'); the slot is wave 0's transpose image, first
+    // written after mrc4096_block's table barrier
+    const long long lb = wg_take_block(tickets, par, nblocks, k0, blockIdx.x, reinterpret_cast<long long *>(lds + X_TAB));
+    if (lb < 0) return;  // whole workgroup: every block taken
     const int nsym = S - 1;
     const long long bpf = (nsym + H_PAIRS - 1) / H_PAIRS;
     const long long f = lb / bpf;
@@ -459,12 +463,13 @@ hipError_t launch_ls_td4096(const float2 *iq, long long nframes, int S, int R, i
 }
 
 hipError_t launch_mrc_td4096(const float2 *iq, long long nframes, int S, int R, int prefix,
-                             const float2 *Hc, const float *P, float2 *out, int mode, hipStream_t s) {
+                             const float2 *Hc, const float *P, float2 *out, int mode, unsigned long long *tickets,
+                             int par, hipStream_t s) {
     using namespace td4096;
     const long long nq = nframes * (S - 1);
     if (nq <= 0) return hipSuccess;
-    const long long bpf = ((S - 1) + H_PAIRS - 1) / H_PAIRS, nb = nframes * bpf, pxcd = (nb + 7) / 8;
-    if (pxcd * 8 > 0x7fffffffll) return hipErrorInvalidValue;
+    const long long bpf = ((S - 1) + H_PAIRS - 1) / H_PAIRS, nb = nframes * bpf, g = td1024::ticket_grid(nb);
+    if (g > 0x7fffffffll) return hipErrorInvalidValue;
     // The row's two FFT1024s software-pipelined through the transpose
     // image and the first quarter of the next row issued at the row start
     // (same-process A/B, R=32 x 300 frames: 6.81 vs 7.53 ms, bit-identical;
@@ -472,8 +477,8 @@ hipError_t launch_mrc_td4096(const float2 *iq, long long nframes, int S, int R, 
     auto kern = k_mrc_td4096h;
     if (hipError_t e = opt_in_lds(reinterpret_cast<const void *>(kern), (int)H_LDS); e != hipSuccess)
         return e;  // > 64 KiB of dynamic LDS
-    hipLaunchKernelGGL(kern, dim3((unsigned)(pxcd * 8)), dim3(128 * H_PAIRS), H_LDS, s, iq, S, R, prefix,
-                       Hc, P, out, nframes, nb, pxcd, mode);
+    hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(128 * H_PAIRS), H_LDS, s, iq, S, R, prefix, Hc, P, out, nframes,
+                       nb, tickets, par, td1024::ticket_k0(1), mode);
     return hipGetLastError();
 }
 

@@ -127,20 +127,23 @@ hipError_t launch_mrc_td1024(const float2 *iq, long long nframes, int S, int R, 
 // MRC workgroups wait for it.  flags: nframes words in the workspace; epoch:
 // a per-launch value no flag holds.  mode 0 (full demod) only.
 hipError_t launch_demod_td1024(const float2 *iq, long long nframes, int S, int R, int prefix, const float2 *X,
-                               float2 *Hc, float *P, float2 *out, unsigned long long *flags,
-                               unsigned long long epoch, long long spin_ticks, hipStream_t s);
+                               float2 *Hc, float *P, float2 *out, unsigned long long *tickets, int par,
+                               unsigned long long *flags, unsigned long long epoch, long long spin_ticks,
+                               hipStream_t s);
 
 // Stage-wise operations of the reference's per-stage gpuLS methods (stages.hip).
 // fused time-domain receiver, C = 2048 (frame_td2048.hip); same contracts
 hipError_t launch_ls_td2048(const float2 *iq, long long nframes, int S, int R, int prefix,
                             const float2 *X, float2 *Hc, float *P, int partial, hipStream_t s);
 hipError_t launch_mrc_td2048(const float2 *iq, long long nframes, int S, int R, int prefix,
-                             const float2 *Hc, const float *P, float2 *out, int mode, hipStream_t s);
+                             const float2 *Hc, const float *P, float2 *out, int mode, unsigned long long *tickets,
+                             int par, hipStream_t s);
 // fused time-domain receiver, C = 4096 (frame_td4096.hip); same contracts
 hipError_t launch_ls_td4096(const float2 *iq, long long nframes, int S, int R, int prefix,
                             const float2 *X, float2 *Hc, float *P, int partial, hipStream_t s);
 hipError_t launch_mrc_td4096(const float2 *iq, long long nframes, int S, int R, int prefix,
-                             const float2 *Hc, const float *P, float2 *out, int mode, hipStream_t s);
+                             const float2 *Hc, const float *P, float2 *out, int mode, unsigned long long *tickets,
+                             int par, hipStream_t s);
 hipError_t launch_conj_product(const float2 *Y, long long nsyms, int R, int C, const float2 *Hc,
                                float2 *prod, hipStream_t s);
 hipError_t launch_combine(const float2 *prod, long long nsyms, int R, int K, const float *P,

@@ -290,6 +290,91 @@ __device__ __forceinline__ void acquire_all() {
     __syncthreads();
 }
 
+// ---------------------------------------------------------------------------
+// Work tickets: which logical block a workgroup processes is decided at run
+// time, not fixed by blockIdx.  Blocks are dealt to the 8 XCDs round-robin
+// by the hardware, so with a static map every XCD gets 1/8 of the blocks and
+// the kernel ends when the SLOWEST XCD does (round-5 stamps, csrc/diag.hpp:
+// per-XCD workgroup lifetimes up to 10 % apart at the headline shape and at
+// C = 4096, at equal clocks -- a memory-side difference).  The blocks are
+// cut into 8 contiguous ranges, one per XCD (a frame's consecutive blocks
+// keep sharing one L2).  The first k0 blocks of range y go statically to
+// the workgroups with (index & 7) == y, (index >> 3) < k0 -- the first round,
+// which would otherwise queue on the counters all at once; every later block
+// is a ticket: a workgroup takes the next one of its own XCD's range (the
+// XCC_ID register; speed only) and, once that range is exhausted, of the
+// other ranges in turn (one atomic add per block taken).  The grid is
+// over-subscribed (ticket_grid: + 25 % + 64 workgroups); a workgroup that
+// finds every range exhausted exits at once.  Every block is processed
+// exactly once whatever the placement or dispatch order.
+// Counters: two sets of 8 (one 128-B line each) in the workspace's ticket
+// area; a launch counts in set `par` and zeroes set par ^ 1 for the next
+// launch on this workspace (the host flips `par` per launch and zeroes both
+// sets the first time it meets a workspace), so no counter needs a reset
+// between two launches and no launch pays for one.
+// ---------------------------------------------------------------------------
+constexpr int TICKET_STRIDE = 16;            // u64 words between counters (128 B)
+constexpr int TICKET_SET = 8 * TICKET_STRIDE;  // words per set
+constexpr int HWREG_XCC_ID = (31 << 11) | 20;
+__device__ __forceinline__ long long ticket_range_count(long long nb, long long per, unsigned y) {
+    const long long lo = (long long)y * per;
+    return nb - lo < per ? (nb - lo > 0 ? nb - lo : 0) : per;
+}
+// thread 0 of workgroup index pb (0-based among the ticketed workgroups)
+__device__ __forceinline__ long long take_block(unsigned long long *set, long long nb, long long k0, long long pb) {
+    const long long per = (nb + 7) / 8;
+    if (pb < 8 * k0) {  // the static first round
+        const unsigned y = (unsigned)(pb & 7);
+        const long long k = pb >> 3, cnt = ticket_range_count(nb, per, y);
+        if (k < (cnt < k0 ? cnt : k0)) return (long long)y * per + k;
+    }
+    const unsigned x = (unsigned)__builtin_amdgcn_s_getreg(HWREG_XCC_ID) & 7u;
+    for (int j = 0; j < 8; ++j) {
+        const unsigned y = (x + (unsigned)j) & 7u;
+        const long long cnt = ticket_range_count(nb, per, y), s0 = cnt < k0 ? cnt : k0;
+        const long long avail = cnt - s0;
+        if (avail <= 0) continue;
+        gu64 *p = (gu64 *)(set + y * TICKET_STRIDE);
+        if ((long long)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= avail) continue;
+        const long long t = (long long)__hip_atomic_fetch_add(p, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t < avail) return (long long)y * per + s0 + t;
+    }
+    return -1;
+}
+// the workgroup's block: thread 0 takes it (workgroup 0 also zeroes the
+// other counter set), everyone reads it from `slot` (an LDS word nothing
+// else touches before the caller's next barrier); SGPR-uniform result
+__device__ __forceinline__ long long wg_take_block(unsigned long long *tickets, int par, long long nb, long long k0,
+                                                   long long pb, long long *slot) {
+    if (threadIdx.x == 0) {
+        if (pb == 0) {
+            unsigned long long *nxt = tickets + (par ^ 1) * TICKET_SET;
+#pragma unroll
+            for (int y = 0; y < 8; ++y)
+                __hip_atomic_store((gu64 *)(nxt + y * TICKET_STRIDE), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        *slot = take_block(tickets + par * TICKET_SET, nb, k0, pb);
+    }
+    __syncthreads();
+    const long long v = *slot;
+    const int lo = __builtin_amdgcn_readfirstlane((int)(v & 0xffffffffll));
+    const int hi = __builtin_amdgcn_readfirstlane((int)(v >> 32));
+    return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
+// the over-subscribed grid of a ticketed kernel: nb blocks + 25 % + 64
+inline long long ticket_grid(long long nb) { return nb + nb / 4 + 64; }
+// static blocks per XCD range: the resident workgroups of one XCD (per_cu
+// workgroups on each of its CUs), i.e. the first round
+inline long long ticket_k0(int per_cu) {
+    static const int cus = [] {
+        int dev = 0, n = 256;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            n = 256;
+        return n;
+    }();
+    return (long long)per_cu * cus / 8;
+}
+
 // Twiddle tables and the two FFT halves in the LDS layout of the HLDS
 // kernels (k_mrc_td1024_hlds, frame_td2048.hip); see frame_td.hip.
 namespace hlds {

@@ -57,7 +57,11 @@ rng = np.random.default_rng(1)
 amp = np.float32(0.70710678)
 X = torch.from_numpy((rng.choice([-amp, amp], K) + 1j * rng.choice([-amp, amp], K)).astype(np.complex64)).to(dev)
 iq = ofdm.synth_frames(F, S, R, C, X, seed=1, noise_std=0.01)
-ws = {n: ofdm.workspace(F, S, R, C, dev) for n in a.libs}
+ws = {}
+for n in a.libs:  # each build sizes its own workspace (ofdm_frame_workspace_bytes)
+    ofdm._lib = libs[n]
+    ws[n] = ofdm.workspace(F, S, R, C, dev)
+ofdm._lib = libs[a.libs[0]]
 out = {n: ofdm.c64((F, S - 1, K), dev) for n in a.libs}
 stream = torch.cuda.current_stream()
 b_sym = R * C * 8 + K * 8

@@ -51,6 +51,14 @@ def analyse(rec, nls=0):
     res["ramp_us_to_90pct"] = float(ts[up[0]]) if len(up) else None
     # work-weighted occupancy: sum of lifetimes / (peak x span)
     res["occupancy_fill"] = float((en - st).sum() / (peak * span)) if peak else 0.0
+    # per XCD (xcc_id): workgroups, median lifetime, last end -- a static
+    # block map makes the slowest XCD's last end the kernel's end
+    xcc = rec[:, 6] & 0xF
+    work = blk >= nls
+    res["per_xcd"] = {int(x): {"n": int((work & (xcc == x)).sum()),
+                               "life_us_p50": float(np.median((en - st)[work & (xcc == x)])),
+                               "last_end_us": float(en[work & (xcc == x)].max())}
+                      for x in range(8) if (work & (xcc == x)).any()}
     return res
 
 

@@ -140,13 +140,14 @@ def test_product_library_dispatches_only_product_kernels(ofdm):
 
 
 def test_workspace_sizes(ofdm):
-    # fused C=1024: Hc [F][R][C] + P [F][C] + one flag word per frame, no staging
+    # fused C=1024: Hc [F][R][C] + P [F][C] + one flag word per frame + the
+    # two sets of 8 work-ticket counters (one 128-B line each), no staging
     F, S, R, C = 100, 101, 16, 1024
     b = ofdm.workspace_bytes(F, S, R, C)
-    assert b == F * R * C * 8 + F * C * 4 + (F * 8 + 255) // 256 * 256
+    assert b == F * R * C * 8 + F * C * 4 + (F * 8 + 255) // 256 * 256 + 2 * 8 * 128
     # non-fused C carries a bounded staging buffer (<= 256 MiB or one frame)
     b2 = ofdm.workspace_bytes(F, S, 64, 2048)
-    assert b2 - (F * 64 * 2048 * 8 + F * 2048 * 4) <= max(256 << 20, S * 64 * 2048 * 8) + 512
+    assert b2 - (F * 64 * 2048 * 8 + F * 2048 * 4) <= max(256 << 20, S * 64 * 2048 * 8) + 512 + 2048
     # any other C in [2, 8192] runs the staged path (mixed-radix row FFT)
     for c in (2, 7, 1000, 1536, 8192):
         assert ofdm.workspace_bytes(F, S, R, c) >= F * R * c * 8 + F * c * 4 + S * R * c * 8
