@@ -224,7 +224,7 @@ def box_probe(ofdm, torch, dev, stream, gib=4, reps=5):
     del src, dst
     torch.cuda.empty_cache()
     return {"box_copy_GBps": res["copy"], "box_read_GBps": res["read"],
-            "box_probe": f"ofdm_hbm_probe float4 over {gib} GiB, median of {reps}; copy counts read + written bytes"}
+            "box_probe": f"ofdm_hbm_probe over {gib} GiB (16 KiB non-temporal chunks per wave, 16 loads per lane in flight), median of {reps}; copy counts read + written bytes"}
 
 
 DIAG_LIB = os.path.join(ROOT, "gpu-accel-ofdm-ls-mrc_amd", "lib", "libofdm_lsmrc_diag.so")

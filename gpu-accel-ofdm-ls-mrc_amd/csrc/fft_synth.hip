@@ -280,56 +280,85 @@ hipError_t launch_count_errors(const float2 *out, long long nframes, int S, int 
 }
 
 // ---------------------------------------------------------------------------
-// HBM probes of the box (bench.py's roofline.box_*): a float4 copy and a
-// float4 read (summed, one float per thread written so the loads are kept)
-// over `n4` float4s, grid-stride, 4 independent 16-B loads per lane per step.
-// Plain loads and stores: the guide's "float4 copy" ceiling
-// (MI355X_MICROARCH.md: 6.29 TB/s measured against the 8 TB/s spec).
+// HBM probes of the box (bench.py's roofline.box_*): a streaming float4 copy
+// and a streaming float4 read (summed; one float per thread written so the
+// loads are kept) over `n4` float4s.  Each wave moves 16 KiB chunks -- 16
+// dwordx4 loads per lane issued before any is used (16 KiB in flight per
+// wave, 32 waves per CU) -- chunk c + grid waves next, non-temporal like the
+// receivers' IQ stream; the tail (< 16 KiB) by single loads.  This is the
+// ceiling of the receivers' access pattern (contiguous multi-KiB pieces per
+// wave) on this box, measured in the same process right after the timed
+// loop.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_hbm_copy(const float4 *__restrict__ src, float4 *__restrict__ dst,
-                                                  long long n4) {
-    const long long stride = (long long)gridDim.x * blockDim.x;
-    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    for (; i + 3 * stride < n4; i += 4 * stride) {
-        const float4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
-        dst[i] = a;
-        dst[i + stride] = b;
-        dst[i + 2 * stride] = c;
-        dst[i + 3 * stride] = d;
-    }
-    for (; i < n4; i += stride) dst[i] = src[i];
+constexpr int PROBE_TPB = 256, PROBE_U = 16;
+typedef float f4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ld_nt(const float4 *p) {
+    const f4v v = __builtin_nontemporal_load(reinterpret_cast<const f4v *>(p));
+    return float4{v.x, v.y, v.z, v.w};
+}
+__device__ __forceinline__ void st_nt(float4 v, float4 *p) {
+    __builtin_nontemporal_store(f4v{v.x, v.y, v.z, v.w}, reinterpret_cast<f4v *>(p));
 }
 
-__global__ void __launch_bounds__(256) k_hbm_read(const float4 *__restrict__ src, float *__restrict__ sink,
-                                                  long long n4) {
-    const long long stride = (long long)gridDim.x * blockDim.x;
-    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    float4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (; i + 3 * stride < n4; i += 4 * stride) {
-        const float4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
-        acc.x += (a.x + b.x) + (c.x + d.x);
-        acc.y += (a.y + b.y) + (c.y + d.y);
-        acc.z += (a.z + b.z) + (c.z + d.z);
-        acc.w += (a.w + b.w) + (c.w + d.w);
+__global__ void __launch_bounds__(PROBE_TPB) k_hbm_copy(const float4 *__restrict__ src, float4 *__restrict__ dst,
+                                                        long long n4) {
+    const int lane = threadIdx.x & 63;
+    const long long wave = ((long long)blockIdx.x * PROBE_TPB + threadIdx.x) >> 6;
+    const long long nwaves = (long long)gridDim.x * (PROBE_TPB / 64);
+    const long long chunk = 64 * PROBE_U, nchunks = n4 / chunk;
+    for (long long c = wave; c < nchunks; c += nwaves) {
+        const float4 *s = src + c * chunk + lane;
+        float4 *d = dst + c * chunk + lane;
+        float4 v[PROBE_U];
+#pragma unroll
+        for (int u = 0; u < PROBE_U; ++u) v[u] = ld_nt(s + 64 * u);
+#pragma unroll
+        for (int u = 0; u < PROBE_U; ++u) st_nt(v[u], d + 64 * u);
     }
-    for (; i < n4; i += stride) {
+    for (long long i = nchunks * chunk + (long long)blockIdx.x * PROBE_TPB + threadIdx.x; i < n4;
+         i += (long long)gridDim.x * PROBE_TPB)
+        dst[i] = src[i];
+}
+
+__global__ void __launch_bounds__(PROBE_TPB) k_hbm_read(const float4 *__restrict__ src, float *__restrict__ sink,
+                                                        long long n4) {
+    const int lane = threadIdx.x & 63;
+    const long long wave = ((long long)blockIdx.x * PROBE_TPB + threadIdx.x) >> 6;
+    const long long nwaves = (long long)gridDim.x * (PROBE_TPB / 64);
+    const long long chunk = 64 * PROBE_U, nchunks = n4 / chunk;
+    float4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (long long c = wave; c < nchunks; c += nwaves) {
+        const float4 *s = src + c * chunk + lane;
+        float4 v[PROBE_U];
+#pragma unroll
+        for (int u = 0; u < PROBE_U; ++u) v[u] = ld_nt(s + 64 * u);
+#pragma unroll
+        for (int u = 0; u < PROBE_U; ++u) {
+            acc.x += v[u].x;
+            acc.y += v[u].y;
+            acc.z += v[u].z;
+            acc.w += v[u].w;
+        }
+    }
+    for (long long i = nchunks * chunk + (long long)blockIdx.x * PROBE_TPB + threadIdx.x; i < n4;
+         i += (long long)gridDim.x * PROBE_TPB) {
         const float4 a = src[i];
         acc.x += a.x;
         acc.y += a.y;
         acc.z += a.z;
         acc.w += a.w;
     }
-    sink[(long long)blockIdx.x * blockDim.x + threadIdx.x] = (acc.x + acc.y) + (acc.z + acc.w);
+    sink[(long long)blockIdx.x * PROBE_TPB + threadIdx.x] = (acc.x + acc.y) + (acc.z + acc.w);
 }
 
 hipError_t launch_hbm_probe(int mode, const void *src, void *dst, long long n4, hipStream_t s) {
     if (n4 <= 0) return hipSuccess;
-    const int blocks = 256 * 8;  // 8 workgroups of 256 threads per CU
+    const int blocks = 256 * 4;  // 4 workgroups of 256 threads per CU (16 waves, 256 KiB in flight)
     if (mode == 0)
-        hipLaunchKernelGGL(k_hbm_copy, dim3(blocks), dim3(256), 0, s, static_cast<const float4 *>(src),
+        hipLaunchKernelGGL(k_hbm_copy, dim3(blocks), dim3(PROBE_TPB), 0, s, static_cast<const float4 *>(src),
                            static_cast<float4 *>(dst), n4);
     else
-        hipLaunchKernelGGL(k_hbm_read, dim3(blocks), dim3(256), 0, s, static_cast<const float4 *>(src),
+        hipLaunchKernelGGL(k_hbm_read, dim3(blocks), dim3(PROBE_TPB), 0, s, static_cast<const float4 *>(src),
                            static_cast<float *>(dst), n4);
     return hipGetLastError();
 }

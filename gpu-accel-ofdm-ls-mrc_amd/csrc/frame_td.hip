@@ -383,6 +383,57 @@ __device__ __forceinline__ void hlds_ls_frame(const float2 *__restrict__ iq, int
     __syncthreads();  // pp (the transpose images) read before they are reused
 }
 
+// A half unit of the one-launch demod's schedule tail: four consecutive data
+// symbols q0 .. q0+3 with each symbol's antenna rows split over two waves
+// (wave w: symbol w & 3, rows [0, R0) for w < 4, [R0, R) for w >= 4), so the
+// unit takes about half a block's time.  Each wave reads its own Hc rows
+// (L2; no shared row, the two halves of the workgroup are at different rows),
+// the second-half waves hand their sums over through their transpose images
+// and the first-half waves add them (first half + second half) and store.
+// Every wave reaches the one workgroup barrier.
+__device__ __forceinline__ void split_unit(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *Hc,
+                                           const float *P, float2 *__restrict__ out, long long nq, long long q0, int w,
+                                           int t, float2 *T, float2 *T0, const float2 *tw1, const float2 *tw2) {
+    const int nsym = S - 1, Cp = C + prefix, hh = w >> 2, R0 = (R + 1) >> 1;
+    const long long qw = q0 + (w & 3);
+    const bool store = qw < nq;
+    const long long q = store ? qw : nq - 1;
+    const long long f = q / nsym;
+    const int s = 1 + (int)(q % nsym);
+    const float2 *sym = iq + (f * S + s) * (long long)R * Cp + prefix;
+    const float4 *Hf = reinterpret_cast<const float4 *>(Hc + f * (long long)R * C);
+    float2 acc[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) acc[k] = float2{0.f, 0.f};
+    const int r1 = hh ? R : R0;
+    for (int r = hh ? R0 : 0; r < r1; ++r) {
+        float2 a[16], x[16], h[16];
+        row_load<true>(sym + (long long)r * Cp, t, a);
+        hlds::row_fft_a(a, t, T, tw1);
+        hlds::row_fft_b(t, T, tw2, x);
+        __builtin_amdgcn_sched_barrier(0);
+        hc_load(Hf + (long long)r * (C / 2), t, h);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {  // matrixMultThenSum (cpuLS.hpp:203-204), antennas in order per half
+            acc[k].x = acc[k].x + (x[k].x * h[k].x - x[k].y * h[k].y);
+            acc[k].y = acc[k].y + (x[k].x * h[k].y + x[k].y * h[k].x);
+        }
+    }
+    if (hh) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) T[k * hlds::TP + t] = acc[k];
+    }
+    __syncthreads();
+    if (hh) return;
+    const float2 *Tp = T0 + (w + 4) * hlds::TS;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const float2 v = Tp[k * hlds::TP + t];
+        acc[k] = float2{acc[k].x + v.x, acc[k].y + v.y};
+    }
+    if (store) hlds_epilogue(acc, P, f, q, t, T, out, 0);
+}
+
 // The estimate is stored write-through (sc1: 16-B Hc stores, 4-B agent
 // atomic P stores) and published without a release fence, whose L2
 // write-back would also flush the output lines the MRC workgroups of the
@@ -392,8 +443,8 @@ __device__ __forceinline__ void hlds_ls_frame(const float2 *__restrict__ iq, int
 __global__ void __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 4)))
 k_demod_td1024(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ X, float2 *Hc,
                float *P, float2 *__restrict__ out, long long nq, long long nblocks, unsigned long long *tickets,
-               int par, long long k0, unsigned long long *flags, unsigned long long epoch, int nls,
-               long long nframes, long long spin_ticks) {
+               int par, long long k0, long long split, unsigned long long *flags, unsigned long long epoch,
+               int nls, long long nframes, long long spin_ticks) {
     using namespace hlds;
     constexpr int HW = WAVES;
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
@@ -417,15 +468,18 @@ k_demod_td1024(const float2 *__restrict__ iq, int S, int R, int prefix, const fl
     auto first_frame = [&](long long lb) { return (lb * HW) / (S - 1); };
     auto last_frame = [&](long long lb) { return ((lb * HW + HW - 1 < nq ? lb * HW + HW - 1 : nq - 1)) / (S - 1); };
     long long e0 = 1, e1 = 0, lb = 0;
+    int um = 0;  // unit mode: 0 the whole block, 1 / 2 its first / second four symbols, rows split over waves
     if (estimator) {
         e0 = e1 = blockIdx.x;
         if (e0 >= nframes) return;
         fill(tw1, tw2);
         __syncthreads();
     } else {
-        lb = wg_take_block(tickets, par, nblocks, k0, (long long)blockIdx.x - nls,
-                           reinterpret_cast<long long *>(hfree + 255));
+        lb = wg_take_unit(tickets, par, nblocks, k0, (long long)blockIdx.x - nls, split,
+                          reinterpret_cast<long long *>(hfree + 255));
         if (lb < 0) return;  // every block taken
+        um = (int)(lb & 3);
+        lb >>= 2;
         fill(tw1, tw2);
         // wait for the estimates of frames f0 .. fl (hfree, not used before
         // the rows, carries the outcome); not published in time: estimate
@@ -448,6 +502,11 @@ k_demod_td1024(const float2 *__restrict__ iq, int S, int R, int prefix, const fl
     OFDM_DIAG_MARK()
 
     const int nsym = S - 1;
+    if (um) {  // a half unit of the schedule's tail (launch_demod_td1024)
+        split_unit(iq, S, R, prefix, Hc, P, out, nq, lb * HW + 4 * (um - 1), w, t, T, T0, tw1, tw2);
+        OFDM_DIAG_END_SLOT(td1024, epoch);
+        return;
+    }
     const long long qw = lb * HW + w;
     const bool store = qw < nq;
     const long long q = store ? qw : nq - 1;
@@ -526,10 +585,14 @@ hipError_t launch_demod_td1024(const float2 *iq, long long nframes, int S, int R
     if (nq <= 0) return hipSuccess;
     const long long nb = (nq + hlds::WAVES - 1) / hlds::WAVES;
     const long long nls = (nframes + 7) / 8 * 8;
-    const long long g = ticket_grid(nb);
+    // the schedule's tail in half units: the last k0 blocks of every XCD
+    // range (k0 = the XCD's resident workgroups) -- the last rounds end on
+    // units of about half a block's time (R >= 2)
+    const long long k0 = ticket_k0(2), split = R >= 2 ? k0 : 0;
+    const long long g = ticket_grid(nb, 8 * split);
     if (g + nls > 0x7fffffffll) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_demod_td1024, dim3((unsigned)(nls + g)), dim3(64 * hlds::WAVES), hlds::LDS_BYTES, s, iq,
-                       S, R, prefix, X, Hc, P, out, nq, nb, tickets, par, ticket_k0(2), flags, epoch, (int)nls, nframes,
+                       S, R, prefix, X, Hc, P, out, nq, nb, tickets, par, k0, split, flags, epoch, (int)nls, nframes,
                        spin_ticks < 0 ? SPIN_TICKS : spin_ticks);
     return hipGetLastError();
 }

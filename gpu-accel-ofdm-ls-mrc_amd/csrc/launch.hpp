@@ -164,7 +164,7 @@ hipError_t launch_synth(float2 *iq, long long nframes, int S, int R, int C, int 
                         int freq_domain, int r0, hipStream_t s);
 // Hard-decision QPSK errors of demodulated output against the synthetic data.
 // HBM probes (bench.py): mode 0 float4 copy src -> dst, mode 1 float4 read
-// of src (dst: 2048 x 256 floats of sums); n4 float4s
+// of src (dst: 1024 x 256 floats of sums); n4 float4s
 hipError_t launch_hbm_probe(int mode, const void *src, void *dst, long long n4, hipStream_t s);
 hipError_t launch_count_errors(const float2 *out, long long nframes, int S, int C,
                                uint64_t seed, long long frame0, unsigned long long *errors,

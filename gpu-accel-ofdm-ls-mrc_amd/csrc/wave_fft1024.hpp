@@ -320,32 +320,43 @@ __device__ __forceinline__ long long ticket_range_count(long long nb, long long 
     const long long lo = (long long)y * per;
     return nb - lo < per ? (nb - lo > 0 ? nb - lo : 0) : per;
 }
-// thread 0 of workgroup index pb (0-based among the ticketed workgroups)
-__device__ __forceinline__ long long take_block(unsigned long long *set, long long nb, long long k0, long long pb) {
+// thread 0 of workgroup index pb (0-based among the ticketed workgroups):
+// the unit (b << 2) | m of block b -- m = 0 the whole block; with split > 0
+// the last `split` blocks of every range are dealt as two half units each,
+// m = 1 and 2 (their first and second halves of symbols), so that the
+// schedule ends on units half as long (k_demod_td1024); -1: none left
+__device__ __forceinline__ long long take_unit(unsigned long long *set, long long nb, long long k0, long long pb,
+                                               long long split) {
     const long long per = (nb + 7) / 8;
     if (pb < 8 * k0) {  // the static first round
         const unsigned y = (unsigned)(pb & 7);
         const long long k = pb >> 3, cnt = ticket_range_count(nb, per, y);
-        if (k < (cnt < k0 ? cnt : k0)) return (long long)y * per + k;
+        if (k < (cnt < k0 ? cnt : k0)) return ((long long)y * per + k) << 2;
     }
     const unsigned x = (unsigned)__builtin_amdgcn_s_getreg(HWREG_XCC_ID) & 7u;
     for (int j = 0; j < 8; ++j) {
         const unsigned y = (x + (unsigned)j) & 7u;
         const long long cnt = ticket_range_count(nb, per, y), s0 = cnt < k0 ? cnt : k0;
-        const long long avail = cnt - s0;
+        const long long avail = cnt - s0;  // ticketed blocks of range y
         if (avail <= 0) continue;
+        const long long ns = split < avail ? split : avail, whole = avail - ns;
+        const long long units = whole + 2 * ns;
         gu64 *p = (gu64 *)(set + y * TICKET_STRIDE);
-        if ((long long)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= avail) continue;
+        if ((long long)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= units) continue;
         const long long t = (long long)__hip_atomic_fetch_add(p, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (t < avail) return (long long)y * per + s0 + t;
+        if (t >= units) continue;
+        const long long b0 = (long long)y * per + s0;
+        if (t < whole) return (b0 + t) << 2;
+        const long long u = t - whole;
+        return ((b0 + whole + (u >> 1)) << 2) | (1 + (u & 1));
     }
     return -1;
 }
-// the workgroup's block: thread 0 takes it (workgroup 0 also zeroes the
+// the workgroup's unit: thread 0 takes it (workgroup 0 also zeroes the
 // other counter set), everyone reads it from `slot` (an LDS word nothing
 // else touches before the caller's next barrier); SGPR-uniform result
-__device__ __forceinline__ long long wg_take_block(unsigned long long *tickets, int par, long long nb, long long k0,
-                                                   long long pb, long long *slot) {
+__device__ __forceinline__ long long wg_take_unit(unsigned long long *tickets, int par, long long nb, long long k0,
+                                                  long long pb, long long split, long long *slot) {
     if (threadIdx.x == 0) {
         if (pb == 0) {
             unsigned long long *nxt = tickets + (par ^ 1) * TICKET_SET;
@@ -353,7 +364,7 @@ __device__ __forceinline__ long long wg_take_block(unsigned long long *tickets, 
             for (int y = 0; y < 8; ++y)
                 __hip_atomic_store((gu64 *)(nxt + y * TICKET_STRIDE), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        *slot = take_block(tickets + par * TICKET_SET, nb, k0, pb);
+        *slot = take_unit(tickets + par * TICKET_SET, nb, k0, pb, split);
     }
     __syncthreads();
     const long long v = *slot;
@@ -361,8 +372,18 @@ __device__ __forceinline__ long long wg_take_block(unsigned long long *tickets, 
     const int hi = __builtin_amdgcn_readfirstlane((int)(v >> 32));
     return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
-// the over-subscribed grid of a ticketed kernel: nb blocks + 25 % + 64
-inline long long ticket_grid(long long nb) { return nb + nb / 4 + 64; }
+// whole blocks only: the block index, -1 when none is left
+__device__ __forceinline__ long long wg_take_block(unsigned long long *tickets, int par, long long nb, long long k0,
+                                                   long long pb, long long *slot) {
+    const long long u = wg_take_unit(tickets, par, nb, k0, pb, 0, slot);
+    return u < 0 ? u : u >> 2;
+}
+// The over-subscribed grid of a ticketed kernel: every workgroup takes at
+// most one unit and exits only once every range is exhausted, so a grid of
+// at least as many workgroups as units (nb blocks + one extra per split
+// block: split_units = 8 x split at most) processes every unit whatever the
+// placement; + 25 % + 64 so that fast XCDs find workgroups to take more.
+inline long long ticket_grid(long long nb, long long split_units = 0) { return nb + split_units + nb / 4 + 64; }
 // static blocks per XCD range: the resident workgroups of one XCD (per_cu
 // workgroups on each of its CUs), i.e. the first round
 inline long long ticket_k0(int per_cu) {

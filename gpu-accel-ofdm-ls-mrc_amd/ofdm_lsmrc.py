@@ -142,7 +142,7 @@ class using:
 
 def hbm_probe(mode, src, dst, stream=None):
     """Box probe: mode 0 copies src -> dst (float4), mode 1 reads src (dst:
-    >= 2 MiB of partial sums).  Byte tensors on the device, 16-B multiples."""
+    >= 1 MiB of partial sums).  Byte tensors on the device, 16-B multiples."""
     nbytes = src.numel() * src.element_size()
     _check(lib().ofdm_hbm_probe(mode, _dptr(src, "src"), _dptr(dst, "dst"), nbytes, _stream(stream)),
            "ofdm_hbm_probe")

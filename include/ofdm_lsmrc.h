@@ -396,9 +396,10 @@ int ofdm_count_symbol_errors(const ofdm_cf32 *d_out, long long nframes, int S, i
 int ofdm_buffer_hash(const void *d_buf, size_t bytes, unsigned long long *d_hash, ofdm_stream_t stream);
 
 /* Box probe for bench.py (no reference counterpart): mode 0 copies `bytes`
- * from d_src to d_dst as float4s, mode 1 reads them (d_dst receives
- * 2048 x 256 float partial sums, 2 MiB).  Plain 16-B loads/stores over the
- * whole chip; `bytes` and both pointers 16-B aligned. */
+ * from d_src to d_dst, mode 1 reads them (d_dst receives 1024 x 256 float
+ * partial sums, 1 MiB): every wave streams 16 KiB chunks with 16 non-temporal
+ * 16-B loads per lane in flight -- the receivers' access pattern.  `bytes`
+ * and both pointers 16-B aligned. */
 int ofdm_hbm_probe(int mode, const void *d_src, void *d_dst, size_t bytes, ofdm_stream_t stream);
 
 #ifdef __cplusplus

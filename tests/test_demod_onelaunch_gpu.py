@@ -52,8 +52,12 @@ def two_launch(ofdm, iq, X, prefix):
 # 7 x 3 = 21 symbols leaves tail waves in the last workgroup; R = 1 and R = 9
 # leave estimator waves without rows / with one extra row.  C = 4096
 # workgroups are frame-aligned (4 symbols): S = 7 leaves tail pairs.
+# Batches of more than 512 workgroups' blocks take work tickets: 60 x 101 x
+# 9 (every ticketed block split into two half units, 5 + 4 rows per wave)
+# and 150 x 101 x 3 (whole tickets, then half units of 2 + 1 rows).
 @pytest.mark.parametrize("C,F,S,R,prefix", [(1024, 100, 101, 16, 0), (1024, 7, 4, 1, 0), (1024, 5, 7, 9, 8),
-                                            (1024, 3, 101, 64, 72), (1024, 1, 2, 4, 0), (1024, 40, 13, 16, 0)])
+                                            (1024, 3, 101, 64, 72), (1024, 1, 2, 4, 0), (1024, 40, 13, 16, 0),
+                                            (1024, 60, 101, 9, 8), (1024, 150, 101, 3, 0)])
 def test_one_launch_matches_two_launch(ofdm, dev, C, F, S, R, prefix):
     X = pilots(dev, C - 1)
     iq = ofdm.synth_frames(F, S, R, C, X, prefix=prefix, seed=F * 1000 + S * 10 + R, noise_std=0.01)
@@ -163,7 +167,7 @@ def test_graph_capture_takes_two_launches(ofdm, dev):
     parity(host(out), two_launch(ofdm, a, X, 0))
 
 
-@pytest.mark.parametrize("F,S,R", [(9, 13, 16), (3, 101, 64), (20, 5, 4)])
+@pytest.mark.parametrize("F,S,R", [(9, 13, 16), (3, 101, 64), (20, 5, 4), (60, 101, 4)])
 def test_bounded_wait_fallback(ofdm, dev, F, S, R):
     """ofdm_frame_demod_ex with spin_ticks = 0: no MRC workgroup waits for a
     flag; each estimates the frame(s) it reads itself, through the same
@@ -192,3 +196,59 @@ def test_frame_demod_ex_rejects_unknown_flow(ofdm, dev):
     iq = torch.zeros((1, 2, 1, 1024), dtype=torch.complex64, device=dev)
     with pytest.raises(ofdm.OfdmError, match="flow=7"):
         ofdm.frame_demod(iq, X, flow=7)
+
+
+def test_work_tickets_reused_workspace(ofdm, dev):
+    """Work tickets (wave_fft1024.hpp take_unit): a batch large enough for
+    ticketed blocks and half units, demodulated 4 times in turn with another
+    batch on ONE workspace -- every launch counts in the counter set the
+    previous launch zeroed; every output must match its two-launch
+    reference, and a repeat must be bit-identical (the schedule changes
+    which workgroup takes a block, never the block's arithmetic)."""
+    import torch
+    F, S, R, C = 60, 101, 4, 1024
+    X = pilots(dev, C - 1)
+    a = ofdm.synth_frames(F, S, R, C, X, seed=31, noise_std=0.01)
+    b = ofdm.synth_frames(F, S, R, C, X, seed=32, noise_std=0.01)
+    ref = {0: two_launch(ofdm, a, X, 0), 1: two_launch(ofdm, b, X, 0)}
+    ws = ofdm.workspace(F, S, R, C, dev)
+    first = {}
+    for i in range(8):
+        o = ofdm.frame_demod(a if i % 2 == 0 else b, X, 0, ws=ws)
+        parity(host(o), ref[i % 2])
+        if i < 2:
+            first[i] = o
+        else:
+            assert torch.equal(o, first[i % 2])
+
+
+@pytest.mark.parametrize("C,F,R", [(2048, 40, 4), (4096, 16, 4)])
+def test_work_tickets_wide_receivers_vs_freq_path(ofdm, dev, C, F, R):
+    """The C = 2048 / 4096 receivers with work tickets active (more blocks
+    than the static first round) against the frequency-domain LS + MRC on
+    the same frames (fft_rows, then ofdm_frame_demod_freq: other kernels,
+    pinned to the oracle in test_gpu_parity.py)."""
+    S = 101
+    X = pilots(dev, C - 1, seed=C)
+    iq = ofdm.synth_frames(F, S, R, C, X, seed=C + F, noise_std=0.01)
+    got = host(ofdm.frame_demod(iq, X, 0))
+    Y = ofdm.fft_rows(iq.clone())
+    ref = host(ofdm.frame_demod_freq(Y, X))
+    parity(got, ref)
+
+
+@pytest.mark.parametrize("F", [41, 52, 66, 100, 131, 300])
+def test_work_tickets_cover_every_unit(ofdm, dev, F):
+    """Batch sizes around and beyond the static first round (512 blocks):
+    every ticketed block and half unit must be processed exactly once (a
+    grid smaller than the unit count would leave outputs unwritten: the
+    output buffer is NaN-filled first, so a missed unit fails the finite
+    check in parity)."""
+    import torch
+    S, R, C = 101, 2, 1024
+    X = pilots(dev, C - 1, seed=F)
+    iq = ofdm.synth_frames(F, S, R, C, X, seed=F, noise_std=0.01)
+    out = ofdm.c64((F, S - 1, C - 1), dev)
+    out.fill_(float("nan"))
+    ofdm.frame_demod(iq, X, 0, out=out)
+    parity(host(out), two_launch(ofdm, iq, X, 0))
