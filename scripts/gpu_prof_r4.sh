@@ -17,7 +17,7 @@ echo "$ARGS" > "$OUT/args.txt"
 timeout -k 10 300 python3 "$ROOT/scripts/clock_sampler.py" "$OUT/clock_unprofiled.jsonl" -- \
   python3 "$ROOT/bench.py" $ARGS > "$OUT/bench_unprofiled.json" 2> "$OUT/bench_unprofiled.err" || { tail "$OUT/bench_unprofiled.err"; exit 1; }
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run \
-  -- python3 "$ROOT/bench.py" $ARGS > "$OUT/bench_trace.json" 2> "$OUT/bench_trace.err" || { tail "$OUT/bench_trace.err"; exit 1; }
+  -- python3 "$ROOT/bench.py" $ARGS --no-box > "$OUT/bench_trace.json" 2> "$OUT/bench_trace.err" || { tail "$OUT/bench_trace.err"; exit 1; }
 PMC_ARGS="$ARGS --no-cpu --no-mode-a --no-box"
 for ctr in FETCH_SIZE WRITE_SIZE "GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU SQ_INSTS_LDS"; do
   name=$(echo $ctr | cut -d' ' -f1)

@@ -34,13 +34,14 @@ for st in "$@"; do
     split) bench split 300 --mode split --no-cpu; rc=$? ;;
     freq) bench freq 300 --mode freq --no-cpu; rc=$? ;;
     prof_default) timeout -k 10 1000 bash scripts/gpu_prof_r4.sh ${TAG}_default > $OUT/prof_default.log 2>&1; rc=$?; echo "prof_default rc=$rc"; tail -3 $OUT/prof_default.log ;;
-    prof_cfg1) timeout -k 10 600 bash scripts/gpu_prof_r4.sh ${TAG}_cfg1 --gpus 1 --steps 20 --warmup 5 --R 16 --frames 100 --no-box > $OUT/prof_cfg1.log 2>&1; rc=$?; echo "prof_cfg1 rc=$rc"; tail -3 $OUT/prof_cfg1.log ;;
-    prof_c4096) timeout -k 10 800 bash scripts/gpu_prof_r4.sh ${TAG}_c4096 --gpus 1 --steps 20 --warmup 5 --R 32 --C 4096 --frames 400 --no-box > $OUT/prof_c4096.log 2>&1; rc=$?; echo "prof_c4096 rc=$rc"; tail -3 $OUT/prof_c4096.log ;;
+    prof_cfg1) timeout -k 10 600 bash scripts/gpu_prof_r4.sh ${TAG}_cfg1 --gpus 1 --steps 20 --warmup 5 --R 16 --frames 100 > $OUT/prof_cfg1.log 2>&1; rc=$?; echo "prof_cfg1 rc=$rc"; tail -3 $OUT/prof_cfg1.log ;;
+    prof_c4096) timeout -k 10 800 bash scripts/gpu_prof_r4.sh ${TAG}_c4096 --gpus 1 --steps 20 --warmup 5 --R 32 --C 4096 --frames 400 > $OUT/prof_c4096.log 2>&1; rc=$?; echo "prof_c4096 rc=$rc"; tail -3 $OUT/prof_c4096.log ;;
     clk_cfg1) for g in 0 9; do timeout -k 10 200 python -u scripts/dispatch_clock.py --R 16 --frames 100 --steps 20 --warmup 5 --gap-ms $g --tag cfg1_gap$g >> $OUT/clk_cfg1.jsonl 2>> $OUT/clk.err || { rc=1; break; }; done
               timeout -k 10 200 python -u scripts/dispatch_clock.py --R 16 --frames 100 --steps 200 --warmup 5 --tag cfg1_200 >> $OUT/clk_cfg1.jsonl 2>> $OUT/clk.err; rc=$?
               echo "clk_cfg1 rc=$rc"; grep summary $OUT/clk_cfg1.jsonl ;;
     clk_default) timeout -k 10 300 python -u scripts/dispatch_clock.py --R 64 --frames 1250 --steps 20 --warmup 5 --gap-ms 9 --tag default >> $OUT/clk_default.jsonl 2>> $OUT/clk.err; rc=$?
               echo "clk_default rc=$rc"; grep summary $OUT/clk_default.jsonl ;;
+    prof_split) timeout -k 10 800 bash scripts/gpu_prof_r4.sh ${TAG}_split --gpus 1 --steps 20 --warmup 5 --mode split > $OUT/prof_split.log 2>&1; rc=$?; echo "prof_split rc=$rc"; tail -3 $OUT/prof_split.log ;;
     abx:*) a=${st#abx:}; timeout -k 10 600 python -u scripts/abx.py ${a//:/ } > $OUT/abx_$(echo $a | tr -c 'a-zA-Z0-9' _).jsonl 2> $OUT/abx.err; rc=$?; echo "abx $a rc=$rc"; tail -8 $OUT/abx_$(echo $a | tr -c 'a-zA-Z0-9' _).jsonl ;;
     *) echo "unknown step $st"; rc=2 ;;
   esac

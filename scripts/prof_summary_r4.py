@@ -65,7 +65,7 @@ def dominant(bench):
 
 def main():
     src, tag = sys.argv[1], sys.argv[2]
-    prof = os.path.join(ROOT, "profiles", "r4")
+    prof = os.path.join(ROOT, "profiles", tag[:2] if tag[:1] == "r" and tag[1:2].isdigit() else "r4")
     os.makedirs(prof, exist_ok=True)
     args = open(os.path.join(src, "args.txt")).read().strip()
     unprof = last_json(os.path.join(src, "bench_unprofiled.json"))
@@ -143,7 +143,7 @@ def main():
                                     "flow": cfg.get("flow", "two-launch")},
              "mrc_kernel": kern, "mrc_hbm_bytes_per_launch": hbm, "mrc_algorithmic_bytes_per_launch": alg,
              "mrc_avg_ns_rocprof": avg_ns, "correction": out["correction"],
-             "source": f"profiles/r4/{tag}_pmc.json"}
+             "source": os.path.relpath(os.path.join(prof, f"{tag}_pmc.json"), ROOT)}
         with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as fp:
             json.dump(t, fp, indent=1)
     md = [f"# Profile {tag}", "",

@@ -237,6 +237,27 @@ def test_bench_gpus2_launches_two_ranks_itself():
     line = _line(_bench(["--gpus", "2", "--frames", "24", "--steps", "2", "--warmup", "1", "--no-cpu"], True))
     assert line["n_gpus"] == 2 and line["config"]["global_data_symbols"] == 2 * 24 * 100
     assert line["check"]["qpsk_symbol_errors"] == 0 and line["check"]["timed_equals_warmup"] is True
+    # per-rank spread of the step and kernel times
+    pr = line["per_rank"]
+    for k in ("step_ms", "kernel_ms"):
+        assert 0 < pr[k]["min"] <= pr[k]["max"], pr
+
+
+@pytest.mark.timeout(400)
+def test_bench_split_rccl_world1_stage_times():
+    """bench.py --mode split on RCCL (world 1, the product collective path):
+    the line carries stages_ms -- the partial LS / FFT+MRC / finalise times,
+    the communication left exposed by the overlap, and the collectives timed
+    alone -- and the exposed time is within the step."""
+    line = _line(_bench(["--mode", "split", "--frames", "8", "--chunk", "2", "--steps", "2", "--warmup", "1",
+                         "--no-cpu"], False))
+    st = line["stages_ms"]
+    assert st["collective_path"] == "device (RCCL)"
+    for k in ("ls_partial", "mrc_partial", "exposed_comm", "finalize", "step_events_ms", "all_reduce_alone_per_chunk",
+              "reduce_scatter_alone_per_chunk", "collectives_alone_step"):
+        assert k in st and st[k] >= 0, (k, st)
+    assert st["exposed_comm"] <= st["step_events_ms"], st
+    assert line["check"]["qpsk_symbol_errors"] == 0
 
 
 @pytest.mark.timeout(200)
