@@ -38,16 +38,28 @@ def last_json(path):
     return json.loads(lines[-1]) if lines else None
 
 
+BIG_ONLY = False  # split mode: only the whole-batch launches (>= half the longest) of the dominant kernel
+
+
 def counters(path):
     """{kernel: {counter: [values per dispatch]}}, {kernel: [durations ns]}"""
-    vals = defaultdict(lambda: defaultdict(list))
+    per = defaultdict(lambda: defaultdict(lambda: defaultdict(float)))
     dur = defaultdict(dict)
     with open(path) as fp:
         for row in csv.DictReader(fp):
             k = short(row["Kernel_Name"])
-            vals[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
+            per[k][row["Dispatch_Id"]][row["Counter_Name"]] += float(row["Counter_Value"])
             dur[k][row["Dispatch_Id"]] = int(row["End_Timestamp"]) - int(row["Start_Timestamp"])
-    return vals, {k: list(v.values()) for k, v in dur.items()}
+    vals = defaultdict(lambda: defaultdict(list))
+    durs = {}
+    for k, d in dur.items():
+        cut = 0.5 * max(d.values()) if BIG_ONLY else -1
+        keep = [i for i in d if d[i] >= cut]
+        for i in keep:
+            for c, v in per[k][i].items():
+                vals[k][c].append(v)
+        durs[k] = [d[i] for i in keep]
+    return vals, durs
 
 
 def dominant(bench):
@@ -72,6 +84,8 @@ def main():
     traced = last_json(os.path.join(src, "bench_trace.json"))
     kern = dominant(traced)
     cfg = traced["config"]
+    global BIG_ONLY
+    BIG_ONLY = "R_total" in cfg
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(prof, f"{tag}_kernel_stats.csv"))
     with open(os.path.join(src, "trace", "run_kernel_stats.csv")) as fp:
         stats = list(csv.DictReader(fp))
@@ -81,6 +95,8 @@ def main():
         for row in csv.DictReader(fp):
             if short(row["Kernel_Name"]).startswith(kern):
                 durs.append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
+    if BIG_ONLY and durs:  # the pipeline's per-chunk launches are not the roofline kernel's
+        durs = [d for d in durs if d >= 0.5 * max(durs)]
     with open(os.path.join(prof, f"{tag}_dispatches.csv"), "w", newline="") as fp:
         w = csv.writer(fp)
         w.writerow(["dispatch", "kernel", "ns"])
