@@ -275,7 +275,7 @@ def clock_probe(step_diag, tag, ofdm, torch, stream, reps=3, save=None):
             e1.synchronize()
             ts.append(e0.elapsed_time(e1))
     nwg = 1 << 20  # diag::MAX_WG (the last launch's records may sit in any slot; the buffer was cleared before it)
-    rec = np.zeros((nwg, 8), dtype=np.uint64)
+    rec = np.zeros((nwg, 12), dtype=np.uint64)  # diag::WORDS
     if read(rec.ctypes.data, nwg) != 0:
         return None
     if save:

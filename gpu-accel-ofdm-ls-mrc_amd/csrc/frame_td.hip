@@ -336,8 +336,9 @@ k_mrc_td1024_hlds(const float2 *__restrict__ iq, int S, int R, int prefix, const
 __device__ __forceinline__ void hlds_ls_frame(const float2 *__restrict__ iq, int S, int R, int prefix,
                                               const float2 *__restrict__ X, float2 *Hc, float *P, long long f,
                                               int w, int t, float2 *T, float2 *T0, const float2 *tw1,
-                                              const float2 *tw2) {
+                                              const float2 *tw2, unsigned long long *mx = nullptr) {
     using namespace hlds;
+    (void)mx;  // diagnostic build: phase stamps
     const int Cp = C + prefix;
     const float2 *pilot = iq + f * (long long)S * R * Cp + prefix;
     float4 *Hf = reinterpret_cast<float4 *>(Hc + f * (long long)R * C);
@@ -366,7 +367,11 @@ __device__ __forceinline__ void hlds_ls_frame(const float2 *__restrict__ iq, int
         // hc_store's layout, write-through (sc1): visible at agent scope once vmcnt drains
 #pragma unroll
         for (int i = 0; i < 8; ++i) store16_wt(Hf, R * C * 8, (r * (C / 2) + i * 64 + t) * 16, x[2 * i], x[2 * i + 1]);
+        if (r == w) {
+            OFDM_DIAG_MARKP(mx, 1)
+        }
     }
+    OFDM_DIAG_MARKP(mx, 2)
     __syncthreads();  // every wave is done with its transpose image
     float *pp = reinterpret_cast<float *>(T0);  // [WAVES][C], over the images
 #pragma unroll
@@ -380,6 +385,7 @@ __device__ __forceinline__ void hlds_ls_frame(const float2 *__restrict__ iq, int
         const float v = b == 0 ? 1.f : sum;
         store4_wt(Pf + b, v);
     }
+    OFDM_DIAG_MARKP(mx, 3)
     __syncthreads();  // pp (the transpose images) read before they are reused
 }
 
@@ -474,6 +480,7 @@ k_demod_td1024(const float2 *__restrict__ iq, int S, int R, int prefix, const fl
         if (e0 >= nframes) return;
         fill(tw1, tw2);
         __syncthreads();
+        OFDM_DIAG_MARKN(0)
     } else {
         lb = wg_take_unit(tickets, par, nblocks, k0, (long long)blockIdx.x - nls, split,
                           reinterpret_cast<long long *>(hfree + 255));
@@ -491,7 +498,8 @@ k_demod_td1024(const float2 *__restrict__ iq, int S, int R, int prefix, const fl
             e1 = fl;
         }
     }
-    for (long long ff = e0; ff <= e1; ++ff) hlds_ls_frame(iq, S, R, prefix, X, Hc, P, ff, w, t, T, T0, tw1, tw2);
+    for (long long ff = e0; ff <= e1; ++ff)
+        hlds_ls_frame(iq, S, R, prefix, X, Hc, P, ff, w, t, T, T0, tw1, tw2, OFDM_DIAG_ARG);
     if (estimator) {
         OFDM_DIAG_MARK()
         publish_flag(flags + e0, epoch);

@@ -72,13 +72,16 @@ for i in range(a.steps):
 torch.cuda.synchronize()
 ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(a.steps)]
 errs = int(ofdm.count_symbol_errors(out, S, seed=1234).item())
-rec = np.zeros((1 << 20, 8), dtype=np.uint64)
+rec = np.zeros((1 << 20, 12), dtype=np.uint64)  # diag::WORDS
 assert read(rec.ctypes.data, 1 << 20) == 0
-slots = rec.reshape(32, -1, 8)
+slots = rec.reshape(32, -1, 12)
 runs = []
 for sl in slots:
     r = sl[sl[:, 2] > 0]
     if len(r):
+        # only the slot's latest launch (word 7's high half = launch counter)
+        r = r[(r[:, 7] >> 32) == (r[:, 7] >> 32).max()]
+        r[:, 7] &= 0xFFFFFFFF
         runs.append((int(r[:, 0].min()), r))
 runs.sort(key=lambda x: x[0])
 # the last len(runs) timed dispatches, in order

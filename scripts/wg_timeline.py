@@ -25,7 +25,7 @@ def analyse(rec, nls=0):
     mk = (rec[:, 1] - t0) * 1e-2
     en = (rec[:, 2] - t0) * 1e-2
     ghz = (rec[:, 4] - rec[:, 3]) / np.maximum(rec[:, 2] - rec[:, 0], 1) * 0.1
-    blk = rec[:, 7]
+    blk = rec[:, 7] & 0xFFFFFFFF
     span = en.max()
     res = {"workgroups": int(len(rec)), "span_us": float(span)}
     roles = {"all": np.ones(len(rec), bool)}

@@ -84,9 +84,9 @@ def test_stamps_summary_clock():
     spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
     bench = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(bench)
-    rec = np.zeros((4, 8), dtype=np.uint64)
+    rec = np.zeros((4, 12), dtype=np.uint64)
     for i in range(3):
-        rec[i] = [1000 + i, 1100 + i, 2000 + i, 50000, 50000 + 20 * 1000, 0, i, i]
+        rec[i] = [1000 + i, 1100 + i, 2000 + i, 50000, 50000 + 20 * 1000, 0, i, i, 0, 0, 0, 0]
     st = bench.stamps_summary(rec)  # the empty 4th record is ignored
     assert st["workgroups"] == 3
     assert abs(st["effective_GHz_median"] - 2.0) < 1e-9
