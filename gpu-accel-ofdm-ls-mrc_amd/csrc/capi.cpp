@@ -117,28 +117,45 @@ struct Workspace {
     float2 *Hc;                 // [F][R][C] bin layout
     float *P;                   // [F][C]   bin layout
     unsigned long long *flags;  // [F] per-frame estimate flags of the one-launch demod
-    unsigned long long *tickets;  // 8 work-ticket counters, 128 B apart (wave_fft1024.hpp take_block)
+    unsigned long long *tickets;  // 4 sets of 8 work-ticket counters, 128 B apart (wave_fft1024.hpp take_block)
     float2 *staging;            // [chunk][S][R][C] (non-fused C only)
     long long chunk;
 };
 
-constexpr size_t TICKET_BYTES = 2 * 8 * 128;  // two sets of 8 counters, one 128-B line each
+constexpr size_t TICKET_SET_BYTES = 8 * 128;         // 8 counters, one 128-B line each
+constexpr size_t TICKET_BYTES = 4 * TICKET_SET_BYTES;  // sets 0 / 1: eager launches; 2 (3): captured ones
 
 // Work-ticket counter sets of a workspace (wave_fft1024.hpp, take_block): a
-// launch counts in set `par` and zeroes the other set for the next launch on
+// launch counts in set `par` and zeroes set par ^ 1 for the next launch on
 // the same workspace; the host keeps `par` per workspace, flips it per
 // launch, and zeroes both sets the first time it meets the workspace (and
 // again after ofdm_workspace_release).  Launches on one workspace are
 // ordered (one stream, as the estimate they share already requires).  A
 // workspace used by two library instances in turn must be released by one
 // before the other uses it, as for its estimate.
+// Under stream capture the parity would be frozen in the graph and every
+// replay would count in a set the previous replay left non-zero: a captured
+// launch counts in set 2 instead, behind a zeroing kernel node of its own
+// (so every replay starts from zero; a captured hipMemsetAsync node replayed
+// with a wrong value here), and zeroes set 3, which nothing reads; the eager
+// sets 0 / 1 and their host parity are untouched, so graphs and eager
+// launches on the same workspace may alternate.
 std::mutex g_tk_mu;
 std::map<const void *, int> g_tk_par;
 hipError_t tickets_next(const void *ws, unsigned long long *tickets, hipStream_t s, int *par) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipError_t e = hipStreamIsCapturing(s, &st); e != hipSuccess) return e;
+    if (st != hipStreamCaptureStatusNone) {
+        if (hipError_t e = ofdm::launch_zero_words(tickets + 2 * TICKET_SET_BYTES / 8, (int)(TICKET_SET_BYTES / 8), s);
+            e != hipSuccess)
+            return e;
+        *par = 2;
+        return hipSuccess;
+    }
     std::lock_guard<std::mutex> lock(g_tk_mu);
     auto it = g_tk_par.find(ws);
     if (it == g_tk_par.end()) {
-        if (hipError_t e = hipMemsetAsync(tickets, 0, TICKET_BYTES, s); e != hipSuccess) return e;
+        if (hipError_t e = hipMemsetAsync(tickets, 0, 2 * TICKET_SET_BYTES, s); e != hipSuccess) return e;
         it = g_tk_par.emplace(ws, 1).first;
     }
     it->second ^= 1;

@@ -150,6 +150,7 @@ hipError_t launch_combine(const float2 *prod, long long nsyms, int R, int K, con
                           int rotate, float2 *out, hipStream_t s);
 hipError_t launch_shift_rows(const float2 *in, long long nrows, int K, float2 *out, hipStream_t s);
 hipError_t launch_hash_words(const void *d, long long nwords, unsigned long long *h, hipStream_t s);
+hipError_t launch_zero_words(unsigned long long *p, int n, hipStream_t s);
 hipError_t launch_dist_sqrd(const float2 *H, int R, int K, float *P, hipStream_t s);
 // One frame's workspace estimate (Hc rows of C float2: lane_order = the
 // fused LS kernel for C wrote them, else bin layout; P bin-indexed) ->

@@ -182,8 +182,22 @@ __global__ void __launch_bounds__(256) k_hash_words(const unsigned *__restrict__
     if ((threadIdx.x & 63) == 0) atomicAdd(h, acc);
 }
 
+// n 64-bit words of zeros (one vector store per thread): the capture counter
+// set of the work tickets, as a kernel node -- a memset node captured by
+// hipMemsetAsync replayed with a wrong value on ROCm 7.2 (the second replay
+// found the set filled with a pointer-like constant, scripts/r5/capture_debug.py)
+__global__ void __launch_bounds__(256) k_zero_words(unsigned long long *p, int n) {
+    const int i = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (i < n) p[i] = 0ull;
+}
+hipError_t launch_zero_words(unsigned long long *p, int n, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_zero_words, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_hash_words(const void *d, long long nwords, unsigned long long *h, hipStream_t s) {
-    if (hipError_t e = hipMemsetAsync(h, 0, sizeof(*h), s); e != hipSuccess) return e;
+    if (hipError_t e = launch_zero_words(h, 1, s); e != hipSuccess) return e;  // capturable (see above)
     if (nwords <= 0) return hipSuccess;
     long long blocks = (nwords + 255) / 256;
     if (blocks > 1024) blocks = 1024;

@@ -141,10 +141,11 @@ def test_product_library_dispatches_only_product_kernels(ofdm):
 
 def test_workspace_sizes(ofdm):
     # fused C=1024: Hc [F][R][C] + P [F][C] + one flag word per frame + the
-    # two sets of 8 work-ticket counters (one 128-B line each), no staging
+    # four sets of 8 work-ticket counters (one 128-B line each: two for eager
+    # launches, one (+ the one it zeroes) for launches captured into graphs), no staging
     F, S, R, C = 100, 101, 16, 1024
     b = ofdm.workspace_bytes(F, S, R, C)
-    assert b == F * R * C * 8 + F * C * 4 + (F * 8 + 255) // 256 * 256 + 2 * 8 * 128
+    assert b == F * R * C * 8 + F * C * 4 + (F * 8 + 255) // 256 * 256 + 4 * 8 * 128
     # non-fused C carries a bounded staging buffer (<= 256 MiB or one frame)
     b2 = ofdm.workspace_bytes(F, S, 64, 2048)
     assert b2 - (F * 64 * 2048 * 8 + F * 2048 * 4) <= max(256 << 20, S * 64 * 2048 * 8) + 512 + 2048

@@ -252,3 +252,40 @@ def test_work_tickets_cover_every_unit(ofdm, dev, F):
     out.fill_(float("nan"))
     ofdm.frame_demod(iq, X, 0, out=out)
     parity(host(out), two_launch(ofdm, iq, X, 0))
+
+
+@pytest.mark.parametrize("C,F,R", [(2048, 64, 4), (4096, 16, 4)])
+def test_graph_capture_ticketed_receivers(ofdm, dev, C, F, R):
+    """The work-ticketed C = 2048 / 4096 receivers captured into a graph:
+    every replay counts in the capture counter set behind a zeroing kernel
+    node of its own, so replays after the first, and eager launches on the same
+    workspace in between, still process every unit (outputs NaN-filled
+    before each run; bit-identical to eager launches on a fresh workspace)."""
+    import torch
+    S = 101
+    X = pilots(dev, C - 1, seed=C + 1)
+    src = [ofdm.synth_frames(F, S, R, C, X, seed=C + k, noise_std=0.01) for k in (1, 2)]
+    ref = [ofdm.frame_demod(a, X, 0) for a in src]
+    torch.cuda.synchronize()
+    iq = src[0].clone()
+    ws = ofdm.workspace(F, S, R, C, dev)
+    out = ofdm.c64((F, S - 1, C - 1), dev)
+    eager = ofdm.c64((F, S - 1, C - 1), dev)
+    st = torch.cuda.Stream()
+    ofdm.frame_demod(iq, X, 0, ws=ws, out=eager, stream=st)  # warm, outside capture
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=st):
+        ofdm.frame_demod(iq, X, 0, ws=ws, out=out, stream=st)
+    for k in (1, 0, 1, 1, 0):
+        iq.copy_(src[k])
+        out.fill_(float("nan"))
+        eager.fill_(float("nan"))
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref[k])
+        with torch.cuda.stream(st):
+            ofdm.frame_demod(iq, X, 0, ws=ws, out=eager, stream=st)
+        torch.cuda.synchronize()
+        assert torch.equal(eager, ref[k])
