@@ -140,8 +140,16 @@ constexpr size_t TICKET_BYTES = 4 * TICKET_SET_BYTES;  // sets 0 / 1: eager laun
 // with a wrong value here), and zeroes set 3, which nothing reads; the eager
 // sets 0 / 1 and their host parity are untouched, so graphs and eager
 // launches on the same workspace may alternate.
+// The counters' offset in the workspace depends on the batch geometry (they
+// follow the estimate), so the host also keeps where they were: a call with
+// another geometry on the same workspace (whose estimate may have written
+// over the old counters' place) zeroes both sets again.
+struct TkState {
+    const void *at;  // the counters' address at the last launch
+    int par;
+};
 std::mutex g_tk_mu;
-std::map<const void *, int> g_tk_par;
+std::map<const void *, TkState> g_tk_par;
 hipError_t tickets_next(const void *ws, unsigned long long *tickets, hipStream_t s, int *par) {
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     if (hipError_t e = hipStreamIsCapturing(s, &st); e != hipSuccess) return e;
@@ -154,12 +162,12 @@ hipError_t tickets_next(const void *ws, unsigned long long *tickets, hipStream_t
     }
     std::lock_guard<std::mutex> lock(g_tk_mu);
     auto it = g_tk_par.find(ws);
-    if (it == g_tk_par.end()) {
+    if (it == g_tk_par.end() || it->second.at != tickets) {
         if (hipError_t e = hipMemsetAsync(tickets, 0, 2 * TICKET_SET_BYTES, s); e != hipSuccess) return e;
-        it = g_tk_par.emplace(ws, 1).first;
+        it = g_tk_par.insert_or_assign(ws, TkState{tickets, 1}).first;
     }
-    it->second ^= 1;
-    *par = it->second;
+    it->second.par ^= 1;
+    *par = it->second.par;
     return hipSuccess;
 }
 void tickets_forget(const void *ws) {

@@ -289,3 +289,26 @@ def test_graph_capture_ticketed_receivers(ofdm, dev, C, F, R):
             ofdm.frame_demod(iq, X, 0, ws=ws, out=eager, stream=st)
         torch.cuda.synchronize()
         assert torch.equal(eager, ref[k])
+
+
+@pytest.mark.parametrize("C,Fbig,Fsmall", [(1024, 100, 60), (4096, 16, 12)])
+def test_work_tickets_workspace_shared_by_two_geometries(ofdm, dev, C, Fbig, Fsmall):
+    """One workspace (sized for the larger batch) used in turn by batches of
+    two sizes: the work-ticket counters follow the estimate, at an offset that
+    depends on the batch, and the smaller batch's counters lie inside the
+    larger batch's estimate, so a call with the other geometry must zero them
+    again (NaN-filled outputs; bit-identical to fresh workspaces)."""
+    import torch
+    S, R = 101, 2
+    X = pilots(dev, C - 1, seed=7)
+    big = ofdm.synth_frames(Fbig, S, R, C, X, seed=71, noise_std=0.01)
+    small = ofdm.synth_frames(Fsmall, S, R, C, X, seed=72, noise_std=0.01)
+    ref = [ofdm.frame_demod(big, X, 0), ofdm.frame_demod(small, X, 0)]
+    ws = ofdm.workspace(Fbig, S, R, C, dev)
+    for k in (0, 1, 0, 1, 1, 0):
+        iq = (big, small)[k]
+        out = ofdm.c64((iq.shape[0], S - 1, C - 1), dev)
+        out.fill_(float("nan"))
+        ofdm.frame_demod(iq, X, 0, ws=ws, out=out)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref[k])
