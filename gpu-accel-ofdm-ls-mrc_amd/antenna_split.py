@@ -8,7 +8,8 @@ cfg5 256 antennas, 32 per GPU).  MRC is a sum over antennas, so
                                        cpuLS.hpp:187-208)
   out        = rotate(N / P)          (cpuLS.hpp:364-368, shiftOneRow 135-149)
 
-Data path per batch (one process per GPU, RCCL over xGMI):
+Data path per batch (one process per GPU, RCCL over xGMI; SplitPipeline
+runs step 1 once per batch and steps 3-5 in chunks):
   1. ofdm_frame_ls_partial     -> P_g, Hc_g (workspace)          local
   2. all_reduce(P)             F*K*4 B                           tiny
   3. ofdm_frame_mrc_partial    -> N_g (F*(S-1)*K complex)        local, HBM-bound
@@ -33,6 +34,7 @@ class HipOps:
     """The HIP library calls used by the antenna-split path."""
     ls_partial = staticmethod(ofdm_lsmrc.frame_ls_partial)        # (shard, X, prefix) -> (P, ws)
     mrc_partial = staticmethod(ofdm_lsmrc.frame_mrc_partial)      # (shard, ws, prefix) -> N
+    mrc_partial_range = staticmethod(ofdm_lsmrc.frame_mrc_partial_range)  # (shard, ws, prefix, f0, count) -> N
     mrc_finalize = staticmethod(ofdm_lsmrc.mrc_finalize)          # (chunk, e0, nsym, K, P, out)
 
 
@@ -86,14 +88,17 @@ class SplitPipeline:
     """Chunked, overlapped antenna-split LS + MRC for a fixed batch shape
     (bench.py --mode split).
 
-    The frames are cut into chunks of `chunk_frames`; per chunk, on the
-    caller's stream: partial LS -> async all_reduce(P) -> partial MRC ->
+    One partial LS over the whole batch (one launch: a workgroup per frame
+    fills the GPU, where per-chunk LS launches of `chunk_frames` workgroups
+    left most CUs idle) -> async all_reduce(P) of every frame; then the MRC
+    streams in chunks of `chunk_frames`, on the caller's stream: partial MRC
+    of chunk c (ofdm_frame_mrc_partial_range on the batch's estimate) ->
     async reduce_scatter(numerators); the collectives of chunk c run on the
     RCCL stream while chunk c+1 computes, and chunk c is finalised (divide +
     rotate of this rank's slice) once both have landed.  Buffers are
-    allocated once and double-buffered, so a step issues no allocation.
-    `ops` as for demod_antenna_split (the kernel calls take the preallocated
-    ws / P / num and the stream as keyword arguments).
+    allocated once (the numerators double-buffered), so a step issues no
+    allocation.  `ops` as for demod_antenna_split (the kernel calls take the
+    preallocated ws / P / num and the stream as keyword arguments).
     Each rank writes only its slices of `out` (see demod_antenna_split).
     """
 
@@ -110,9 +115,8 @@ class SplitPipeline:
         fc = self.chunk
         n = fc * (S - 1) * self.K
         self.per = -(-n // self.world)
-        self.ws = [ofdm_lsmrc.workspace(fc, S, R_local, C, device) if ops is HipOps else None
-                   for _ in range(2)]
-        self.P = [torch.empty((fc, self.K), dtype=torch.float32, device=device) for _ in range(2)]
+        self.ws = ofdm_lsmrc.workspace(F, S, R_local, C, device) if ops is HipOps else None
+        self.P = torch.empty((F, self.K), dtype=torch.float32, device=device)
         # numerators padded to world * per complex values (padding stays 0)
         self.num = [torch.zeros(self.per * self.world, dtype=torch.complex64, device=device)
                     for _ in range(2)]
@@ -164,23 +168,23 @@ class SplitPipeline:
             return sum(x.elapsed_time(y) for x, y in zip(ev.get(a, []), ev.get(b, [])))
         st = {"step_wall_ms": wall}
         if ev:
-            st.update({"ls_partial": span("ls0", "ls1"), "mrc_partial": span("ls1", "mrc1"),
+            st.update({"ls_partial": span("ls0", "ls1"), "mrc_partial": span("m0", "mrc1"),
                        "exposed_comm": span("w0", "w1"), "finalize": span("w1", "fin1"),
                        "step_events_ms": ev["ls0"][0].elapsed_time(ev["fin1"][-1])})
         # the collectives alone, on the last buffers used
         b = 0
         fc = min(self.chunk, self.F)
-        iso = {}
+        iso = {}  # (the all-reduce of one chunk's P, as the per-chunk form issued it)
         for name in ("all_reduce", "reduce_scatter"):
             if stream is not None:
                 torch.cuda.synchronize()
             t0 = time.perf_counter()
             if name == "all_reduce":
                 if self.host_coll:
-                    Ph = self.P[b][:fc].cpu()
+                    Ph = self.P[:fc].cpu()
                     dist.all_reduce(Ph, group=self.group)
                 else:
-                    dist.all_reduce(self.P[b][:fc], group=self.group)
+                    dist.all_reduce(self.P[:fc], group=self.group)
             else:
                 if self.host_coll:
                     mine_h = torch_real(self.mine[b]).cpu()
@@ -195,7 +199,7 @@ class SplitPipeline:
         st.update({"all_reduce_alone_per_chunk": iso["all_reduce"],
                    "reduce_scatter_alone_per_chunk": iso["reduce_scatter"],
                    "chunks": nchunks,
-                   "collectives_alone_step": (iso["all_reduce"] + iso["reduce_scatter"]) * nchunks,
+                   "collectives_alone_step": iso["all_reduce"] + iso["reduce_scatter"] * nchunks,
                    "collective_path": "host-staged (gloo rehearsal)" if self.host_coll else "device (RCCL)"})
         return st
 
@@ -204,6 +208,7 @@ class SplitPipeline:
         import torch.distributed as dist
         F, S, K = self.F, self.S, self.K
         pending = []
+        reduced = {"P": None}  # the async all-reduce of P, waited for once
 
         def mark(name):  # HIP events on the current stream (kernel stand-ins of the CPU tests: none)
             if timing is not None and self.ops is HipOps:
@@ -211,10 +216,12 @@ class SplitPipeline:
                 e.record()
                 timing.setdefault(name, []).append(e)
 
-        def finalize(c, b, wp, wn):
+        def finalize(c, b, wn):
             mark("w0")
-            if wp is not None:
-                wp.wait()
+            if reduced["P"] is not None:
+                reduced["P"].wait()
+                reduced["P"] = None
+            if wn is not None:
                 wn.wait()
             mark("w1")
             f0 = c * self.chunk
@@ -223,40 +230,39 @@ class SplitPipeline:
             e0 = min(self.rank * self.per, n)
             count = max(0, min(self.per, n - e0))
             if count:
-                self.ops.mrc_finalize(self.mine[b][:count], e0, S - 1, K, self.P[b][:fc],
+                self.ops.mrc_finalize(self.mine[b][:count], e0, S - 1, K, self.P[f0:f0 + fc],
                                       out[f0:f0 + fc], stream=stream)
             mark("fin1")
 
+        mark("ls0")
+        _, self.ws = self.ops.ls_partial(shard, X, self.prefix, ws=self.ws, P=self.P, stream=stream)
+        mark("ls1")
+        if self.host_coll:
+            Ph = self.P.cpu()
+            dist.all_reduce(Ph, group=self.group)
+            self.P.copy_(Ph)
+        else:
+            reduced["P"] = dist.all_reduce(self.P, group=self.group, async_op=True)
         nchunks = -(-F // self.chunk)
         for c in range(nchunks):
             b = c & 1
             f0 = c * self.chunk
             fc = min(self.chunk, F - f0)
-            part = shard[f0:f0 + fc]
-            P = self.P[b][:fc]
-            mark("ls0")
-            _, self.ws[b] = self.ops.ls_partial(part, X, self.prefix, ws=self.ws[b], P=P, stream=stream)
-            mark("ls1")
-            if self.host_coll:
-                Ph = P.cpu()
-                dist.all_reduce(Ph, group=self.group)
-                P.copy_(Ph)
-            else:
-                wp = dist.all_reduce(P, group=self.group, async_op=True)
             n = fc * (S - 1) * K
             num = self.num[b][:n].view(fc, S - 1, K)
-            self.ops.mrc_partial(part, self.ws[b], self.prefix, num=num, stream=stream)
+            mark("m0")
+            self.ops.mrc_partial_range(shard, self.ws, self.prefix, f0, fc, num=num, stream=stream)
             mark("mrc1")
             flat = self.num[b] if n == self.per * self.world else self._padded(b, n)
             if self.host_coll:
                 mine_h = torch_real(self.mine[b]).cpu()
                 dist.reduce_scatter_tensor(mine_h, torch_real(flat).cpu(), group=self.group)
                 torch_real(self.mine[b]).copy_(mine_h)
-                wp = wn = None
+                wn = None
             else:
                 wn = dist.reduce_scatter_tensor(torch_real(self.mine[b]), torch_real(flat),
                                                 group=self.group, async_op=True)
-            pending.append((c, b, wp, wn))
+            pending.append((c, b, wn))
             if len(pending) == 2:
                 finalize(*pending.pop(0))
         while pending:

@@ -654,6 +654,32 @@ int ofdm_frame_mrc_partial(const ofdm_cf32 *d_iq, long long nframes, int S, int 
     return td_staged(F2(d_iq), nframes, S, R, C, prefix, nullptr, w, F2(d_num), 1, s);
 }
 
+int ofdm_frame_mrc_partial_range(const ofdm_cf32 *d_iq, long long nframes, long long f0, long long count, int S,
+                                 int R, int C, int prefix, void *d_ws, size_t ws_bytes_, ofdm_cf32 *d_num,
+                                 ofdm_stream_t stream) {
+    static const char *fn = "ofdm_frame_mrc_partial_range";
+    if (nframes < 0 || f0 < 0 || count < 0 || f0 > nframes || count > nframes - f0)
+        return fail(OFDM_E_ARG, "%s: frames [%lld, %lld) outside [0, %lld)", fn, f0, f0 + count, nframes);
+    if (count == 0) return OFDM_OK;
+    int rc = check_frame_args(d_iq, nframes, S, R, C, prefix, d_num, fn);
+    if (rc) return rc;
+    WsTag tag;
+    if ((rc = ws_check(d_ws, ws_bytes_, nframes, S, R, C, false, fn, &tag))) return rc;
+    if (tag.lane_order != lane_c(C))
+        return fail(OFDM_E_ARG, "%s: the workspace holds a frequency-domain estimate, not the time-domain one of "
+                                "ofdm_frame_ls_partial / ofdm_frame_estimate", fn);
+    Workspace w;
+    if ((rc = carve(d_ws, ws_bytes_, nframes, S, R, C, !fused_c(C), w))) return rc;
+    hipStream_t s = hs(stream);
+    const float2 *iq = F2(d_iq) + f0 * (long long)S * R * (C + prefix);
+    Workspace v = w;  // the range's estimate: frames f0 .. in the same [F][R][C] / [F][C] layout
+    v.Hc += f0 * (long long)R * C;
+    v.P += f0 * C;
+    if (fused_c(C))
+        return hip_check(mrc_fused(iq, count, S, R, C, prefix, v.Hc, v.P, F2(d_num), 1, s, d_ws, w.tickets), fn);
+    return td_staged(iq, count, S, R, C, prefix, nullptr, v, F2(d_num), 1, s);
+}
+
 int ofdm_symbols_demod(const ofdm_cf32 *d_sym, long long nsym, int R, int C, int prefix, const void *d_ws,
                        size_t ws_bytes_, long long frame, ofdm_cf32 *d_out, ofdm_stream_t stream) {
     static const char *fn = "ofdm_symbols_demod";

@@ -56,6 +56,7 @@ _SIGS = {
     "ofdm_frame_demod_freq_mfma": (_I, [_P, _LL, _I, _I, _I, _P, _P, _c.c_size_t, _P, _P]),
     "ofdm_frame_ls_partial": (_I, [_P, _LL, _I, _I, _I, _I, _P, _P, _c.c_size_t, _P, _P]),
     "ofdm_frame_mrc_partial": (_I, [_P, _LL, _I, _I, _I, _I, _P, _c.c_size_t, _P, _P]),
+    "ofdm_frame_mrc_partial_range": (_I, [_P, _LL, _LL, _LL, _I, _I, _I, _I, _P, _c.c_size_t, _P, _P]),
     "ofdm_frame_export_estimate": (_I, [_P, _c.c_size_t, _LL, _I, _I, _I, _LL, _P, _P, _P]),
     "ofdm_symbols_demod": (_I, [_P, _LL, _I, _I, _I, _P, _c.c_size_t, _LL, _P, _P]),
     "ofdm_synth_frames": (_I, [_P, _LL, _I, _I, _I, _I, _P, _c.c_ulonglong, _LL, _c.c_float,
@@ -409,6 +410,18 @@ def frame_mrc_partial(iq, ws, prefix=0, num=None, stream=None):
         num = c64((F, S - 1, C - 1), iq.device)
     _check(lib().ofdm_frame_mrc_partial(_dptr(iq), F, S, R, C, prefix, _dptr(ws), ws.numel(),
                                         _dptr(num), _stream(stream)), "ofdm_frame_mrc_partial")
+    return num
+
+
+def frame_mrc_partial_range(iq, ws, prefix, f0, count, num=None, stream=None):
+    """Partial MRC numerators of frames [f0, f0 + count) of the batch `iq`
+    whose estimate one frame_ls_partial call left in `ws`."""
+    F, S, R, Cp = iq.shape
+    C = Cp - prefix
+    if num is None:
+        num = c64((count, S - 1, C - 1), iq.device)
+    _check(lib().ofdm_frame_mrc_partial_range(_dptr(iq), F, f0, count, S, R, C, prefix, _dptr(ws), ws.numel(),
+                                              _dptr(num), _stream(stream)), "ofdm_frame_mrc_partial_range")
     return num
 
 

@@ -267,6 +267,14 @@ int ofdm_frame_ls_partial(const ofdm_cf32 *d_iq, long long nframes, int S, int R
 int ofdm_frame_mrc_partial(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int C,
                            int cp_len, void *d_ws, size_t ws_bytes, ofdm_cf32 *d_num,
                            ofdm_stream_t stream);
+/* ofdm_frame_mrc_partial for frames [f0, f0 + count) of a batch of nframes
+ * whose estimate ONE ofdm_frame_ls_partial call put in d_ws (no reference
+ * counterpart: the pipelined antenna split estimates the whole batch in one
+ * launch and streams the MRC in chunks).  d_iq is the whole batch, d_num
+ * [count][S-1][K].  OFDM_E_ARG for a range outside [0, nframes). */
+int ofdm_frame_mrc_partial_range(const ofdm_cf32 *d_iq, long long nframes, long long f0, long long count, int S,
+                                 int R, int C, int cp_len, void *d_ws, size_t ws_bytes, ofdm_cf32 *d_num,
+                                 ofdm_stream_t stream);
 
 /* ---------------------------------------------------- streaming ingest --- */
 

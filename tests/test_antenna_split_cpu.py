@@ -52,6 +52,10 @@ class NumpyOps:
         return num
 
     @staticmethod
+    def mrc_partial_range(shard, Hc, prefix, f0, count, num=None, stream=None):
+        return NumpyOps.mrc_partial(shard[f0:f0 + count], Hc[f0:f0 + count], prefix, num=num, stream=stream)
+
+    @staticmethod
     def mrc_finalize(chunk, e0, nsym, K, P, out, stream=None):
         c = chunk.numpy()
         e = e0 + np.arange(c.size)

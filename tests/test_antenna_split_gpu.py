@@ -99,6 +99,16 @@ class HipOpsViaHost:
         return num
 
     @staticmethod
+    def mrc_partial_range(shard, ws, prefix, f0, count, num=None, stream=None):
+        import ofdm_lsmrc
+        sd, wsd = HipOpsViaHost._ws
+        N = ofdm_lsmrc.frame_mrc_partial_range(sd, wsd, prefix, f0, count).cpu()
+        if num is None:
+            return N
+        num.copy_(N)
+        return num
+
+    @staticmethod
     def mrc_finalize(chunk, e0, nsym, K, P, out, stream=None):
         import ofdm_lsmrc
         od = out.cuda()
@@ -283,3 +293,28 @@ def test_bench_split_eight_ranks_share_gpu():
     assert line["n_gpus"] == 8 and line["config"]["R_total"] == 256 and line["config"]["C"] == 4096
     chk = line["check"]
     assert chk["qpsk_symbol_errors"] == 0 and chk["vs_full_receiver"]["ok"], chk
+
+
+@pytest.mark.parametrize("C,F,S,R,prefix", [(4096, 9, 11, 4, 0), (1024, 7, 13, 3, 8), (2048, 6, 9, 2, 0),
+                                            (1536, 5, 7, 2, 0)])
+def test_mrc_partial_range_matches_chunk_workspaces(ofdm, dev, C, F, S, R, prefix):
+    """ofdm_frame_mrc_partial_range (the pipelined split's MRC over one batch
+    estimate) against ofdm_frame_ls_partial + ofdm_frame_mrc_partial on each
+    chunk alone: the same kernels on the same frames, so bit-identical; a
+    range outside the batch is refused."""
+    import torch
+    rng = np.random.default_rng(C + F)
+    a = np.float32(0.70710678)
+    X = torch.from_numpy((rng.choice([-a, a], C - 1) + 1j * rng.choice([-a, a], C - 1))
+                         .astype(np.complex64)).to(dev)
+    iq = ofdm.synth_frames(F, S, R, C, X, prefix=prefix, seed=C + 3, noise_std=0.02)
+    _, ws = ofdm.frame_ls_partial(iq, X, prefix)
+    for f0, cnt in ((0, 2), (2, 3), (5, F - 5), (0, F)):
+        got = ofdm.frame_mrc_partial_range(iq, ws, prefix, f0, cnt)
+        part = iq[f0:f0 + cnt].contiguous()
+        _, wsc = ofdm.frame_ls_partial(part, X, prefix)
+        ref = ofdm.frame_mrc_partial(part, wsc, prefix)
+        torch.cuda.synchronize()
+        assert torch.equal(got, ref), (f0, cnt)
+    with pytest.raises(ofdm.OfdmError, match="outside"):
+        ofdm.frame_mrc_partial_range(iq, ws, prefix, F - 1, 2)
