@@ -312,3 +312,30 @@ def test_work_tickets_workspace_shared_by_two_geometries(ofdm, dev, C, Fbig, Fsm
         ofdm.frame_demod(iq, X, 0, ws=ws, out=out)
         torch.cuda.synchronize()
         assert torch.equal(out, ref[k])
+
+
+def test_two_streams_two_workspaces_concurrently(ofdm, dev):
+    """Two batches on two streams with a workspace each, enqueued in turn
+    without host synchronisation (the one-launch kernels may run at the same
+    time: each one's flags, epochs and work-ticket counters are its own);
+    every output equals the serial run's (NaN-filled outputs)."""
+    import torch
+    S, R, C = 101, 4, 1024
+    X = pilots(dev, C - 1, seed=9)
+    iqs = [ofdm.synth_frames(F, S, R, C, X, seed=90 + F, noise_std=0.01) for F in (70, 45)]
+    ref = [ofdm.frame_demod(iq, X, 0) for iq in iqs]
+    torch.cuda.synchronize()
+    sts = [torch.cuda.Stream(), torch.cuda.Stream()]
+    wss = [ofdm.workspace(iq.shape[0], S, R, C, dev) for iq in iqs]
+    outs = [[ofdm.c64((iq.shape[0], S - 1, C - 1), dev) for _ in range(3)] for iq in iqs]
+    for o in outs:
+        for t in o:
+            t.fill_(float("nan"))
+    torch.cuda.synchronize()
+    for rep in range(3):
+        for i in (0, 1):
+            ofdm.frame_demod(iqs[i], X, 0, ws=wss[i], out=outs[i][rep], stream=sts[i])
+    torch.cuda.synchronize()
+    for i in (0, 1):
+        for rep in range(3):
+            assert torch.equal(outs[i][rep], ref[i]), (i, rep)
