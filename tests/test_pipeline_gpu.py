@@ -130,3 +130,29 @@ def test_pipeline_rejects_bad_use(ofdm, dev):
             p.submit(3)
         p.submit(0)
         p.sync()
+
+
+def test_pipeline_ticketed_chunks_with_short_tail(ofdm, dev):
+    """Chunks large enough for the one-launch demod's work tickets (48 frames
+    x 100 symbols = 600 blocks) and a short last chunk (34 frames): a slot's
+    workspace then serves two batch sizes, whose ticket counters sit at
+    different offsets; two passes over the same pipeline, bit-identical, and
+    within rounding of the one-shot device path."""
+    import torch
+    F, S, R, C, prefix = 130, 101, 2, 1024, 0
+    rng = np.random.default_rng(130)
+    a = np.float32(0.70710678)
+    Xh = (rng.choice([-a, a], C - 1) + 1j * rng.choice([-a, a], C - 1)).astype(np.complex64)
+    X = torch.from_numpy(Xh).to(dev)
+    iq_d = ofdm.synth_frames(F, S, R, C, X, prefix=prefix, seed=130, noise_std=0.02)
+    ref = ofdm.frame_demod(iq_d, X, prefix).cpu().numpy()
+    iq = iq_d.cpu().numpy()
+    with ofdm.Pipeline(S, R, C, Xh, prefix, chunk_frames=48, depth=2) as p:
+        outs = []
+        for _ in range(2):
+            out = np.full((F, S - 1, C - 1), np.nan, np.complex64)
+            p.demod(iq, out)
+            p.sync()
+            outs.append(out)
+    parity(outs[0], ref)
+    assert np.array_equal(outs[0], outs[1])
