@@ -152,7 +152,7 @@ std::mutex g_tk_mu;
 std::map<const void *, TkState> g_tk_par;
 hipError_t tickets_next(const void *ws, unsigned long long *tickets, hipStream_t s, int *par) {
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-    if (hipError_t e = hipStreamIsCapturing(s, &st); e != hipSuccess) return e;
+    if (hipStreamIsCapturing(s, &st) != hipSuccess) st = hipStreamCaptureStatusNone;  // as before the query existed
     if (st != hipStreamCaptureStatusNone) {
         if (hipError_t e = ofdm::launch_zero_words(tickets + 2 * TICKET_SET_BYTES / 8, (int)(TICKET_SET_BYTES / 8), s);
             e != hipSuccess)
