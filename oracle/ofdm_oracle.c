@@ -292,7 +292,9 @@ static void load_symbol(const oracle_cf32 *sym, int R, int C, int prefix,
                (size_t)C * sizeof(*Y));
     /* fftOneRow per antenna row (cpuLS.hpp:278-281, 342-345) */
     for (int r = 0; r < R; ++r) {
-        if (fft32)
+        if (fft32 == 2)
+            oracle_fft_row_fast(&Y[(size_t)r * C], C);
+        else if (fft32)
             oracle_fft_row_f32(&Y[(size_t)r * C], C);
         else
             oracle_fft_row(&Y[(size_t)r * C], C, 0);
@@ -355,6 +357,21 @@ void oracle_frames_demod_fft32(const oracle_cf32 *iq, long long nframes, int S, 
     for (long long f = 0; f < nframes; ++f)
         frame_demod_ex(iq + f * frame_elems, S, R, C, prefix, X,
                        out + f * out_elems, NULL, NULL, 1);
+    (void)nthreads;
+}
+
+void oracle_frames_demod_fftfast(const oracle_cf32 *iq, long long nframes, int S, int R,
+                                 int C, int prefix, const oracle_cf32 *X,
+                                 oracle_cf32 *out, int nthreads) {
+    size_t frame_elems = (size_t)S * R * (C + prefix);
+    size_t out_elems = (size_t)(S - 1) * (C - 1);
+#ifdef _OPENMP
+    if (nthreads <= 0) nthreads = omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads)
+#endif
+    for (long long f = 0; f < nframes; ++f)
+        frame_demod_ex(iq + f * frame_elems, S, R, C, prefix, X,
+                       out + f * out_elems, NULL, NULL, 2);
     (void)nthreads;
 }
 

@@ -80,6 +80,11 @@ void oracle_frames_demod(const oracle_cf32 *iq, long long nframes, int S, int R,
  * the precision of the reference's fftwf): the timed CPU baseline of
  * bench.py.  Not a parity path (oracle_frames_demod is). */
 void oracle_fft_row_f32(oracle_cf32 *row, int C);
+/* bench.py's CPU baseline only (fft_fast.c): the same transform, vectorised
+ * (split arrays, unit-stride per-stage twiddles, -O3 -march=x86-64-v3) */
+void oracle_fft_row_fast(oracle_cf32 *row, int C);
+void oracle_frames_demod_fftfast(const oracle_cf32 *iq, long long nframes, int S, int R, int C, int prefix,
+                                 const oracle_cf32 *X, oracle_cf32 *out, int nthreads);
 void oracle_frames_demod_fft32(const oracle_cf32 *iq, long long nframes, int S, int R,
                                int C, int prefix, const oracle_cf32 *X,
                                oracle_cf32 *out, int nthreads);

@@ -45,6 +45,9 @@ class Oracle:
         L.oracle_frames_demod_fft32.argtypes = [_P, _c.c_longlong, _c.c_int, _c.c_int,
                                                 _c.c_int, _c.c_int, _P, _P, _c.c_int]
         L.oracle_fft_row_f32.argtypes = [_P, _c.c_int]
+        L.oracle_fft_row_fast.argtypes = [_P, _c.c_int]
+        L.oracle_frames_demod_fftfast.argtypes = [_P, _c.c_longlong, _c.c_int, _c.c_int,
+                                                  _c.c_int, _c.c_int, _P, _P, _c.c_int]
         L.oracle_frames_demod_freq.argtypes = [_P, _c.c_longlong, _c.c_int, _c.c_int,
                                                _c.c_int, _P, _P, _c.c_int]
         L.oracle_max_threads.restype = _c.c_int
@@ -172,6 +175,23 @@ class Oracle:
         self.lib.oracle_frames_demod_fft32(_ptr(iq), F, S, R, C, prefix, _ptr(X), _ptr(out),
                                            nthreads)
         return out
+
+    def frames_demod_fast(self, iq, X, prefix=0, nthreads=0):
+        """frames_demod with the vectorised single-precision FFT of fft_fast.c
+        (bench.py's timed CPU baseline only; not the parity oracle)."""
+        iq, X = c64(iq), c64(X)
+        F, S, R, Cp = iq.shape
+        C = Cp - prefix
+        out = np.empty((F, S - 1, C - 1), np.complex64)
+        self.lib.oracle_frames_demod_fftfast(_ptr(iq), F, S, R, C, prefix, _ptr(X), _ptr(out),
+                                             nthreads)
+        return out
+
+    def fft_rows_fast(self, rows):
+        rows = c64(rows).copy()
+        for r in rows.reshape(-1, rows.shape[-1]):
+            self.lib.oracle_fft_row_fast(_ptr(r), r.shape[-1])
+        return rows
 
     def fft_rows_f32(self, rows):
         rows = c64(rows).copy()

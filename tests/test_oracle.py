@@ -123,3 +123,18 @@ def test_reference_matrix_readX_vs_oracle(oracle, tmp_path):
     # missing file: the CPU path fills 0.707 + 0.707i (cpuLS.hpp:84-90)
     X = ref.matrix_readX(str(tmp_path / "missing.dat"), 15)
     assert np.all(X == np.complex64(0.707 + 0.707j))
+
+
+def test_fast_fft_matches_scalar_oracle_fft(oracle):
+    """oracle/fft_fast.c (the timed CPU baseline's vectorised FFT) computes
+    the same transform as oracle_fft_row_f32, bit for bit, at every power of
+    two the scalar one handles; and a frame demod through it equals the
+    scalar-FFT demod."""
+    rng = np.random.default_rng(17)
+    for C in (4, 16, 128, 1024, 2048, 4096):
+        x = (rng.standard_normal((3, C)) + 1j * rng.standard_normal((3, C))).astype(np.complex64)
+        assert np.array_equal(oracle.fft_rows_fast(x), oracle.fft_rows_f32(x)), C
+    F, S, R, C = 2, 5, 4, 1024
+    iq = (rng.standard_normal((F, S, R, C + 8)) + 1j * rng.standard_normal((F, S, R, C + 8))).astype(np.complex64)
+    X = ((rng.choice([-1, 1], C - 1) + 1j * rng.choice([-1, 1], C - 1)) * 0.7071).astype(np.complex64)
+    assert np.array_equal(oracle.frames_demod_fast(iq, X, 8, nthreads=2), oracle.frames_demod_fft32(iq, X, 8, nthreads=2))
