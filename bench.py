@@ -537,7 +537,9 @@ def main():
         dist.all_reduce(hi, op=dist.ReduceOp.MAX)
         names = ["step_ms", "kernel_ms", "box_copy_GBps", "effective_GHz"]
         scale = [1e3 / args.steps, 1.0, 1.0, 1.0]
-        per_rank = {n: {"min": float(lo[i]) * scale[i], "max": float(hi[i]) * scale[i]} for i, n in enumerate(names)}
+        fin = lambda v: v if v == v else None  # NaN (a probe that did not run) -> null: strict JSON
+        per_rank = {n: {"min": fin(float(lo[i]) * scale[i]), "max": fin(float(hi[i]) * scale[i])}
+                    for i, n in enumerate(names)}
     failed = not same or errs > 0
     if failed:
         log(f"CHECK FAILURE: timed output equals warm-up: {same}, QPSK errors on the timed output: {errs}")
