@@ -744,10 +744,10 @@ def bench_pcie(args, X, dev, world, rank, barrier):
 
 def bench_split(args, X, dev, world, rank, barrier):
     """configs[4]: every rank holds all frames of ITS --R antennas (global
-    antennas rank*R ...); step = SplitPipeline.run (partial LS, all_reduce of
-    |H|^2, partial FFT+MRC, reduce_scatter of the numerators over RCCL,
-    finalise of the rank's slice), chunked so the collectives overlap the
-    next chunk's kernels.  value = data symbols demodulated per second (every
+    antennas rank*R ...); step = SplitPipeline.run (one partial LS over the
+    batch, all_reduce of |H|^2, then per chunk the partial FFT+MRC,
+    reduce_scatter of the numerators over RCCL and the finalise of the rank's
+    slice), chunked so the collectives overlap the next chunk's kernels.  value = data symbols demodulated per second (every
     rank covers the same symbols; the antenna count grows with N)."""
     import torch
     import torch.distributed as dist
