@@ -101,7 +101,9 @@ def lib():
         import torch  # noqa: F401
         L = _c.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
-            fn = getattr(L, name)
+            if _LIBSEL and not hasattr(L, name):
+                continue  # an older variant build (OFDM_LSMRC_LIB): its missing entries fail when called
+            fn = getattr(L, name)  # the product library: every entry, or AttributeError here
             fn.restype = res
             fn.argtypes = args
         _lib = L
