@@ -111,6 +111,13 @@ def test_workspace_registry_without_device(ofdm):
     assert L.ofdm_frame_combine_freq(fake, 2, 5, 8, 1024, ws, need, fake, None) == -1
     assert L.ofdm_frame_export_estimate(ws, need, 2, 5, 8, 1024, 0, fake, None, None) == -1
     assert b"holds no estimate" in L.ofdm_last_error()
+    # the range entry: its range is checked first, then the same registry
+    assert L.ofdm_frame_mrc_partial_range(fake, 2, 1, 2, 5, 8, 1024, 0, ws, need, fake, None) == -1
+    assert b"outside" in L.ofdm_last_error()
+    assert L.ofdm_frame_mrc_partial_range(fake, 2, -1, 1, 5, 8, 1024, 0, ws, need, fake, None) == -1
+    assert L.ofdm_frame_mrc_partial_range(None, 2, 2, 0, 5, 8, 1024, 0, ws, need, None, None) == 0  # empty range
+    assert L.ofdm_frame_mrc_partial_range(fake, 2, 0, 2, 5, 8, 1024, 0, ws, need, fake, None) == -1
+    assert b"holds no estimate" in L.ofdm_last_error()
 
 
 def test_product_library_dispatches_only_product_kernels(ofdm):
