@@ -290,10 +290,13 @@ def clock_probe(step_diag, tag, ofdm, torch, stream, reps=3, save=None):
     return out
 
 
-def pmc_traffic(path, cfg):
-    """Corrected PMC HBM bytes per MRC launch for this exact config: `path`
+def pmc_traffic(path, cfg, build):
+    """Corrected PMC HBM bytes per launch for this exact config AND this
+    build of the library (`build`: ofdm_lsmrc.build_id(), which
+    scripts/pmc_summary.py records from the profiled run's bench line): `path`
     (profiles/pmc_traffic.json, the default shape) or else the latest-tagged
-    profiles/r*_traffic.json written by scripts/pmc_summary.py for it."""
+    profiles/r*_traffic.json for it.  A profile of other code is never
+    credited: (None, "no profile of this build")."""
     cands = [path] + sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")) +
                             glob.glob(os.path.join(ROOT, "profiles", "r*", "r*_traffic.json")),
                             key=os.path.basename, reverse=True)
@@ -306,9 +309,10 @@ def pmc_traffic(path, cfg):
         dc = d.get("config", {})
         if all(dc.get(k) == cfg[k] for k in ("R", "C", "S", "frames_per_gpu", "prefix")) and \
                 dc.get("domain", "time") == cfg["domain"] and \
-                dc.get("flow", "two-launch") == cfg.get("flow", "two-launch"):
+                dc.get("flow", "two-launch") == cfg.get("flow", "two-launch") and \
+                d.get("build_id") == build:
             return d.get("mrc_hbm_bytes_per_launch"), os.path.relpath(p, ROOT)
-    return None, None
+    return None, "no profile of this build"
 
 
 def visible_gpus():
@@ -562,7 +566,8 @@ def main():
         mrc_name = f"k_demod_td{C} (LS + FFT+MRC+normalise+rotate, one launch)"
         bytes_launch += F * (R * C * 8 + K * 8)
     achieved = bytes_launch / (mrc_ms * 1e-3) / 1e9
-    traffic, tsrc = pmc_traffic(args.pmc, cfg)
+    build = ofdm.build_id()
+    traffic, tsrc = pmc_traffic(args.pmc, cfg, build)
     step_bytes = F * S * R * C * 8 + Q * K * 8
     result = {
         "metric": "OFDM symbols/s (LS+MRC) at 1024 subcarriers x 64 ant; achieved HBM GB/s vs peak",
@@ -589,6 +594,7 @@ def main():
                      "box_read_GBps": box["box_read_GBps"] if box else None,
                      "frac_of_box_read": achieved / box["box_read_GBps"] if box else None,
                      "box_probe": box["box_probe"] if box else None},
+        "build_id": build,
         "clock": clock,
         "stages_ms": {"demod_one_launch": mrc_ms} if one else {"estimate_ls": ls_ms, "combine_mrc": mrc_ms},
         "step_algorithmic_GBps": step_bytes / (elapsed / args.steps) / 1e9,

@@ -62,20 +62,15 @@ hipError_t ls_fused(const float2 *iq, long long F, int S, int R, int C, int pref
     if (C == 2048) return ofdm::launch_ls_td2048(iq, F, S, R, prefix, X, Hc, P, partial, s);
     return ofdm::launch_ls_td4096(iq, F, S, R, prefix, X, Hc, P, partial, s);
 }
-hipError_t tickets_next(const void *ws, unsigned long long *tickets, hipStream_t s, int *par);
-void tickets_forget(const void *ws);
-// ws / tickets: the frame workspace and its ticket area (work-ticketed
-// kernels: C = 2048 and 4096)
+hipError_t tickets_for(unsigned long long *area, hipStream_t s, ofdm::Tickets *tk);
+// tickets: the frame workspace's ticket area (work-ticketed kernels: C = 2048 and 4096)
 hipError_t mrc_fused(const float2 *iq, long long F, int S, int R, int C, int prefix, const float2 *Hc,
-                     const float *P, float2 *out, int mode, hipStream_t s, const void *ws,
-                     unsigned long long *tickets) {
+                     const float *P, float2 *out, int mode, hipStream_t s, unsigned long long *tickets) {
     if (C == 1024) return ofdm::launch_mrc_td1024(iq, F, S, R, prefix, Hc, P, out, mode, s);
-    int par = 0;
-    if (hipError_t e = tickets_next(ws, tickets, s, &par); e != hipSuccess) return e;
-    hipError_t e = C == 2048 ? ofdm::launch_mrc_td2048(iq, F, S, R, prefix, Hc, P, out, mode, tickets, par, s)
-                             : ofdm::launch_mrc_td4096(iq, F, S, R, prefix, Hc, P, out, mode, tickets, par, s);
-    if (e != hipSuccess) tickets_forget(ws);  // no kernel zeroed the next set
-    return e;
+    ofdm::Tickets tk;
+    if (hipError_t e = tickets_for(tickets, s, &tk); e != hipSuccess) return e;
+    return C == 2048 ? ofdm::launch_mrc_td2048(iq, F, S, R, prefix, Hc, P, out, mode, tk, s)
+                     : ofdm::launch_mrc_td4096(iq, F, S, R, prefix, Hc, P, out, mode, tk, s);
 }
 
 // ofdm_frame_demod at C = 1024 runs LS and MRC as ONE launch (k_demod_td1024)
@@ -117,62 +112,82 @@ struct Workspace {
     float2 *Hc;                 // [F][R][C] bin layout
     float *P;                   // [F][C]   bin layout
     unsigned long long *flags;  // [F] per-frame estimate flags of the one-launch demod
-    unsigned long long *tickets;  // 4 sets of 8 work-ticket counters, 128 B apart (wave_fft1024.hpp take_block)
+    unsigned long long *tickets;  // 8 work-ticket counters, 128 B apart (wave_fft1024.hpp take_ticket)
     float2 *staging;            // [chunk][S][R][C] (non-fused C only)
     long long chunk;
 };
 
-constexpr size_t TICKET_SET_BYTES = 8 * 128;         // 8 counters, one 128-B line each
-constexpr size_t TICKET_BYTES = 4 * TICKET_SET_BYTES;  // sets 0 / 1: eager launches; 2 (3): captured ones
+constexpr size_t TICKET_BYTES = 4096;  // the ticket area: 8 counters, one 128-B line each (+ room)
+constexpr int TICKET_WORDS = 8 * 16;
 
-// Work-ticket counter sets of a workspace (wave_fft1024.hpp, take_block): a
-// launch counts in set `par` and zeroes set par ^ 1 for the next launch on
-// the same workspace; the host keeps `par` per workspace, flips it per
-// launch, and zeroes both sets the first time it meets the workspace (and
-// again after ofdm_workspace_release).  Launches on one workspace are
-// ordered (one stream, as the estimate they share already requires).  A
-// workspace used by two library instances in turn must be released by one
-// before the other uses it, as for its estimate.
-// Under stream capture the parity would be frozen in the graph and every
-// replay would count in a set the previous replay left non-zero: a captured
-// launch counts in set 2 instead, behind a zeroing kernel node of its own
-// (so every replay starts from zero; a captured hipMemsetAsync node replayed
-// with a wrong value here), and zeroes set 3, which nothing reads; the eager
-// sets 0 / 1 and their host parity are untouched, so graphs and eager
-// launches on the same workspace may alternate.
-// The counters' offset in the workspace depends on the batch geometry (they
-// follow the estimate), so the host also keeps where they were: a call with
-// another geometry on the same workspace (whose estimate may have written
-// over the old counters' place) zeroes both sets again.
-struct TkState {
-    const void *at;  // the counters' address at the last launch
-    int par;
-};
-std::mutex g_tk_mu;
-std::map<const void *, TkState> g_tk_par;
-hipError_t tickets_next(const void *ws, unsigned long long *tickets, hipStream_t s, int *par) {
-    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(s, &st) != hipSuccess) st = hipStreamCaptureStatusNone;  // as before the query existed
-    if (st != hipStreamCaptureStatusNone) {
-        if (hipError_t e = ofdm::launch_zero_words(tickets + 2 * TICKET_SET_BYTES / 8, (int)(TICKET_SET_BYTES / 8), s);
-            e != hipSuccess)
-            return e;
-        *par = 2;
-        return hipSuccess;
+// Work-ticket tags (wave_fft1024.hpp, take_ticket): one per ticketed launch,
+// never 0, not repeated in this process before 2^32 launches, from an offset
+// drawn once per process (so counters another process left in recycled
+// memory do not carry it either, but for a 2^-32 chance per word).
+unsigned next_tag() {
+    static std::atomic<unsigned> ctr{0};
+    static const unsigned salt = [] {
+        std::random_device rd;
+        return (unsigned)rd();
+    }();
+    for (;;) {
+        const unsigned t = salt + ctr.fetch_add(1);
+        if (t != 0) return t;
     }
-    std::lock_guard<std::mutex> lock(g_tk_mu);
-    auto it = g_tk_par.find(ws);
-    if (it == g_tk_par.end() || it->second.at != tickets) {
-        if (hipError_t e = hipMemsetAsync(tickets, 0, 2 * TICKET_SET_BYTES, s); e != hipSuccess) return e;
-        it = g_tk_par.insert_or_assign(ws, TkState{tickets, 1}).first;
-    }
-    it->second.par ^= 1;
-    *par = it->second.par;
-    return hipSuccess;
 }
-void tickets_forget(const void *ws) {
-    std::lock_guard<std::mutex> lock(g_tk_mu);
-    g_tk_par.erase(ws);
+
+// The sticky device status word: host-mapped, library-owned (one per
+// process, every device writes it), allocated at the first ticketed launch.
+// A ticketed launch that meets a counter it cannot trust stores a TK_* bit
+// there (wave_fft1024.hpp, ticket_fault); every entry that launches ticketed
+// kernels reads it first (a host load, no synchronisation) and, if set,
+// clears it and returns OFDM_E_DEVICE, as ofdm_device_status() does.
+// g_status_host stands in before the mapped word exists (and for
+// ofdm_device_status_inject on a machine without a GPU).
+std::once_flag g_status_once;
+unsigned *g_status_mapped = nullptr;
+volatile unsigned g_status_host = 0;
+unsigned *status_word_for_device() {
+    std::call_once(g_status_once, [] {
+        void *p = nullptr;
+        if (hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent) ==
+            hipSuccess) {
+            std::memset(p, 0, 64);
+            g_status_mapped = static_cast<unsigned *>(p);
+        } else {
+            (void)hipGetLastError();  // no mapped word: launches run without fault reporting
+        }
+    });
+    return g_status_mapped;
+}
+int take_status(const char *fn) {
+    unsigned v = g_status_host;
+    volatile unsigned *m = g_status_mapped;
+    if (m) v |= *m;
+    if (!v) return OFDM_OK;
+    g_status_host = 0;
+    if (m) *m = 0;
+    return fail(OFDM_E_DEVICE,
+                "%s: an earlier work-ticketed launch (C = 1024 one-launch demod, C = 2048 / 4096 MRC) found its "
+                "work-ticket counters taken by another launch (status 0x%x: %s%s%s); its output may be incomplete "
+                "-- one workspace was used by two launches at once", fn, v,
+                (v & ofdm::TK_FOREIGN) ? "foreign count " : "", (v & ofdm::TK_RANGE) ? "count out of range " : "",
+                (v & ofdm::TK_CONTENDED) ? "contended claim" : "");
+}
+
+// The tickets of one launch.  Under stream capture the tag is frozen in the
+// graph and every replay would meet the counts of the previous one: a
+// captured launch is preceded by a zeroing kernel node over the counters (a
+// captured hipMemsetAsync node replayed with a wrong value here), so every
+// replay claims zero words.
+hipError_t tickets_for(unsigned long long *area, hipStream_t s, ofdm::Tickets *tk) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &st) != hipSuccess) st = hipStreamCaptureStatusNone;
+    tk->set = area;
+    tk->tag = next_tag();
+    tk->status = st == hipStreamCaptureStatusNone ? status_word_for_device() : g_status_mapped;
+    if (st != hipStreamCaptureStatusNone) return ofdm::launch_zero_words(area, TICKET_WORDS, s);
+    return hipSuccess;
 }
 
 size_t ws_bytes(long long F, int S, int R, int C, bool need_staging) {
@@ -452,7 +467,13 @@ size_t ofdm_frame_workspace_bytes(long long nframes, int S, int R, int C) {
 
 int ofdm_workspace_release(const void *d_ws) {
     ws_forget(d_ws);
-    tickets_forget(d_ws);
+    return OFDM_OK;
+}
+
+int ofdm_device_status(void) { return take_status("ofdm_device_status"); }
+
+int ofdm_device_status_inject(unsigned bits) {
+    g_status_host = g_status_host | bits;
     return OFDM_OK;
 }
 
@@ -476,6 +497,7 @@ int ofdm_frame_estimate(const ofdm_cf32 *d_iq, long long nframes, int S, int R, 
 
 int ofdm_frame_combine(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, int prefix,
                        void *d_ws, size_t ws_bytes_, ofdm_cf32 *d_out, ofdm_stream_t stream) {
+    if (int st = take_status("ofdm_frame_combine")) return st;
     int rc = check_frame_args(d_iq, nframes, S, R, C, prefix, d_out, "ofdm_frame_combine");
     if (rc) return rc;
     if (nframes == 0) return OFDM_OK;
@@ -489,7 +511,7 @@ int ofdm_frame_combine(const ofdm_cf32 *d_iq, long long nframes, int S, int R, i
     hipStream_t s = hs(stream);
     if (fused_c(C))
         return hip_check(mrc_fused(F2(d_iq), nframes, S, R, C, prefix, w.Hc, w.P,
-                                                 F2(d_out), 0, s, d_ws, w.tickets),
+                                                 F2(d_out), 0, s, w.tickets),
                          "mrc_fused");
     // staged path: the FFT of every chunk is redone here (estimate kept only Hc/P)
     return td_staged(F2(d_iq), nframes, S, R, C, prefix, nullptr, w, F2(d_out), 3, s);
@@ -505,6 +527,7 @@ int ofdm_frame_demod(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int
 int ofdm_frame_demod_ex(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int C, int prefix,
                         const ofdm_cf32 *d_X, void *d_ws, size_t ws_bytes_, ofdm_cf32 *d_out, int flow,
                         long long spin_ticks, ofdm_stream_t stream) {
+    if (int st = take_status("ofdm_frame_demod")) return st;
     int rc = check_frame_args(d_iq, nframes, S, R, C, prefix, d_out, "ofdm_frame_demod");
     if (rc) return rc;
     if (!d_X) return fail(OFDM_E_ARG, "ofdm_frame_demod: null pilots");
@@ -516,15 +539,12 @@ int ofdm_frame_demod_ex(const ofdm_cf32 *d_iq, long long nframes, int S, int R, 
     hipStream_t s = hs(stream);
     ws_forget(d_ws);
     if (flow == OFDM_FLOW_AUTO && one_launch_demod(C, s)) {
-        int par = 0;
-        if ((rc = hip_check(tickets_next(d_ws, w.tickets, s, &par), "work tickets"))) return rc;
-        rc = hip_check(ofdm::launch_demod_td1024(F2(d_iq), nframes, S, R, prefix, F2(d_X), w.Hc, w.P, F2(d_out),
-                                                 w.tickets, par, w.flags, next_epoch(), spin_ticks, s),
+        ofdm::Tickets tk;
+        if ((rc = hip_check(tickets_for(w.tickets, s, &tk), "work tickets"))) return rc;
+        rc = hip_check(ofdm::launch_demod_td1024(F2(d_iq), nframes, S, R, prefix, F2(d_X), w.Hc, w.P, F2(d_out), tk,
+                                                 w.flags, next_epoch(), spin_ticks, s),
                        "launch_demod_td");
-        if (rc == OFDM_OK)
-            ws_record(d_ws, ws_bytes_, nframes, S, R, C, true, false);
-        else
-            tickets_forget(d_ws);  // no kernel zeroed the next set: start over at the next use
+        if (rc == OFDM_OK) ws_record(d_ws, ws_bytes_, nframes, S, R, C, true, false);
         return rc;
     }
     if (fused_c(C)) {
@@ -533,7 +553,7 @@ int ofdm_frame_demod_ex(const ofdm_cf32 *d_iq, long long nframes, int S, int R, 
         if (rc) return rc;
         // the estimate is in the workspace once the LS launch is enqueued
         ws_record(d_ws, ws_bytes_, nframes, S, R, C, true, false);
-        return hip_check(mrc_fused(F2(d_iq), nframes, S, R, C, prefix, w.Hc, w.P, F2(d_out), 0, s, d_ws, w.tickets),
+        return hip_check(mrc_fused(F2(d_iq), nframes, S, R, C, prefix, w.Hc, w.P, F2(d_out), 0, s, w.tickets),
                          "mrc_fused");
     }
     rc = td_staged(F2(d_iq), nframes, S, R, C, prefix, F2(d_X), w, F2(d_out), 0, s);
@@ -636,6 +656,7 @@ int ofdm_frame_ls_partial(const ofdm_cf32 *d_iq, long long nframes, int S, int R
 int ofdm_frame_mrc_partial(const ofdm_cf32 *d_iq, long long nframes, int S, int R, int C,
                            int prefix, void *d_ws, size_t ws_bytes_, ofdm_cf32 *d_num,
                            ofdm_stream_t stream) {
+    if (int st = take_status("ofdm_frame_mrc_partial")) return st;
     int rc = check_frame_args(d_iq, nframes, S, R, C, prefix, d_num, "ofdm_frame_mrc_partial");
     if (rc) return rc;
     if (nframes == 0) return OFDM_OK;
@@ -649,7 +670,7 @@ int ofdm_frame_mrc_partial(const ofdm_cf32 *d_iq, long long nframes, int S, int 
     hipStream_t s = hs(stream);
     if (fused_c(C))
         return hip_check(mrc_fused(F2(d_iq), nframes, S, R, C, prefix, w.Hc, w.P,
-                                                 F2(d_num), 1, s, d_ws, w.tickets),
+                                                 F2(d_num), 1, s, w.tickets),
                          "mrc_fused");
     return td_staged(F2(d_iq), nframes, S, R, C, prefix, nullptr, w, F2(d_num), 1, s);
 }
@@ -658,6 +679,7 @@ int ofdm_frame_mrc_partial_range(const ofdm_cf32 *d_iq, long long nframes, long 
                                  int R, int C, int prefix, void *d_ws, size_t ws_bytes_, ofdm_cf32 *d_num,
                                  ofdm_stream_t stream) {
     static const char *fn = "ofdm_frame_mrc_partial_range";
+    if (int st = take_status(fn)) return st;
     if (nframes < 0 || f0 < 0 || count < 0 || f0 > nframes || count > nframes - f0)
         return fail(OFDM_E_ARG, "%s: frames [%lld, %lld) outside [0, %lld)", fn, f0, f0 + count, nframes);
     if (count == 0) return OFDM_OK;
@@ -676,13 +698,14 @@ int ofdm_frame_mrc_partial_range(const ofdm_cf32 *d_iq, long long nframes, long 
     v.Hc += f0 * (long long)R * C;
     v.P += f0 * C;
     if (fused_c(C))
-        return hip_check(mrc_fused(iq, count, S, R, C, prefix, v.Hc, v.P, F2(d_num), 1, s, d_ws, w.tickets), fn);
+        return hip_check(mrc_fused(iq, count, S, R, C, prefix, v.Hc, v.P, F2(d_num), 1, s, w.tickets), fn);
     return td_staged(iq, count, S, R, C, prefix, nullptr, v, F2(d_num), 1, s);
 }
 
 int ofdm_symbols_demod(const ofdm_cf32 *d_sym, long long nsym, int R, int C, int prefix, const void *d_ws,
                        size_t ws_bytes_, long long frame, ofdm_cf32 *d_out, ofdm_stream_t stream) {
     static const char *fn = "ofdm_symbols_demod";
+    if (int st = take_status(fn)) return st;
     if (nsym < 0 || nsym > 0x7ffffffell) return fail(OFDM_E_ARG, "%s: nsym=%lld out of range", fn, nsym);
     if (nsym > 0 && (!d_sym || !d_out)) return fail(OFDM_E_ARG, "%s: null pointer", fn);
     if (R < 1) return fail(OFDM_E_ARG, "%s: R=%d < 1", fn, R);
@@ -716,7 +739,7 @@ int ofdm_symbols_demod(const ofdm_cf32 *d_sym, long long nsym, int R, int C, int
     const long long row = (long long)R * (C + prefix);
     const float2 *iq = reinterpret_cast<const float2 *>(reinterpret_cast<uintptr_t>(d_sym) - (uintptr_t)(row * 8));
     return hip_check(mrc_fused(iq, 1, (int)(nsym + 1), R, C, prefix, w.Hc + frame * (long long)R * C,
-                               w.P + frame * C, F2(d_out), 0, hs(stream), d_ws, w.tickets),
+                               w.P + frame * C, F2(d_out), 0, hs(stream), w.tickets),
                      fn);
 }
 
@@ -764,9 +787,12 @@ int ofdm_buffer_hash(const void *d_buf, size_t bytes, unsigned long long *d_hash
                      "ofdm_buffer_hash");
 }
 
-int ofdm_hbm_probe(int mode, const void *d_src, void *d_dst, size_t bytes, ofdm_stream_t stream) {
+int ofdm_hbm_probe(int mode, const void *d_src, void *d_dst, size_t bytes, size_t dst_bytes, ofdm_stream_t stream) {
     if ((mode != 0 && mode != 1) || !d_src || !d_dst)
         return fail(OFDM_E_ARG, "ofdm_hbm_probe: mode 0 (copy) or 1 (read) and non-null buffers");
+    const size_t need = mode == 0 ? bytes : (size_t)OFDM_HBM_PROBE_SINK_BYTES;
+    if (dst_bytes < need)
+        return fail(OFDM_E_ARG, "ofdm_hbm_probe: d_dst holds %zu bytes, mode %d writes %zu", dst_bytes, mode, need);
     if ((reinterpret_cast<size_t>(d_src) | reinterpret_cast<size_t>(d_dst) | bytes) % 16)
         return fail(OFDM_E_ARG, "ofdm_hbm_probe: 16-B aligned buffers and a multiple of 16 bytes");
     return hip_check(ofdm::launch_hbm_probe(mode, d_src, d_dst, (long long)(bytes / 16), hs(stream)),

@@ -448,8 +448,7 @@ __device__ __forceinline__ void split_unit(const float2 *__restrict__ iq, int S,
 // DESIGN.md 4.6).
 __global__ void __attribute__((amdgpu_flat_work_group_size(512, 512), amdgpu_waves_per_eu(4, 4)))
 k_demod_td1024(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ X, float2 *Hc,
-               float *P, float2 *__restrict__ out, long long nq, long long nblocks, unsigned long long *tickets,
-               int par, long long k0, long long split, unsigned long long *flags, unsigned long long epoch,
+               float *P, float2 *__restrict__ out, long long nq, long long nblocks, Tickets tk, long long k0, long long split, unsigned long long *flags, unsigned long long epoch,
                int nls, long long nframes, long long spin_ticks) {
     using namespace hlds;
     constexpr int HW = WAVES;
@@ -482,7 +481,7 @@ k_demod_td1024(const float2 *__restrict__ iq, int S, int R, int prefix, const fl
         __syncthreads();
         OFDM_DIAG_MARKN(0)
     } else {
-        lb = wg_take_unit(tickets, par, nblocks, k0, (long long)blockIdx.x - nls, split,
+        lb = wg_take_unit(tk, nblocks, k0, (long long)blockIdx.x - nls, split,
                           reinterpret_cast<long long *>(hfree + 255));
         if (lb < 0) return;  // every block taken
         um = (int)(lb & 3);
@@ -585,7 +584,7 @@ hipError_t launch_mrc_td1024(const float2 *iq, long long nframes, int S, int R, 
 // spin_ticks: how long (100 MHz ticks) an MRC workgroup waits for a frame's
 // flag before it estimates the frame itself (< 0: SPIN_TICKS).
 hipError_t launch_demod_td1024(const float2 *iq, long long nframes, int S, int R, int prefix, const float2 *X,
-                               float2 *Hc, float *P, float2 *out, unsigned long long *tickets, int par,
+                               float2 *Hc, float *P, float2 *out, Tickets tk,
                                unsigned long long *flags, unsigned long long epoch, long long spin_ticks,
                                hipStream_t s) {
     using namespace td1024;
@@ -600,7 +599,7 @@ hipError_t launch_demod_td1024(const float2 *iq, long long nframes, int S, int R
     const long long g = ticket_grid(nb, 8 * split);
     if (g + nls > 0x7fffffffll) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_demod_td1024, dim3((unsigned)(nls + g)), dim3(64 * hlds::WAVES), hlds::LDS_BYTES, s, iq,
-                       S, R, prefix, X, Hc, P, out, nq, nb, tickets, par, k0, split, flags, epoch, (int)nls, nframes,
+                       S, R, prefix, X, Hc, P, out, nq, nb, tk, k0, split, flags, epoch, (int)nls, nframes,
                        spin_ticks < 0 ? SPIN_TICKS : spin_ticks);
     return hipGetLastError();
 }

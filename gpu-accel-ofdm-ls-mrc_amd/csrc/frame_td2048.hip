@@ -256,7 +256,7 @@ __device__ __forceinline__ void mrc2048_symbol(const float2 *__restrict__ iq, in
 __global__ void __attribute__((amdgpu_flat_work_group_size(256, 256), amdgpu_waves_per_eu(2, 2)))
 k_mrc_td2048(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
              const float *__restrict__ P, float2 *__restrict__ out, long long nq, long long nblocks,
-             unsigned long long *tickets, int par, long long k0, int mode) {
+             Tickets tk, long long k0, int mode) {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     const int w = threadIdx.x >> 6, t = threadIdx.x & 63;
     float2 *T = lds + TAB + w * hl::TS;
@@ -264,7 +264,7 @@ k_mrc_td2048(const float2 *__restrict__ iq, int S, int R, int prefix, const floa
     // the logical block (4 consecutive data symbols) is a work ticket
     // (wave_fft1024.hpp take_block); the slot is wave 0's transpose image,
     // first written after the table barrier
-    const long long lb = td1024::wg_take_block(tickets, par, nblocks, k0, blockIdx.x,
+    const long long lb = td1024::wg_take_block(tk, nblocks, k0, blockIdx.x,
                                                reinterpret_cast<long long *>(lds + TAB));
     if (lb < 0) return;
     fill_tables(lds);
@@ -288,8 +288,8 @@ hipError_t launch_ls_td2048(const float2 *iq, long long nframes, int S, int R, i
 }
 
 hipError_t launch_mrc_td2048(const float2 *iq, long long nframes, int S, int R, int prefix,
-                             const float2 *Hc, const float *P, float2 *out, int mode, unsigned long long *tickets,
-                             int par, hipStream_t s) {
+                             const float2 *Hc, const float *P, float2 *out, int mode, Tickets tk,
+                             hipStream_t s) {
     using namespace td2048;
     const long long nq = nframes * (S - 1);
     if (nq <= 0) return hipSuccess;
@@ -298,7 +298,7 @@ hipError_t launch_mrc_td2048(const float2 *iq, long long nframes, int S, int R, 
     if (grid > 0x7fffffffll) return hipErrorInvalidValue;
     auto kern = k_mrc_td2048;
     hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(64 * MRC_WAVES), lds_bytes(MRC_WAVES), s, iq, S,
-                       R, prefix, Hc, P, out, nq, nblocks, tickets, par, td1024::ticket_k0(2), mode);
+                       R, prefix, Hc, P, out, nq, nblocks, tk, td1024::ticket_k0(2), mode);
     return hipGetLastError();
 }
 

@@ -426,7 +426,7 @@ __device__ __forceinline__ void mrc4096_block(const float2 *__restrict__ iq, int
 __global__ void __attribute__((amdgpu_flat_work_group_size(128 * H_PAIRS, 128 * H_PAIRS), amdgpu_waves_per_eu(2, 2)))
 k_mrc_td4096h(const float2 *__restrict__ iq, int S, int R, int prefix, const float2 *__restrict__ Hc,
               const float *__restrict__ P, float2 *__restrict__ out, long long nframes, long long nblocks,
-              unsigned long long *tickets, int par, long long k0, int mode) {
+              Tickets tk, long long k0, int mode) {
     extern __shared__ __attribute__((aligned(16))) float2 lds[];
     const int pair = __builtin_amdgcn_readfirstlane(threadIdx.x >> 7);
     OFDM_DIAG_BEGIN()
@@ -434,7 +434,7 @@ k_mrc_td4096h(const float2 *__restrict__ iq, int S, int R, int prefix, const flo
     // XCD's range of consecutive blocks first -- a frame's blocks share an
     // L2 -- then the others'); the slot is wave 0's transpose image, first
     // written after mrc4096_block's table barrier
-    const long long lb = wg_take_block(tickets, par, nblocks, k0, blockIdx.x, reinterpret_cast<long long *>(lds + X_TAB));
+    const long long lb = wg_take_block(tk, nblocks, k0, blockIdx.x, reinterpret_cast<long long *>(lds + X_TAB));
     if (lb < 0) return;  // whole workgroup: every block taken
     const int nsym = S - 1;
     const long long bpf = (nsym + H_PAIRS - 1) / H_PAIRS;
@@ -463,8 +463,8 @@ hipError_t launch_ls_td4096(const float2 *iq, long long nframes, int S, int R, i
 }
 
 hipError_t launch_mrc_td4096(const float2 *iq, long long nframes, int S, int R, int prefix,
-                             const float2 *Hc, const float *P, float2 *out, int mode, unsigned long long *tickets,
-                             int par, hipStream_t s) {
+                             const float2 *Hc, const float *P, float2 *out, int mode, Tickets tk,
+                             hipStream_t s) {
     using namespace td4096;
     const long long nq = nframes * (S - 1);
     if (nq <= 0) return hipSuccess;
@@ -478,7 +478,7 @@ hipError_t launch_mrc_td4096(const float2 *iq, long long nframes, int S, int R, 
     if (hipError_t e = opt_in_lds(reinterpret_cast<const void *>(kern), (int)H_LDS); e != hipSuccess)
         return e;  // > 64 KiB of dynamic LDS
     hipLaunchKernelGGL(kern, dim3((unsigned)g), dim3(128 * H_PAIRS), H_LDS, s, iq, S, R, prefix, Hc, P, out, nframes,
-                       nb, tickets, par, td1024::ticket_k0(1), mode);
+                       nb, tk, td1024::ticket_k0(1), mode);
     return hipGetLastError();
 }
 

@@ -32,6 +32,22 @@ inline hipError_t opt_in_lds(const void *kernel, int bytes) {
 // Sets ofdm_last_error() for the calling thread and returns `code`.
 int set_error(int code, const char *msg);
 
+// The work tickets of ONE launch of a ticketed receiver (wave_fft1024.hpp,
+// take_unit): set = 8 counter words 128 B apart (the workspace's ticket
+// area); tag = this launch's value, never 0, in the high half of every word
+// the launch counts in (a word holding anything else is claimed afresh, so
+// no stale or foreign value is ever consumed as a count); status = the
+// library's host-mapped sticky status word (capi.cpp, OFDM_E_DEVICE), or null.
+struct Tickets {
+    unsigned long long *set;
+    unsigned *status;
+    unsigned tag;
+};
+// status bits a ticketed launch raises
+constexpr unsigned TK_FOREIGN = 1u;     // a count of another launch in a fetch_add result
+constexpr unsigned TK_RANGE = 2u;       // a count beyond units + grid
+constexpr unsigned TK_CONTENDED = 4u;   // a claim that did not settle in 64 compare-and-swaps
+
 // Generic batched row FFT (Stockham in LDS), in place or out of place.
 // Row i is read from in + i*in_stride + in_off and written to
 // out + i*out_stride + out_off.  Any 2 <= C <= FFT_ANY_MAX: powers of two up
@@ -127,7 +143,7 @@ hipError_t launch_mrc_td1024(const float2 *iq, long long nframes, int S, int R, 
 // MRC workgroups wait for it.  flags: nframes words in the workspace; epoch:
 // a per-launch value no flag holds.  mode 0 (full demod) only.
 hipError_t launch_demod_td1024(const float2 *iq, long long nframes, int S, int R, int prefix, const float2 *X,
-                               float2 *Hc, float *P, float2 *out, unsigned long long *tickets, int par,
+                               float2 *Hc, float *P, float2 *out, Tickets tk,
                                unsigned long long *flags, unsigned long long epoch, long long spin_ticks,
                                hipStream_t s);
 
@@ -136,14 +152,14 @@ hipError_t launch_demod_td1024(const float2 *iq, long long nframes, int S, int R
 hipError_t launch_ls_td2048(const float2 *iq, long long nframes, int S, int R, int prefix,
                             const float2 *X, float2 *Hc, float *P, int partial, hipStream_t s);
 hipError_t launch_mrc_td2048(const float2 *iq, long long nframes, int S, int R, int prefix,
-                             const float2 *Hc, const float *P, float2 *out, int mode, unsigned long long *tickets,
-                             int par, hipStream_t s);
+                             const float2 *Hc, const float *P, float2 *out, int mode, Tickets tk,
+                             hipStream_t s);
 // fused time-domain receiver, C = 4096 (frame_td4096.hip); same contracts
 hipError_t launch_ls_td4096(const float2 *iq, long long nframes, int S, int R, int prefix,
                             const float2 *X, float2 *Hc, float *P, int partial, hipStream_t s);
 hipError_t launch_mrc_td4096(const float2 *iq, long long nframes, int S, int R, int prefix,
-                             const float2 *Hc, const float *P, float2 *out, int mode, unsigned long long *tickets,
-                             int par, hipStream_t s);
+                             const float2 *Hc, const float *P, float2 *out, int mode, Tickets tk,
+                             hipStream_t s);
 hipError_t launch_conj_product(const float2 *Y, long long nsyms, int R, int C, const float2 *Hc,
                                float2 *prod, hipStream_t s);
 hipError_t launch_combine(const float2 *prod, long long nsyms, int R, int K, const float *P,

@@ -12,6 +12,7 @@
 // (q, a) finally owns bins b = q + 256 c(a) + 16 k', c(a) = (a >> 1) + 2 (a & 1).
 #pragma once
 #include "common.hpp"
+#include "launch.hpp"
 #include "pk.hpp"
 
 namespace ofdm {
@@ -307,25 +308,64 @@ __device__ __forceinline__ void acquire_all() {
 // over-subscribed (ticket_grid: + 25 % + 64 workgroups); a workgroup that
 // finds every range exhausted exits at once.  Every block is processed
 // exactly once whatever the placement or dispatch order.
-// Counters: two sets of 8 (one 128-B line each) in the workspace's ticket
-// area; a launch counts in set `par` and zeroes set par ^ 1 for the next
-// launch on this workspace (the host flips `par` per launch and zeroes both
-// sets the first time it meets a workspace), so no counter needs a reset
-// between two launches and no launch pays for one.
+// Counters: one set of 8 words (one 128-B line each) in the workspace's
+// ticket area, written by nothing but ticketed launches -- but the memory is
+// the caller's, and a word may hold anything when a launch starts (an earlier
+// launch's count, an estimate of another geometry written over it, a freed
+// and re-used allocation).  So a count is tagged: word = tag << 32 | count,
+// tag = a per-launch value (never 0; Tickets, launch.hpp).  The first
+// workgroup of a launch to meet a range's word with another tag claims it
+// with ONE compare-and-swap to (tag, 1) and takes ticket 0; every later one
+// adds 1 (the counts stay below 2^32: units + grid < 2^31).  No host
+// registry, no zeroing launch, no parity: a stale or garbage word is never
+// consumed as a count.  Two launches counting in one word at once (two
+// streams sharing a workspace, against the header's contract) show up as a
+// foreign tag in a fetch_add result: that launch raises TK_FOREIGN in the
+// host-mapped status word (the host returns OFDM_E_DEVICE at the next call)
+// and takes nothing more from that range.
 // ---------------------------------------------------------------------------
 constexpr int TICKET_STRIDE = 16;            // u64 words between counters (128 B)
-constexpr int TICKET_SET = 8 * TICKET_STRIDE;  // words per set
 constexpr int HWREG_XCC_ID = (31 << 11) | 20;
 __device__ __forceinline__ long long ticket_range_count(long long nb, long long per, unsigned y) {
     const long long lo = (long long)y * per;
     return nb - lo < per ? (nb - lo > 0 ? nb - lo : 0) : per;
 }
+__device__ __forceinline__ void ticket_fault(const Tickets &tk, unsigned why) {
+    if (tk.status) __hip_atomic_store((gu32 *)tk.status, why, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// ticket t of range y (t in [0, units)), or -1: none left in the range, -2:
+// give up on the range (a fault was raised)
+__device__ __forceinline__ long long take_ticket(const Tickets &tk, unsigned y, long long units) {
+    gu64 *p = (gu64 *)(tk.set + y * TICKET_STRIDE);
+    const unsigned long long mine = (unsigned long long)tk.tag << 32;
+    unsigned long long v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int tries = 0; (v >> 32) != tk.tag; ++tries) {  // not counted in by this launch yet: claim it
+        if (tries == 64) {
+            ticket_fault(tk, TK_CONTENDED);
+            return -2;
+        }
+        if (__hip_atomic_compare_exchange_strong(p, &v, mine | 1ull, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT))
+            return 0;
+    }
+    if ((long long)(unsigned)v >= units) return -1;
+    const unsigned long long r = __hip_atomic_fetch_add(p, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((r >> 32) != tk.tag) {
+        ticket_fault(tk, TK_FOREIGN);
+        return -2;
+    }
+    const long long t = (long long)(unsigned)r;
+    if (t < units) return t;
+    if (t > units + (long long)gridDim.x) ticket_fault(tk, TK_RANGE);
+    return -1;
+}
 // thread 0 of workgroup index pb (0-based among the ticketed workgroups):
 // the unit (b << 2) | m of block b -- m = 0 the whole block; with split > 0
 // the last `split` blocks of every range are dealt as two half units each,
 // m = 1 and 2 (their first and second halves of symbols), so that the
-// schedule ends on units half as long (k_demod_td1024); -1: none left
-__device__ __forceinline__ long long take_unit(unsigned long long *set, long long nb, long long k0, long long pb,
+// schedule ends on units half as long (k_demod_td1024); -1: none left.
+// Every block index formed is in [0, nb).
+__device__ __forceinline__ long long take_unit(const Tickets &tk, long long nb, long long k0, long long pb,
                                                long long split) {
     const long long per = (nb + 7) / 8;
     if (pb < 8 * k0) {  // the static first round
@@ -340,11 +380,8 @@ __device__ __forceinline__ long long take_unit(unsigned long long *set, long lon
         const long long avail = cnt - s0;  // ticketed blocks of range y
         if (avail <= 0) continue;
         const long long ns = split < avail ? split : avail, whole = avail - ns;
-        const long long units = whole + 2 * ns;
-        gu64 *p = (gu64 *)(set + y * TICKET_STRIDE);
-        if ((long long)__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= units) continue;
-        const long long t = (long long)__hip_atomic_fetch_add(p, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (t >= units) continue;
+        const long long t = take_ticket(tk, y, whole + 2 * ns);
+        if (t < 0) continue;
         const long long b0 = (long long)y * per + s0;
         if (t < whole) return (b0 + t) << 2;
         const long long u = t - whole;
@@ -352,20 +389,12 @@ __device__ __forceinline__ long long take_unit(unsigned long long *set, long lon
     }
     return -1;
 }
-// the workgroup's unit: thread 0 takes it (workgroup 0 also zeroes the
-// other counter set), everyone reads it from `slot` (an LDS word nothing
-// else touches before the caller's next barrier); SGPR-uniform result
-__device__ __forceinline__ long long wg_take_unit(unsigned long long *tickets, int par, long long nb, long long k0,
-                                                  long long pb, long long split, long long *slot) {
-    if (threadIdx.x == 0) {
-        if (pb == 0) {
-            unsigned long long *nxt = tickets + (par ^ 1) * TICKET_SET;
-#pragma unroll
-            for (int y = 0; y < 8; ++y)
-                __hip_atomic_store((gu64 *)(nxt + y * TICKET_STRIDE), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        *slot = take_unit(tickets + par * TICKET_SET, nb, k0, pb, split);
-    }
+// the workgroup's unit: thread 0 takes it, everyone reads it from `slot` (an
+// LDS word nothing else touches before the caller's next barrier);
+// SGPR-uniform result
+__device__ __forceinline__ long long wg_take_unit(const Tickets &tk, long long nb, long long k0, long long pb,
+                                                  long long split, long long *slot) {
+    if (threadIdx.x == 0) *slot = take_unit(tk, nb, k0, pb, split);
     __syncthreads();
     const long long v = *slot;
     const int lo = __builtin_amdgcn_readfirstlane((int)(v & 0xffffffffll));
@@ -373,9 +402,9 @@ __device__ __forceinline__ long long wg_take_unit(unsigned long long *tickets, i
     return (long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
 // whole blocks only: the block index, -1 when none is left
-__device__ __forceinline__ long long wg_take_block(unsigned long long *tickets, int par, long long nb, long long k0,
-                                                   long long pb, long long *slot) {
-    const long long u = wg_take_unit(tickets, par, nb, k0, pb, 0, slot);
+__device__ __forceinline__ long long wg_take_block(const Tickets &tk, long long nb, long long k0, long long pb,
+                                                   long long *slot) {
+    const long long u = wg_take_unit(tk, nb, k0, pb, 0, slot);
     return u < 0 ? u : u >> 2;
 }
 // The over-subscribed grid of a ticketed kernel: every workgroup takes at

@@ -947,9 +947,14 @@ k_zf_wstat(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__rest
                     const mf4 v = hi ? mf4{rx, ry, acc[p][g][2], acc[p][g][3]} : mf4{acc[p][g][0], acc[p][g][1], rx, ry};
                     const int m = mr0 + 2 * p + (hi ? 1 : 0);
                     if (s < send && m < M && kp < K) {
-                        float2 *o = out + (s * M + m) * (long long)K + kp;
-                        if (kp + 1 < K) *reinterpret_cast<mf4 *>(o) = v;
-                        else *o = float2{v[0], v[1]};
+                        const long long e = (s * M + m) * (long long)K + kp;
+                        float2 *o = out + e;
+                        if (kp + 1 < K && !(e & 1)) {
+                            *reinterpret_cast<mf4 *>(o) = v;  // 16-B aligned (out is)
+                        } else {  // the row's last bin, or an odd K's odd row: 8-B pieces
+                            o[0] = float2{v[0], v[1]};
+                            if (kp + 1 < K) o[1] = float2{v[2], v[3]};
+                        }
                     }
                 }
             }

@@ -76,11 +76,30 @@ _SIGS = {
     "ofdm_zf_transpose": (_I, [_P, _I, _I, _I, _P, _P]),
     "ofdm_zf_apply": (_I, [_P, _P, _I, _I, _I, _LL, _P, _P]),
     "ofdm_zf_detect": (_I, [_P, _P, _I, _I, _I, _LL, _P, _P]),
-    "ofdm_hbm_probe": (_I, [_I, _P, _P, _c.c_size_t, _P]),
+    "ofdm_hbm_probe": (_I, [_I, _P, _P, _c.c_size_t, _c.c_size_t, _P]),
+    "ofdm_device_status": (_I, []),
+    "ofdm_device_status_inject": (_I, [_c.c_uint]),
     "ofdm_buffer_hash": (_I, [_P, _c.c_size_t, _P, _P]),
 }
 
 _lib = None
+
+
+def build_id():
+    """Identity of the product library's build: the first 16 hex digits of
+    a SHA-256 over its sources (csrc/, the Makefile, include/ofdm_lsmrc.h),
+    in sorted order.  PMC profiles record it (scripts/pmc_summary.py) and
+    bench.py attaches a profile's traffic only to the build it measured."""
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(HERE, "csrc")
+    files = [os.path.join(csrc, f) for f in sorted(os.listdir(csrc))] + [os.path.join(HERE, "Makefile"), HEADER_PATH]
+    for f in files:
+        if os.path.isfile(f):
+            h.update(os.path.basename(f).encode() + b"\0")
+            with open(f, "rb") as fp:
+                h.update(fp.read())
+    return h.hexdigest()[:16]
 
 
 class OfdmError(RuntimeError):
@@ -147,8 +166,15 @@ def hbm_probe(mode, src, dst, stream=None):
     """Box probe: mode 0 copies src -> dst (float4), mode 1 reads src (dst:
     >= 1 MiB of partial sums).  Byte tensors on the device, 16-B multiples."""
     nbytes = src.numel() * src.element_size()
-    _check(lib().ofdm_hbm_probe(mode, _dptr(src, "src"), _dptr(dst, "dst"), nbytes, _stream(stream)),
+    _check(lib().ofdm_hbm_probe(mode, _dptr(src, "src"), _dptr(dst, "dst"), nbytes, dst.numel() * dst.element_size(),
+                                _stream(stream)),
            "ofdm_hbm_probe")
+
+
+def device_status():
+    """Raises OfdmError (OFDM_E_DEVICE) if a ticketed launch reported a fault
+    since the last check, and clears it (include/ofdm_lsmrc.h)."""
+    _check(lib().ofdm_device_status(), "ofdm_device_status")
 
 
 def _check(rc, fn):

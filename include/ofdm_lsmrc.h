@@ -47,7 +47,9 @@ enum {
     OFDM_E_ARG = -1,         /* invalid argument (shape, null, alignment) */
     OFDM_E_HIP = -2,         /* HIP runtime / launch failure */
     OFDM_E_UNSUPPORTED = -3, /* shape not supported by this build */
-    OFDM_E_IO = -4           /* file I/O */
+    OFDM_E_IO = -4,          /* file I/O */
+    OFDM_E_DEVICE = -5       /* an EARLIER launch reported a fault from the device (see
+                                ofdm_device_status); its output may be incomplete */
 };
 
 int ofdm_version(void);
@@ -145,6 +147,30 @@ int ofdm_dist_sqrd(const ofdm_cf32 *d_H, int R, int K, float *d_Hsqrd, ofdm_stre
  * launches and records it only after every launch was enqueued, so a failed
  * estimate leaves a workspace that the consumers refuse. */
 size_t ofdm_frame_workspace_bytes(long long nframes, int S, int R, int C);
+
+/* Work tickets.  The C = 1024 one-launch demod and the C = 2048 / 4096 MRC
+ * kernels (ofdm_frame_demod, _combine, _mrc_partial(_range),
+ * ofdm_symbols_demod) deal their blocks to workgroups at run time through 8
+ * counter words in the workspace (after the flag words).  These entry points
+ * therefore WRITE the workspace, ofdm_symbols_demod's const d_ws included.
+ * A counter holds tag << 32 | count with a per-launch tag, so whatever the
+ * words hold when a launch starts (zeros, an earlier launch's counts, an
+ * estimate of another geometry, recycled memory) is claimed afresh and never
+ * consumed as a count: no zeroing, release or registry state is needed for
+ * them.  One workspace serves one launch at a time (one stream, as for its
+ * estimate).  Two ticketed launches that overlap on one workspace either
+ * both complete (a block may be processed twice: same bytes) or one of them
+ * sees the other's tag and raises the sticky device status below.
+ *
+ * Sticky device status: a library-owned, host-mapped word that ticketed
+ * launches set when they meet a counter they cannot trust.  Every ticketed
+ * entry point reads it first (no synchronisation) and, if set, clears it and
+ * returns OFDM_E_DEVICE without launching anything; ofdm_device_status()
+ * does the same on demand (synchronise the stream first to see the status of
+ * launches still in flight).  ofdm_device_status_inject() ORs `bits` into
+ * the status (tests of the reporting path; no device needed). */
+int ofdm_device_status(void);
+int ofdm_device_status_inject(unsigned bits);
 
 /* Drops what the registry above knows about d_ws.  Call it before the memory
  * is freed (or handed to another user): a workspace later allocated at the
@@ -405,10 +431,14 @@ int ofdm_buffer_hash(const void *d_buf, size_t bytes, unsigned long long *d_hash
 
 /* Box probe for bench.py (no reference counterpart): mode 0 copies `bytes`
  * from d_src to d_dst, mode 1 reads them (d_dst receives 1024 x 256 float
- * partial sums, 1 MiB): every wave streams 16 KiB chunks with 16 non-temporal
- * 16-B loads per lane in flight -- the receivers' access pattern.  `bytes`
- * and both pointers 16-B aligned. */
-int ofdm_hbm_probe(int mode, const void *d_src, void *d_dst, size_t bytes, ofdm_stream_t stream);
+ * partial sums, OFDM_HBM_PROBE_SINK_BYTES): every wave streams 16 KiB chunks
+ * with 16 non-temporal 16-B loads per lane in flight -- the receivers' access
+ * pattern.  `bytes` and both pointers 16-B aligned; dst_bytes = the size of
+ * d_dst, at least `bytes` (mode 0) or OFDM_HBM_PROBE_SINK_BYTES (mode 1),
+ * else OFDM_E_ARG. */
+#define OFDM_HBM_PROBE_SINK_BYTES (1024 * 256 * 4)
+int ofdm_hbm_probe(int mode, const void *d_src, void *d_dst, size_t bytes, size_t dst_bytes,
+                   ofdm_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -1,7 +1,8 @@
 /* fft_fast.c -- TEST INFRASTRUCTURE ONLY (bench.py's timed CPU baseline).
  *
  * A single-precision complex FFT for power-of-two sizes written so that the
- * compiler vectorises it (Makefile: -O3 -march=x86-64-v3, i.e. AVX2 + FMA):
+ * compiler vectorises it (AVX2 code generation in fft_row_avx2 only, entered
+ * behind a runtime CPU check; -ffp-contract=off, so no FMA contraction):
  * split real / imaginary arrays, a precomputed bit-reversal table, and per
  * stage a contiguous twiddle table (stage of half-length h: w[h + k] =
  * exp(-2 pi i k / 2h), k < h), so the butterfly loop over k reads every
@@ -54,8 +55,9 @@ static const plan_t *plan_for(int log2c) {
     return np;
 }
 
-void oracle_fft_row_fast(oracle_cf32 *row, int C) {
-    if (C < 4 || C > 8192 || (C & (C - 1))) { oracle_fft_row_f32(row, C); return; }
+/* the vectorised body: AVX2 code generation for this function only, entered
+ * only on a CPU that has AVX2 (oracle_fft_row_fast below) */
+__attribute__((target("avx2"))) static void fft_row_avx2(oracle_cf32 *row, int C) {
     int log2c = 0;
     while ((1 << log2c) < C) ++log2c;
     const plan_t *p = plan_for(log2c);
@@ -95,4 +97,12 @@ void oracle_fft_row_fast(oracle_cf32 *row, int C) {
         row[i].re = re[i];
         row[i].im = im[i];
     }
+}
+
+void oracle_fft_row_fast(oracle_cf32 *row, int C) {
+    if (C < 4 || C > 8192 || (C & (C - 1)) || !__builtin_cpu_supports("avx2")) {
+        oracle_fft_row_f32(row, C);  /* the same butterflies in the same order: identical bits */
+        return;
+    }
+    fft_row_avx2(row, C);
 }

@@ -20,4 +20,5 @@ else
 fi
 make -C $W/pkg -j${MAKE_JOBS:-8} LIB=lib/libofdm_lsmrc.so > $W/build.log 2>&1 || { tail -20 $W/build.log; exit 1; }
 mkdir -p $ROOT/$PKG/lib && cp $W/pkg/lib/libofdm_lsmrc.so $ROOT/$PKG/lib/libofdm_lsmrc_$NAME.so
+rm -rf $W   # the .so is all abx.py needs; keep no source copies in the tree
 echo "built $PKG/lib/libofdm_lsmrc_$NAME.so"

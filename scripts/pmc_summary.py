@@ -89,6 +89,7 @@ def main():
            "mrc_avg_ns_rocprof": float(mrc_stat[0]["AverageNs"]) if mrc_stat else None,
            "ls_avg_ns_rocprof": float(ls_stat[0]["AverageNs"]) if ls_stat else None,
            "correction": "2*FETCH_SIZE + WRITE_SIZE (KiB->B); MI355X_MICROARCH.md HBM section",
+           "build_id": bench.get("build_id"),  # the library the profiled run loaded (ofdm_lsmrc.build_id)
            "source": f"profiles/{tag}_pmc.csv"}
     if "notraffic" not in sys.argv[3:]:  # the default-config summary bench.py reads
         with open(os.path.join(prof, "pmc_traffic.json"), "w") as fp:

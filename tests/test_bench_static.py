@@ -91,3 +91,28 @@ def test_stamps_summary_clock():
     assert st["workgroups"] == 3
     assert abs(st["effective_GHz_median"] - 2.0) < 1e-9
     assert abs(st["stamped_span_ms"] - 1002 * 1e-5) < 1e-12
+
+
+def test_pmc_traffic_only_for_the_profiled_build(tmp_path):
+    """roofline.traffic is attached only from a profile
+    whose recorded build id is the running library's (ofdm_lsmrc.build_id);
+    a profile of other code gives null and says so."""
+    import importlib.util
+    import json
+    import sys
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    cfg = {"R": 3, "C": 1024, "S": 7, "frames_per_gpu": 5, "prefix": 0, "domain": "time", "flow": "one-launch"}
+    p = tmp_path / "t.json"
+    with open(p, "w") as fp:
+        json.dump({"config": dict(cfg), "mrc_hbm_bytes_per_launch": 123.0, "build_id": "abc"}, fp)
+    val, src = bench.pmc_traffic(str(p), cfg, "abc")
+    assert val == 123.0 and src.endswith("t.json")
+    assert bench.pmc_traffic(str(p), cfg, "def") == (None, "no profile of this build")
+    sys.path.insert(0, os.path.join(ROOT, "gpu-accel-ofdm-ls-mrc_amd"))
+    import ofdm_lsmrc
+    bid = ofdm_lsmrc.build_id()
+    assert len(bid) == 16 and int(bid, 16) >= 0 and bid == ofdm_lsmrc.build_id()
+    assert '"build_id": build' in _src("bench.py")
+    assert '"build_id": bench.get("build_id")' in _src("scripts/pmc_summary.py")

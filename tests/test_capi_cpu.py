@@ -148,8 +148,7 @@ def test_product_library_dispatches_only_product_kernels(ofdm):
 
 def test_workspace_sizes(ofdm):
     # fused C=1024: Hc [F][R][C] + P [F][C] + one flag word per frame + the
-    # four sets of 8 work-ticket counters (one 128-B line each: two for eager
-    # launches, one (+ the one it zeroes) for launches captured into graphs), no staging
+    # 4-KiB ticket area (8 work-ticket counters, one 128-B line each), no staging
     F, S, R, C = 100, 101, 16, 1024
     b = ofdm.workspace_bytes(F, S, R, C)
     assert b == F * R * C * 8 + F * C * 4 + (F * 8 + 255) // 256 * 256 + 4 * 8 * 128
@@ -181,3 +180,44 @@ def test_pipeline_argument_validation_without_device(ofdm):
     assert L.ofdm_pipeline_sync(None) == -1
     assert L.ofdm_pipeline_destroy(None) == 0
     assert L.ofdm_host_register(None, 10) == -1
+
+
+def test_device_status_reporting_without_device(ofdm):
+    """The sticky device status (include/ofdm_lsmrc.h): once raised, the next
+    work-ticketed entry returns OFDM_E_DEVICE (-5) before validating or
+    launching anything and clears it; entries without tickets ignore it;
+    ofdm_device_status() reports and clears it on demand."""
+    L = ofdm.lib()
+    P = ctypes.c_void_p
+    fake, ws = P(4096), P(1 << 20)
+    assert L.ofdm_device_status() == 0
+    need = L.ofdm_frame_workspace_bytes(2, 5, 8, 4096)
+    ticketed = [
+        lambda: L.ofdm_frame_demod(None, 1, 1, 4, 1024, 0, None, None, 0, None, None),
+        lambda: L.ofdm_frame_demod_ex(None, 1, 1, 4, 1024, 0, None, None, 0, None, 0, -1, None),
+        lambda: L.ofdm_frame_combine(fake, 2, 5, 8, 4096, 0, ws, need, fake, None),
+        lambda: L.ofdm_frame_mrc_partial(fake, 2, 5, 8, 4096, 0, ws, need, fake, None),
+        lambda: L.ofdm_frame_mrc_partial_range(fake, 2, 0, 2, 5, 8, 4096, 0, ws, need, fake, None),
+        lambda: L.ofdm_symbols_demod(fake, 1, 8, 4096, 0, ws, need, 0, fake, None),
+    ]
+    for call in ticketed:
+        assert L.ofdm_device_status_inject(1) == 0
+        assert L.ofdm_fft_rows(fake, fake, 1, 8193, 0, None) == -3  # no tickets: not consumed here
+        assert call() == -5
+        assert b"work-ticket" in L.ofdm_last_error() and b"foreign count" in L.ofdm_last_error()
+        assert call() == -1  # cleared: the call's own validation speaks again
+    assert L.ofdm_device_status_inject(2 | 4) == 0
+    assert L.ofdm_device_status() == -5
+    assert b"count out of range" in L.ofdm_last_error() and b"contended" in L.ofdm_last_error()
+    assert L.ofdm_device_status() == 0
+
+
+def test_hbm_probe_refuses_small_destination(ofdm):
+    """ofdm_hbm_probe checks d_dst's size before launching."""
+    L = ofdm.lib()
+    P = ctypes.c_void_p
+    fake = P(4096)
+    assert L.ofdm_hbm_probe(0, fake, fake, 1 << 20, (1 << 20) - 16, None) == -1
+    assert b"d_dst holds" in L.ofdm_last_error()
+    assert L.ofdm_hbm_probe(1, fake, fake, 1 << 20, (1 << 20) - 16, None) == -1
+    assert L.ofdm_hbm_probe(2, fake, fake, 1 << 20, 1 << 20, None) == -1

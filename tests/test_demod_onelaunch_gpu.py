@@ -201,8 +201,8 @@ def test_frame_demod_ex_rejects_unknown_flow(ofdm, dev):
 def test_work_tickets_reused_workspace(ofdm, dev):
     """Work tickets (wave_fft1024.hpp take_unit): a batch large enough for
     ticketed blocks and half units, demodulated 4 times in turn with another
-    batch on ONE workspace -- every launch counts in the counter set the
-    previous launch zeroed; every output must match its two-launch
+    batch on ONE workspace -- every launch claims the counters the previous
+    launch left (tagged counts); every output must match its two-launch
     reference, and a repeat must be bit-identical (the schedule changes
     which workgroup takes a block, never the block's arithmetic)."""
     import torch
@@ -257,8 +257,8 @@ def test_work_tickets_cover_every_unit(ofdm, dev, F):
 @pytest.mark.parametrize("C,F,R", [(2048, 64, 4), (4096, 16, 4)])
 def test_graph_capture_ticketed_receivers(ofdm, dev, C, F, R):
     """The work-ticketed C = 2048 / 4096 receivers captured into a graph:
-    every replay counts in the capture counter set behind a zeroing kernel
-    node of its own, so replays after the first, and eager launches on the same
+    the launch's tag is frozen in the graph, so every replay counts behind a
+    zeroing kernel node of its own; replays after the first, and eager launches on the same
     workspace in between, still process every unit (outputs NaN-filled
     before each run; bit-identical to eager launches on a fresh workspace)."""
     import torch
@@ -296,8 +296,9 @@ def test_work_tickets_workspace_shared_by_two_geometries(ofdm, dev, C, Fbig, Fsm
     """One workspace (sized for the larger batch) used in turn by batches of
     two sizes: the work-ticket counters follow the estimate, at an offset that
     depends on the batch, and the smaller batch's counters lie inside the
-    larger batch's estimate, so a call with the other geometry must zero them
-    again (NaN-filled outputs; bit-identical to fresh workspaces)."""
+    larger batch's estimate, so a call with the other geometry meets
+    estimate bytes there and must claim them afresh (NaN-filled outputs;
+    bit-identical to fresh workspaces)."""
     import torch
     S, R = 101, 2
     X = pilots(dev, C - 1, seed=7)
@@ -361,3 +362,111 @@ def test_many_small_frames(ofdm, dev, C, F, S, R):
     out.fill_(float("nan"))
     ofdm.frame_demod(iq, X, 0, out=out)
     parity(host(out), two_launch(ofdm, iq, X, 0), erel_tol=2e-3)
+
+
+def ticket_words(ws, F, R, C):
+    """The workspace's work-ticket counters (capi.cpp carve: Hc [F][R][C],
+    P [F][C] and one flag word per frame, each padded to 256 B, then 8
+    counters 128 B apart) as int64 words."""
+    import torch
+    up = lambda x: (x + 255) // 256 * 256
+    off = up(F * R * C * 8) + up(F * C * 4) + up(F * 8)
+    return ws[off:off + 1024].view(torch.int64)
+
+
+@pytest.mark.parametrize("C,F,R", [(1024, 150, 3), (2048, 40, 4), (4096, 16, 4)])
+def test_work_tickets_garbage_counters(ofdm, dev, C, F, R):
+    """the ticket area of a workspace the registry knows
+    (filled by an earlier demod, never released) overwritten with all-ones
+    words, then small and large positive counts, then random bytes, before
+    each ofdm_frame_demod: every word is claimed afresh by its tag, so every
+    unit is processed (NaN-filled output) and the output is bit-identical to
+    a fresh workspace's; no device fault is reported.  (Before round 6 a
+    positive stale count skipped units and a negative one faulted at C =
+    4096: gpurun_out/r5t/old.log.)"""
+    import torch
+    S = 101
+    X = pilots(dev, C - 1, seed=C + 3)
+    iq = ofdm.synth_frames(F, S, R, C, X, seed=C + 33, noise_std=0.01)
+    ref = ofdm.frame_demod(iq, X, 0)
+    ws = ofdm.workspace(F, S, R, C, dev)
+    ofdm.frame_demod(iq, X, 0, ws=ws)
+    torch.cuda.synchronize()
+    words = ticket_words(ws, F, R, C)
+    g = torch.Generator(device="cpu").manual_seed(C)
+    for fill in (-1, 3, 1 << 20, (7 << 32) | 5, None):
+        if fill is None:
+            words.copy_(torch.randint(-(1 << 62), 1 << 62, words.shape, generator=g))
+        else:
+            words.fill_(fill)
+        out = ofdm.c64((F, S - 1, C - 1), dev)
+        out.fill_(float("nan"))
+        ofdm.frame_demod(iq, X, 0, ws=ws, out=out)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref), fill
+    ofdm.device_status()
+
+
+@pytest.mark.parametrize("C,Fs", [(2048, 40), (4096, 16)])
+def test_work_tickets_after_freq_estimate_of_other_geometry(ofdm, dev, C, Fs):
+    """ofdm_frame_demod at a small batch, then
+    ofdm_frame_demod_freq at a batch twice as large on the same workspace
+    (its estimate covers the small batch's counters; no ticketed launch sees
+    it), then the small ofdm_frame_demod again: its counters hold estimate
+    bytes and must be claimed afresh (NaN-filled output, bit-identical to a
+    fresh workspace)."""
+    import torch
+    S, R = 101, 2
+    Fb = 2 * Fs
+    X = pilots(dev, C - 1, seed=C + 5)
+    small = ofdm.synth_frames(Fs, S, R, C, X, seed=C + 51, noise_std=0.01)
+    big_td = ofdm.synth_frames(Fb, S, R, C, X, seed=C + 52, noise_std=0.01)
+    big = ofdm.fft_rows(big_td.clone())
+    del big_td
+    ref = ofdm.frame_demod(small, X, 0)
+    ref_big = ofdm.frame_demod_freq(big, X)
+    ws = ofdm.workspace(Fb, S, R, C, dev)
+    for k in range(2):
+        out = ofdm.c64((Fs, S - 1, C - 1), dev)
+        out.fill_(float("nan"))
+        ofdm.frame_demod(small, X, 0, ws=ws, out=out)
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref), k
+        ob = ofdm.frame_demod_freq(big, X, ws=ws)
+        torch.cuda.synchronize()
+        assert torch.equal(ob, ref_big)
+    ofdm.device_status()
+
+
+def test_work_tickets_one_workspace_two_streams(ofdm, dev):
+    """one estimate read by ofdm_frame_combine on two
+    streams at once -- against the header's one-launch-at-a-time rule for a
+    workspace.  Tagged counters make the overlap safe or loud: every output
+    is complete and equal to the serial one, or the device status reports
+    the overlap (OFDM_E_DEVICE); never a silently incomplete output."""
+    import torch
+    C, F, S, R = 4096, 16, 101, 4
+    X = pilots(dev, C - 1, seed=44)
+    iq = ofdm.synth_frames(F, S, R, C, X, seed=45, noise_std=0.01)
+    ws = ofdm.workspace(F, S, R, C, dev)
+    ofdm.frame_estimate(iq, X, 0, ws)
+    ref = ofdm.frame_combine(iq, 0, ws, ofdm.c64((F, S - 1, C - 1), dev))
+    torch.cuda.synchronize()
+    sts = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = [[ofdm.c64((F, S - 1, C - 1), dev) for _ in range(2)] for _ in range(4)]
+    for o in outs:
+        for t in o:
+            t.fill_(float("nan"))
+    torch.cuda.synchronize()
+    for rep in range(4):
+        for i in (0, 1):
+            ofdm.frame_combine(iq, 0, ws, outs[rep][i], stream=sts[i])
+    torch.cuda.synchronize()
+    try:
+        ofdm.device_status()
+        reported = False
+    except ofdm.OfdmError as e:
+        assert "work-ticket" in str(e)
+        reported = True
+    bad = [(rep, i) for rep in range(4) for i in (0, 1) if not torch.equal(outs[rep][i], ref)]
+    assert not bad or reported, bad
