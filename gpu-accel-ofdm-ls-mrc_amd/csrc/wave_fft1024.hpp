@@ -391,10 +391,25 @@ __device__ __forceinline__ long long take_unit(const Tickets &tk, long long nb, 
 }
 // the workgroup's unit: thread 0 takes it, everyone reads it from `slot` (an
 // LDS word nothing else touches before the caller's next barrier);
-// SGPR-uniform result
+// SGPR-uniform result.  Workgroup 0 (a static block of the first round,
+// which takes no ticket) claims the 8 counters for this launch -- (tag, 0)
+// -- about a block's time before the first ticket is taken, so that the
+// tickets normally meet their tag and cost one add, as untagged counters did
+// (the compare-and-swap claim costs 1.3 % at configs[1] without it, profiles/
+// r6/r6a_split_estimator_ab_cfg1.jsonl "tk").  Should the claim land after
+// tickets were taken, it re-deals them: blocks processed twice, the same
+// bytes stored twice; no unit is ever skipped.
 __device__ __forceinline__ long long wg_take_unit(const Tickets &tk, long long nb, long long k0, long long pb,
                                                   long long split, long long *slot) {
-    if (threadIdx.x == 0) *slot = take_unit(tk, nb, k0, pb, split);
+    if (threadIdx.x == 0) {
+        if (pb == 0) {
+#pragma unroll
+            for (int y = 0; y < 8; ++y)
+                __hip_atomic_store((gu64 *)(tk.set + y * TICKET_STRIDE), (unsigned long long)tk.tag << 32,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        *slot = take_unit(tk, nb, k0, pb, split);
+    }
     __syncthreads();
     const long long v = *slot;
     const int lo = __builtin_amdgcn_readfirstlane((int)(v & 0xffffffffll));
