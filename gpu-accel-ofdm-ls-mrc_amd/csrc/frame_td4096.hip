@@ -13,8 +13,10 @@
 // Lane (q, a) of wave e owns bins 4 b + e and 4 b + 2 + e, b = b0(t) + 16 k.
 //
 // Hc "lane order" for C = 4096: per (frame, antenna) 4096 float2 in planes
-// [e][h][k][t]: float2 e*2048 + h*1024 + k*64 + t = Hc[4 b + 2 h + e] with
-// b = b0(t) + 16 k -- each plane one coalesced 512-B wave load per k.
+// [e][h][k >> 1][t][k & 1]: float2 e*2048 + h*1024 + (k >> 1)*128 + 2 t +
+// (k & 1) = Hc[4 b + 2 h + e] with b = b0(t) + 16 k -- lane t's bins k and
+// k + 1 side by side, so that the MRC kernel reads a plane from LDS as 8
+// ds_read_b128 (4 LDS cycles each) instead of 8 ds_read2st64_b64 (8 each).
 // P bin-indexed [F][C].  The LS kernel (one read per frame) uses the direct
 // form above, each wave reading the whole row.
 //
@@ -115,18 +117,22 @@ __device__ __forceinline__ void ls_rows(const float2 *pilot, int Cp, int R, int 
     for (int r = j; r < R; r += LS_PAIRS) {
         float2 xe[16], xo[16];
         row_fft4096<E, false>(pilot + (long long)r * Cp, t, T, lds, xe, xo);
-        float2 *hr = Hf + (long long)r * C + E * 2048;
+        float4 *hr = reinterpret_cast<float4 *>(Hf + (long long)r * C + E * 2048);
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const int be = 4 * (b0 + 16 * k) + E;
-            // divideOneRow + conj (cpuLS.hpp:233-244, 303-307); DC bin dropped
-            float2 he = ls_conj(xe[k], xs[be]);
-            if (be == 0) he = float2{0.f, 0.f};
-            const float2 ho = ls_conj(xo[k], xs[be + 2]);
-            pe[k] = pe[k] + (he.x * he.x) + (he.y * he.y);  // findDistSqrd order
-            po[k] = po[k] + (ho.x * ho.x) + (ho.y * ho.y);
-            hr[k * 64 + t] = he;
-            hr[1024 + k * 64 + t] = ho;
+        for (int k = 0; k < 16; k += 2) {
+            float2 he[2], ho[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int be = 4 * (b0 + 16 * (k + i)) + E;
+                // divideOneRow + conj (cpuLS.hpp:233-244, 303-307); DC bin dropped
+                he[i] = ls_conj(xe[k + i], xs[be]);
+                if (be == 0) he[i] = float2{0.f, 0.f};
+                ho[i] = ls_conj(xo[k + i], xs[be + 2]);
+                pe[k + i] = pe[k + i] + (he[i].x * he[i].x) + (he[i].y * he[i].y);  // findDistSqrd order
+                po[k + i] = po[k + i] + (ho[i].x * ho[i].x) + (ho[i].y * ho[i].y);
+            }
+            hr[(k >> 1) * 64 + t] = float4{he[0].x, he[0].y, he[1].x, he[1].y};
+            hr[512 + (k >> 1) * 64 + t] = float4{ho[0].x, ho[0].y, ho[1].x, ho[1].y};
         }
     }
     __syncthreads();  // every wave is done with its transpose image (pp reuses it)
@@ -187,6 +193,30 @@ __global__ void __launch_bounds__(64 * NW) k_ls_td4096(const float2 *__restrict_
 // (pk.hpp) in the split, both FFT halves and the MAC.
 // ---------------------------------------------------------------------------
 constexpr int X_TAB = hl::TW1S + hl::TW2S;
+// The MRC kernel's transpose images: 16 rows of pitch TP4 = 72 float2, row
+// element c = a + 4 l (a < 4) at position 8 (l >> 1) + 2 a + (l & 1), so
+// that the second FFT half reads lane (q, a)'s values l = 2 j, 2 j + 1 as
+// ONE 16-B ds_read_b128 at q TP4 + 8 j + 2 a (4 LDS cycles; the hlds image
+// of pitch 68 gives ds_read2_b64, 8 cycles: MI355X_MICROARCH.md LDS table).
+// Conflict-free both ways: a transpose-write row covers 16 lanes x 8 B
+// contiguously per lane group, and the four rows a ds_read_b128 lane group
+// reads start 16 dwords apart mod 64 (pitch 144 dwords).
+constexpr int TP4 = 72;
+constexpr int TS4 = 16 * TP4;
+__device__ __forceinline__ int perm4(int c) { return 8 * (c >> 3) + 2 * (c & 3) + ((c >> 2) & 1); }
+__device__ __forceinline__ void fa_write4(const pk::v2f (&v)[16], int pt, float2 *T) {
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2) T[k2 * TP4 + pt] = pk::F(v[k2]);
+}
+__device__ __forceinline__ void fb_read4(int t, const float2 *T, pk::v2f (&v)[16]) {
+    const float4 *s = reinterpret_cast<const float4 *>(T + (t >> 2) * TP4 + 2 * (t & 3));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float4 x = s[4 * j];  // float2 offset 8 j
+        v[2 * j] = pk::V(float2{x.x, x.y});
+        v[2 * j + 1] = pk::V(float2{x.z, x.w});
+    }
+}
 
 template <int CM, int M>
 __device__ __forceinline__ pk::v2f dif_tw(pk::v2f base) {  // base * W64^(CM * M)
@@ -222,7 +252,7 @@ __device__ __forceinline__ void dma_hc_row(const float2 *g, unsigned lds) {
 // faster here than 15 table reads per stage).
 template <int E, bool PREF>
 __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const float2 *__restrict__ hr,
-                                      int t, float2 *T, const float2 *Tp, const float2 *tw1,
+                                      int t, int pt, float2 *T, const float2 *Tp, const float2 *tw1,
                                       const float2 *tw2, pk::v2f wb0, pk::v2f wb1, float2 (&a)[16],
                                       float2 (&b)[16], float2 (&ae)[16], float2 (&ao)[16],
                                       const float2 *hnext, unsigned hb_next) {
@@ -234,16 +264,28 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
         v[m] = sub(V(a[m]), V(b[m]));  // d
     }
     float2 h[16];
-    // wave 0 sends d and keeps s (= a); wave 1 sends s (= c) and keeps d
+    // wave 0 sends d and keeps s (= a); wave 1 sends s (= c) and keeps d:
+    // 16-B pieces [m >> 1][t] (ds_write_b128 / ds_read_b128)
+    float4 *T4 = reinterpret_cast<float4 *>(T);
+    const float4 *Tp4 = reinterpret_cast<const float4 *>(Tp);
 #pragma unroll
-    for (int m = 0; m < 16; ++m) T[hl::swz(m, t)] = F(E ? u[m] : v[m]);
+    for (int m = 0; m < 16; m += 2) {
+        const float2 x0 = F(E ? u[m] : v[m]), x1 = F(E ? u[m + 1] : v[m + 1]);
+        T4[(m >> 1) * 64 + t] = float4{x0.x, x0.y, x1.x, x1.y};
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this row's Hc DMA landed
     td1024::lds_barrier();
     if (hnext) dma_hc_row(hnext, hb_next);
 #pragma unroll
-    for (int m = 0; m < 16; ++m) {
-        if (E) u[m] = V(Tp[hl::swz(m, t)]);  // b
-        else v[m] = V(Tp[hl::swz(m, t)]);    // c
+    for (int m = 0; m < 16; m += 2) {
+        const float4 x = Tp4[(m >> 1) * 64 + t];
+        if (E) {  // b
+            u[m] = V(float2{x.x, x.y});
+            u[m + 1] = V(float2{x.z, x.w});
+        } else {  // c
+            v[m] = V(float2{x.x, x.y});
+            v[m + 1] = V(float2{x.z, x.w});
+        }
     }
     td1024::lds_barrier();  // the partner has read T before the FFT reuses it
     // E = 0: u = a, v = c:  z0 = a + c, z2 = (a - c) W^(2 n0)
@@ -286,14 +328,19 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
     // reads, consumed after B's radix-16
     const hl::TwAnchors a_tw = hl::anchors_a(tw1, t);
     hl::fa_compute(u, a_tw);
-    hl::fa_write(u, t, T);
-    hl::fb_read(t, T, xu);
+    fa_write4(u, pt, T);
+    fb_read4(t, T, xu);
     hl::fa_compute(v, a_tw);
-    hl::fa_write(v, t, T);
-    hl::fb_read(t, T, u);  // u's registers are free: v's transpose lands in them
+    fa_write4(v, pt, T);
+    fb_read4(t, T, u);  // u's registers are free: v's transpose lands in them
     __builtin_amdgcn_sched_barrier(0);
+    const float4 *hr4 = reinterpret_cast<const float4 *>(hr);
 #pragma unroll
-    for (int k = 0; k < 16; ++k) h[k] = hr[k * 64 + t];  // plane 0, lands during B(u)
+    for (int k = 0; k < 16; k += 2) {  // plane 0, lands during B(u)
+        const float4 x = hr4[(k >> 1) * 64 + t];
+        h[k] = float2{x.x, x.y};
+        h[k + 1] = float2{x.z, x.w};
+    }
     hl::TwAnchors b_tw = hl::anchors_b(tw2, t);
     __builtin_amdgcn_sched_barrier(0);
     hl::fb_compute(xu, b_tw, t, x);
@@ -305,7 +352,11 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int k = 0; k < 16; ++k) h[k] = hr[1024 + k * 64 + t];  // plane 1, lands during B(v)
+    for (int k = 0; k < 16; k += 2) {  // plane 1, lands during B(v)
+        const float4 x = hr4[512 + (k >> 1) * 64 + t];
+        h[k] = float2{x.x, x.y};
+        h[k + 1] = float2{x.z, x.w};
+    }
     __builtin_amdgcn_sched_barrier(0);
     if (PREF) row_load<true>(next + 1024 * (E + 2), t, b);
     b_tw = hl::anchors_b(tw2, t);
@@ -331,7 +382,7 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
 // workgroup (8 waves, 2 per SIMD as the 242-VGPR x kernel) per CU.
 // ---------------------------------------------------------------------------
 constexpr int H_PAIRS = 4;
-constexpr size_t H_LDS = (size_t)(X_TAB + 2 * H_PAIRS * hl::TS + 2 * C) * sizeof(float2);
+constexpr size_t H_LDS = (size_t)(X_TAB + 2 * H_PAIRS * TS4 + 2 * C) * sizeof(float2);
 static_assert(H_LDS <= 160 * 1024, "one workgroup per CU");
 
 template <int E>
@@ -342,10 +393,11 @@ __device__ __forceinline__ void h_rows(const float2 *sym, int Cp, int R, const f
     row_load<true>(sym + 1024 * E, t, a);
     row_load<true>(sym + 1024 * (E + 2), t, b);
     const unsigned hb0 = lds_addr(HB), hb1 = lds_addr(HB + C);
+    const int pt = perm4(t);
     for (int r = 0; r + 1 < R; ++r)
-        x_row<E, true>(sym + (long long)(r + 1) * Cp, HB + (r & 1) * C + E * 2048, t, T, Tp, tw1, tw2, wb0, wb1, a,
+        x_row<E, true>(sym + (long long)(r + 1) * Cp, HB + (r & 1) * C + E * 2048, t, pt, T, Tp, tw1, tw2, wb0, wb1, a,
                        b, ae, ao, Hg + (long long)(r + 1) * C, (r & 1) ? hb0 : hb1);
-    x_row<E, false>(sym, HB + ((R - 1) & 1) * C + E * 2048, t, T, Tp, tw1, tw2, wb0, wb1, a, b, ae, ao, nullptr, 0);
+    x_row<E, false>(sym, HB + ((R - 1) & 1) * C + E * 2048, t, pt, T, Tp, tw1, tw2, wb0, wb1, a, b, ae, ao, nullptr, 0);
 }
 
 // The MRC of one logical block (H_PAIRS pairs = data symbols of frame f, pair
@@ -357,9 +409,9 @@ __device__ __forceinline__ void mrc4096_block(const float2 *__restrict__ iq, int
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), t = threadIdx.x & 63;
     const int e = w & 1, pair = w >> 1;
     const float2 *tw1 = lds, *tw2 = lds + hl::TW1S;
-    float2 *T = lds + X_TAB + w * hl::TS;
-    const float2 *Tp = lds + X_TAB + (w ^ 1) * hl::TS;
-    float2 *HB = lds + X_TAB + 2 * H_PAIRS * hl::TS;  // [2][C] Hc rows
+    float2 *T = lds + X_TAB + w * TS4;
+    const float2 *Tp = lds + X_TAB + (w ^ 1) * TS4;
+    float2 *HB = lds + X_TAB + 2 * H_PAIRS * TS4;  // [2][C] Hc rows
     const int nsym = S - 1;
     const float2 *Hg = Hc + f * (long long)R * C;
     dma_hc_row(Hg, lds_addr(HB));  // row 0; landed at the first row's barrier
@@ -395,7 +447,7 @@ __device__ __forceinline__ void mrc4096_block(const float2 *__restrict__ iq, int
             ao[k] = float2{ao[k].x / po, ao[k].y / po};
         }
     }
-    float2 *Tpair = lds + X_TAB + 2 * pair * hl::TS;  // images of waves 2 pair, 2 pair + 1
+    float2 *Tpair = lds + X_TAB + 2 * pair * TS4;  // images of waves 2 pair, 2 pair + 1
     td1024::lds_barrier();  // both waves are done with their last transposes
 #pragma unroll
     for (int h0 = 0; h0 < 4; h0 += 2) {
@@ -406,8 +458,8 @@ __device__ __forceinline__ void mrc4096_block(const float2 *__restrict__ iq, int
             const int jo = (mode & 1) ? be + 1 : out_pos(be + 1, K);
             const int he = je >> 10, ho = jo >> 10;
             if (be > 0 && (he >> 1) == (h0 >> 1))
-                Tpair[(he & 1) * hl::TS + ((je & 1023) >> 6) * hl::TP + (je & 63)] = ae[k];
-            if ((ho >> 1) == (h0 >> 1)) Tpair[(ho & 1) * hl::TS + ((jo & 1023) >> 6) * hl::TP + (jo & 63)] = ao[k];
+                Tpair[(he & 1) * TS4 + ((je & 1023) >> 6) * TP4 + (je & 63)] = ae[k];
+            if ((ho >> 1) == (h0 >> 1)) Tpair[(ho & 1) * TS4 + ((jo & 1023) >> 6) * TP4 + (jo & 63)] = ao[k];
         }
         td1024::lds_barrier();
         if (store) {
@@ -415,7 +467,7 @@ __device__ __forceinline__ void mrc4096_block(const float2 *__restrict__ iq, int
             for (int m = 0; m < 16; ++m) {
                 const int jj = 1024 * (h0 + e) + t + 64 * m;
                 if (jj < K)
-                    __builtin_nontemporal_store(__builtin_bit_cast(unsigned long long, T[m * hl::TP + t]),
+                    __builtin_nontemporal_store(__builtin_bit_cast(unsigned long long, T[m * TP4 + t]),
                                                 reinterpret_cast<unsigned long long *>(o + jj));
             }
         }

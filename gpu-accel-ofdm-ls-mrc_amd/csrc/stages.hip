@@ -97,9 +97,9 @@ __device__ __forceinline__ int hc_pos(int b, int C) {  // C = 0: bin layout
         const int q = b / 3, j = b - 3 * q, e = q & 3, kk = q >> 2;
         return e * 1536 + (8 * j + (kk >> 6)) * 64 + 8 * (kk & 7) + ((kk >> 3) & 7);
     }
-    if (C == 4096) {  // float2 e * 2048 + h * 1024 + k * 64 + t = Hc[4 b' + 2 h + e]
+    if (C == 4096) {  // float2 e * 2048 + h * 1024 + (k >> 1) * 128 + 2 t + (k & 1) = Hc[4 b' + 2 h + e]
         const int t = lane_of(b >> 2, k);
-        return (b & 1) * 2048 + ((b >> 1) & 1) * 1024 + k * 64 + t;
+        return (b & 1) * 2048 + ((b >> 1) & 1) * 1024 + (k >> 1) * 128 + 2 * t + (k & 1);
     }
     return b;
 }
