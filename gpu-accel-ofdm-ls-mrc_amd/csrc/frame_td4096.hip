@@ -193,30 +193,13 @@ __global__ void __launch_bounds__(64 * NW) k_ls_td4096(const float2 *__restrict_
 // (pk.hpp) in the split, both FFT halves and the MAC.
 // ---------------------------------------------------------------------------
 constexpr int X_TAB = hl::TW1S + hl::TW2S;
-// The MRC kernel's transpose images: 16 rows of pitch TP4 = 72 float2, row
-// element c = a + 4 l (a < 4) at position 8 (l >> 1) + 2 a + (l & 1), so
-// that the second FFT half reads lane (q, a)'s values l = 2 j, 2 j + 1 as
-// ONE 16-B ds_read_b128 at q TP4 + 8 j + 2 a (4 LDS cycles; the hlds image
-// of pitch 68 gives ds_read2_b64, 8 cycles: MI355X_MICROARCH.md LDS table).
-// Conflict-free both ways: a transpose-write row covers 16 lanes x 8 B
-// contiguously per lane group, and the four rows a ds_read_b128 lane group
-// reads start 16 dwords apart mod 64 (pitch 144 dwords).
-constexpr int TP4 = 72;
-constexpr int TS4 = 16 * TP4;
-__device__ __forceinline__ int perm4(int c) { return 8 * (c >> 3) + 2 * (c & 3) + ((c >> 2) & 1); }
-__device__ __forceinline__ void fa_write4(const pk::v2f (&v)[16], int pt, float2 *T) {
-#pragma unroll
-    for (int k2 = 0; k2 < 16; ++k2) T[k2 * TP4 + pt] = pk::F(v[k2]);
-}
-__device__ __forceinline__ void fb_read4(int t, const float2 *T, pk::v2f (&v)[16]) {
-    const float4 *s = reinterpret_cast<const float4 *>(T + (t >> 2) * TP4 + 2 * (t & 3));
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const float4 x = s[4 * j];  // float2 offset 8 j
-        v[2 * j] = pk::V(float2{x.x, x.y});
-        v[2 * j + 1] = pk::V(float2{x.z, x.w});
-    }
-}
+// The MRC kernel's transpose images: hlds::TP16 pitch (16-B reads of the
+// second FFT half, wave_fft1024.hpp)
+constexpr int TP4 = hl::TP16;
+constexpr int TS4 = hl::TS16;
+using hl::fa_write16;
+using hl::fb_read16;
+using hl::perm16;
 
 template <int CM, int M>
 __device__ __forceinline__ pk::v2f dif_tw(pk::v2f base) {  // base * W64^(CM * M)
@@ -328,11 +311,11 @@ __device__ __forceinline__ void x_row(const float2 *__restrict__ next, const flo
     // reads, consumed after B's radix-16
     const hl::TwAnchors a_tw = hl::anchors_a(tw1, t);
     hl::fa_compute(u, a_tw);
-    fa_write4(u, pt, T);
-    fb_read4(t, T, xu);
+    fa_write16(u, pt, T);
+    fb_read16(t, T, xu);
     hl::fa_compute(v, a_tw);
-    fa_write4(v, pt, T);
-    fb_read4(t, T, u);  // u's registers are free: v's transpose lands in them
+    fa_write16(v, pt, T);
+    fb_read16(t, T, u);  // u's registers are free: v's transpose lands in them
     __builtin_amdgcn_sched_barrier(0);
     const float4 *hr4 = reinterpret_cast<const float4 *>(hr);
 #pragma unroll
@@ -393,7 +376,7 @@ __device__ __forceinline__ void h_rows(const float2 *sym, int Cp, int R, const f
     row_load<true>(sym + 1024 * E, t, a);
     row_load<true>(sym + 1024 * (E + 2), t, b);
     const unsigned hb0 = lds_addr(HB), hb1 = lds_addr(HB + C);
-    const int pt = perm4(t);
+    const int pt = perm16(t);
     for (int r = 0; r + 1 < R; ++r)
         x_row<E, true>(sym + (long long)(r + 1) * Cp, HB + (r & 1) * C + E * 2048, t, pt, T, Tp, tw1, tw2, wb0, wb1, a,
                        b, ae, ao, Hg + (long long)(r + 1) * C, (r & 1) ? hb0 : hb1);

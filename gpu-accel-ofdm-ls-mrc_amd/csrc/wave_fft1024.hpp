@@ -579,6 +579,32 @@ __device__ __forceinline__ void row_fft_b(int t, float2 *T, const float2 *tw2, f
     }
     quad_dft(x, qa);
 }
+// Transpose images for 16-B reads (the C = 2048 / 4096 receivers, whose LDS
+// budget has room for the wider pitch): 16 rows of pitch TP16 = 72 float2, row
+// element c = a + 4 l (a < 4) at position 8 (l >> 1) + 2 a + (l & 1), so
+// that the second FFT half reads lane (q, a)'s values l = 2 j, 2 j + 1 as
+// ONE 16-B ds_read_b128 at q TP16 + 8 j + 2 a (4 LDS cycles; the hlds image
+// of pitch 68 gives ds_read2_b64, 8 cycles: MI355X_MICROARCH.md LDS table).
+// Conflict-free both ways: a transpose-write row covers 16 lanes x 8 B
+// contiguously per lane group, and the four rows a ds_read_b128 lane group
+// reads start 16 dwords apart mod 64 (pitch 144 dwords).
+constexpr int TP16 = 72;
+constexpr int TS16 = 16 * TP16;
+__device__ __forceinline__ int perm16(int c) { return 8 * (c >> 3) + 2 * (c & 3) + ((c >> 2) & 1); }
+__device__ __forceinline__ void fa_write16(const pk::v2f (&v)[16], int pt, float2 *T) {
+#pragma unroll
+    for (int k2 = 0; k2 < 16; ++k2) T[k2 * TP16 + pt] = pk::F(v[k2]);
+}
+__device__ __forceinline__ void fb_read16(int t, const float2 *T, pk::v2f (&v)[16]) {
+    const float4 *s = reinterpret_cast<const float4 *>(T + (t >> 2) * TP16 + 2 * (t & 3));
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float4 x = s[4 * j];  // float2 offset 8 j
+        v[2 * j] = pk::V(float2{x.x, x.y});
+        v[2 * j + 1] = pk::V(float2{x.z, x.w});
+    }
+}
+
 // The two FFT1024 stages of hlds::row_fft_a / row_fft_b (PK = 3, TW = 3:
 // packed butterflies, twiddles by recurrence) split at the transpose, so that
 // the IL variants of the C = 2048 / 4096 rows can put one transform's compute between the other's
