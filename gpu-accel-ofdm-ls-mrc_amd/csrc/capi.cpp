@@ -874,4 +874,19 @@ int ofdm_zf_detect(const ofdm_cf32 *d_Wt, const ofdm_cf32 *d_Y, int users, int r
                      "ofdm_zf_detect");
 }
 
+int ofdm_zf_detect_ex(const ofdm_cf32 *d_Wt, const ofdm_cf32 *d_Y, long long ldy, int users, int rows, int K,
+                      long long nsym, ofdm_cf32 *d_X, long long ldx, ofdm_stream_t stream) {
+    static const char *fn = "ofdm_zf_detect_ex";
+    int rc = zf_geometry(users, rows, K, fn);
+    if (rc) return rc;
+    if (nsym < 0) return fail(OFDM_E_ARG, "%s: nsym < 0", fn);
+    if (ldy < K || ldx < K) return fail(OFDM_E_ARG, "%s: ldy=%lld, ldx=%lld below K=%d", fn, ldy, ldx, K);
+    if ((ldy != K || ldx != K) && !ofdm::zf_detect_pitched_supported(users, rows))
+        return fail(OFDM_E_UNSUPPORTED, "%s: row pitches other than K need rows <= 72 (rows=%d)", fn, rows);
+    if (K > 0 && nsym > 0 && (!d_Wt || !d_X || !d_Y)) return fail(OFDM_E_ARG, "%s: null pointer", fn);
+    return hip_check(ofdm::launch_zf_detect_ld(F2(d_Wt), F2(d_Y), ldy, users, rows, K, nsym, F2(d_X), ldx,
+                                               hs(stream)),
+                     fn);
+}
+
 }  // extern "C"

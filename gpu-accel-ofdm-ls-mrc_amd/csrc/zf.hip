@@ -845,7 +845,8 @@ template <bool CONJ, bool XMAP = false, int MR = 16, int PDT = 2>
 __global__ void __attribute__((amdgpu_flat_work_group_size(MR == 64 ? 256 : 512, MR == 64 ? 256 : 512),
                                amdgpu_waves_per_eu(MR == 64 ? 1 : 2, MR == 64 ? 1 : 2)))
 k_zf_wstat(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__restrict__ in, int N, int M, int K,
-           long long nsym, float2 *__restrict__ out, int nkb, int nmb, long long chunk_syms) {
+           long long nsym, float2 *__restrict__ out, int nkb, int nmb, long long chunk_syms, long long ldi,
+           long long ldo) {
     // MR rows per tile: 16 (MP = 8 row pairs x SG = 4 symbol quads per wave) or
     // 64 (apply at U = 16: all R = 64 output rows, MP = 32 x SG = 1)
     // MR = 64: 4-wave workgroups, one wave per SIMD (512 registers for 128 accumulators + 32 A pairs)
@@ -872,7 +873,7 @@ k_zf_wstat(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__rest
     }
     __syncthreads();
     const bool odd = i & 1;
-    const long long NK = (long long)N * K;
+    const long long NK = (long long)N * ldi;  // input rows of ldi elements, output rows of ldo (>= K)
     const float2 *wl = smd + (i >> 1) * 16 + b;  // + n * TR + 2 p * 16
 
     for (long long s0 = sbeg + (long long)w * SW; s0 < send; s0 += (long long)NW * SW) {
@@ -888,7 +889,7 @@ k_zf_wstat(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__rest
 #pragma unroll
         for (int d = 0; d < PD; ++d)
 #pragma unroll
-            for (int g = 0; g < SG; ++g) xq[d][g] = xrow[g][(long long)min(d, N - 1) * K];
+            for (int g = 0; g < SG; ++g) xq[d][g] = xrow[g][(long long)min(d, N - 1) * ldi];
         for (int n0 = 0; n0 < N; n0 += PD) {
 #pragma unroll
             for (int d = 0; d < PD; ++d) {
@@ -899,7 +900,7 @@ k_zf_wstat(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__rest
                     for (int g = 0; g < SG; ++g) xv[g] = xq[d][g];
                     const int nn = min(n + PD, N - 1);  // refill this slot PD steps ahead
 #pragma unroll
-                    for (int g = 0; g < SG; ++g) xq[d][g] = xrow[g][(long long)nn * K];
+                    for (int g = 0; g < SG; ++g) xq[d][g] = xrow[g][(long long)nn * ldi];
                     // row pairs in groups of 4: only one group's A operands live
 #pragma unroll
                     for (int p0 = 0; p0 < MP; p0 += 4) {
@@ -947,7 +948,7 @@ k_zf_wstat(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__rest
                     const mf4 v = hi ? mf4{rx, ry, acc[p][g][2], acc[p][g][3]} : mf4{acc[p][g][0], acc[p][g][1], rx, ry};
                     const int m = mr0 + 2 * p + (hi ? 1 : 0);
                     if (s < send && m < M && kp < K) {
-                        const long long e = (s * M + m) * (long long)K + kp;
+                        const long long e = (s * M + m) * ldo + kp;
                         float2 *o = out + e;
                         if (kp + 1 < K && !(e & 1)) {
                             *reinterpret_cast<mf4 *>(o) = v;  // 16-B aligned (out is)
@@ -1228,7 +1229,7 @@ hipError_t mfma_w128_launch(const float2 *Wt, int a_m, int a_n, const float2 *in
 
 template <bool CONJ, bool XMAP, int MR = 16, int PD = 2>
 hipError_t wstat_launch(const float2 *Wt, int a_m, int a_n, const float2 *in, int N, int M, int K,
-                        long long nsym, float2 *out, hipStream_t s) {
+                        long long nsym, float2 *out, hipStream_t s, long long ldi = -1, long long ldo = -1) {
     const size_t lds = (size_t)N * MR * 16 * sizeof(float2);  // N * MR <= 1152: <= 144 KiB
     const int nkb = (K + 15) / 16, nmb = (M + MR - 1) / MR;
     // ~1 workgroup per CU over all (tile, symbol chunk) pairs;
@@ -1245,7 +1246,7 @@ hipError_t wstat_launch(const float2 *Wt, int a_m, int a_n, const float2 *in, in
         e != hipSuccess)
         return e;
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(MR == 64 ? 256 : 512), lds, s, Wt, a_m, a_n, in, N, M, K,
-                       nsym, out, nkb, nmb, chunk_syms);
+                       nsym, out, nkb, nmb, chunk_syms, ldi < 0 ? K : ldi, ldo < 0 ? K : ldo);
     return hipGetLastError();
 }
 
@@ -1312,6 +1313,20 @@ hipError_t launch_zf_detect(const float2 *Wt, const float2 *Y, int U, int R, int
                             float2 *X, hipStream_t s) {
     if (K == 0 || nsym == 0) return hipSuccess;
     return gemm_dispatch<true>(Wt, R, 1, Y, R, U, K, nsym, X, s);
+}
+
+// The same with row pitches: Y[s][r][k] at Y[(s R + r) ldy + k], X[s][u][k]
+// at X[(s U + u) ldx + k] (ldy, ldx >= K; the pad is neither read nor
+// written).  Rows padded to a multiple of 16 elements start on 128-B lines,
+// so no workgroup leaves a partly written line for its neighbour to complete
+// (DESIGN.md 7c, round 6).  The W-stationary kernel for every U: R <= 72.
+bool zf_detect_pitched_supported(int U, int R) { return U >= 1 && R <= 72; }
+hipError_t launch_zf_detect_ld(const float2 *Wt, const float2 *Y, long long ldy, int U, int R, int K,
+                               long long nsym, float2 *X, long long ldx, hipStream_t s) {
+    if (K == 0 || nsym == 0) return hipSuccess;
+    if (ldy == K && ldx == K) return gemm_dispatch<true>(Wt, R, 1, Y, R, U, K, nsym, X, s);
+    if (!zf_detect_pitched_supported(U, R)) return hipErrorInvalidValue;
+    return wstat_launch<true, true>(Wt, R, 1, Y, R, U, K, nsym, X, s, ldy, ldx);
 }
 
 }  // namespace ofdm

@@ -76,6 +76,7 @@ _SIGS = {
     "ofdm_zf_transpose": (_I, [_P, _I, _I, _I, _P, _P]),
     "ofdm_zf_apply": (_I, [_P, _P, _I, _I, _I, _LL, _P, _P]),
     "ofdm_zf_detect": (_I, [_P, _P, _I, _I, _I, _LL, _P, _P]),
+    "ofdm_zf_detect_ex": (_I, [_P, _P, _LL, _I, _I, _I, _LL, _P, _LL, _P]),
     "ofdm_hbm_probe": (_I, [_I, _P, _P, _c.c_size_t, _c.c_size_t, _P]),
     "ofdm_device_status": (_I, []),
     "ofdm_device_status_inject": (_I, [_c.c_uint]),
@@ -555,6 +556,21 @@ def zf_detect(Wt, Y, out=None, stream=None):
         out = c64((n, U, K), Y.device)
     _check(lib().ofdm_zf_detect(_dptr(Wt, "Wt"), _dptr(Y, "Y"), U, R, K, n, _dptr(out, "out"),
                                 _stream(stream)), "ofdm_zf_detect")
+    return out
+
+
+def zf_detect_pitched(Wt, Y, out=None, ldx=None, stream=None):
+    """ofdm_zf_detect_ex: Y (nsym, R, ldy) with rows padded to ldy >= K (only
+    the first K columns read) -> out (nsym, U, ldx), first K columns written
+    (ldx default: ldy)."""
+    U, R, K = Wt.shape
+    n, r, ldy = Y.shape
+    assert r == R and ldy >= K, Y.shape
+    if out is None:
+        out = c64((n, U, ldx or ldy), Y.device)
+    assert out.shape[0] == n and out.shape[1] == U and out.shape[2] >= K, out.shape
+    _check(lib().ofdm_zf_detect_ex(_dptr(Wt, "Wt"), _dptr(Y, "Y"), ldy, U, R, K, n, _dptr(out, "out"),
+                                   out.shape[2], _stream(stream)), "ofdm_zf_detect_ex")
     return out
 
 

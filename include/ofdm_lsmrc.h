@@ -402,6 +402,14 @@ int ofdm_zf_apply(const ofdm_cf32 *d_Wt, const ofdm_cf32 *d_X, int users, int ro
                   ofdm_cf32 *d_Y, ofdm_stream_t stream);
 int ofdm_zf_detect(const ofdm_cf32 *d_Wt, const ofdm_cf32 *d_Y, int users, int rows, int K, long long nsym,
                    ofdm_cf32 *d_X, ofdm_stream_t stream);
+/* ofdm_zf_detect on row-padded layouts (no reference counterpart):
+ * d_Y[(s*rows + r)*ldy + k] and d_X[(s*users + u)*ldx + k], ldy, ldx >= K
+ * (the pad is neither read nor written; ldy = ldx = K is ofdm_zf_detect).
+ * Rows padded to a multiple of 16 elements (K = 1023 -> 1024) start on
+ * 128-B lines, so no part of a line is left for another workgroup to
+ * complete.  Pitches other than K need rows <= 72 (else OFDM_E_UNSUPPORTED). */
+int ofdm_zf_detect_ex(const ofdm_cf32 *d_Wt, const ofdm_cf32 *d_Y, long long ldy, int users, int rows, int K,
+                      long long nsym, ofdm_cf32 *d_X, long long ldx, ofdm_stream_t stream);
 
 /* --------------------------------------------------- synthetic frames --- */
 

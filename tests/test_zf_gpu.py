@@ -136,3 +136,39 @@ def test_zf_full_size_round_trips(ofdm, dev):
     err = (torch.linalg.vector_norm(down - X) / torch.linalg.vector_norm(X)).item()
     assert err < 1e-4
     assert int(dec(down).sum().item()) == 0
+
+
+@pytest.mark.parametrize("U,R,K,n,ldy,ldx", [(16, 64, 1023, 40, 1024, 1024), (16, 64, 1023, 33, 1023, 1024),
+                                             (16, 64, 1023, 20, 1030, 1023), (4, 16, 1023, 9, 1024, 1040),
+                                             (24, 40, 200, 16, 208, 201), (9, 72, 65, 70, 80, 72)])
+def test_zf_detect_pitched(ofdm, oracle, dev, U, R, K, n, ldy, ldx):
+    """ofdm_zf_detect_ex on row-padded layouts: the first K columns of every
+    row read and written, the pad untouched (NaN-filled input pad, NaN
+    sentinels in the output pad), the result against the oracle at the
+    detect's 1e-5 bound -- and bit-identical to the unpadded detect where
+    both run the W-stationary kernel (U > 8, R <= 72)."""
+    import torch
+    H = channel(U, R, K, seed=n + 5)
+    W = oracle.zf_precoder(H)
+    Yn = (oracle.zf_apply(W, qpsk(n, U, K, seed=n + 6)) + 0.05 * qpsk(n, R, K, seed=n + 7)).astype(np.complex64)
+    ref = oracle.zf_detect(W, Yn)
+    Wt = ofdm.zf_transpose(dev_t(W, dev))
+    Yp = torch.full((n, R, ldy), float("nan"), dtype=torch.complex64, device=dev)
+    Yp[:, :, :K] = dev_t(Yn, dev)
+    out = torch.full((n, U, ldx), float("nan"), dtype=torch.complex64, device=dev)
+    ofdm.zf_detect_pitched(Wt, Yp, out=out)
+    got = out.cpu().numpy()
+    assert np.isnan(got[:, :, K:]).all()
+    parity(got[:, :, :K], ref)
+    if U > 8:
+        assert np.array_equal(got[:, :, :K], ofdm.zf_detect(Wt, dev_t(Yn, dev)).cpu().numpy())
+
+
+def test_zf_detect_pitched_limits(ofdm, dev):
+    import torch
+    Wt = torch.zeros((4, 100, 16), dtype=torch.complex64, device=dev)
+    Y = torch.zeros((2, 100, 32), dtype=torch.complex64, device=dev)
+    with pytest.raises(ofdm.OfdmError, match="rows <= 72"):
+        ofdm.zf_detect_pitched(Wt, Y)
+    Y = torch.zeros((2, 100, 16), dtype=torch.complex64, device=dev)  # ldy = K: the plain detect, any R
+    assert ofdm.zf_detect_pitched(Wt, Y).shape == (2, 4, 16)
