@@ -874,6 +874,21 @@ int ofdm_zf_detect(const ofdm_cf32 *d_Wt, const ofdm_cf32 *d_Y, int users, int r
                      "ofdm_zf_detect");
 }
 
+int ofdm_zf_apply_ex(const ofdm_cf32 *d_Wt, const ofdm_cf32 *d_X, long long ldx, int users, int rows, int K,
+                     long long nsym, ofdm_cf32 *d_Y, long long ldy, ofdm_stream_t stream) {
+    static const char *fn = "ofdm_zf_apply_ex";
+    int rc = zf_geometry(users, rows, K, fn);
+    if (rc) return rc;
+    if (nsym < 0) return fail(OFDM_E_ARG, "%s: nsym < 0", fn);
+    if (ldx < K || ldy < K) return fail(OFDM_E_ARG, "%s: ldx=%lld, ldy=%lld below K=%d", fn, ldx, ldy, K);
+    if ((ldx != K || ldy != K) && !ofdm::zf_apply_pitched_supported(users, rows, K))
+        return fail(OFDM_E_UNSUPPORTED, "%s: row pitches other than K need K >= 2, rows >= 8 and users <= 40", fn);
+    if (K > 0 && nsym > 0 && (!d_Wt || !d_X || !d_Y)) return fail(OFDM_E_ARG, "%s: null pointer", fn);
+    return hip_check(ofdm::launch_zf_apply_ld(F2(d_Wt), F2(d_X), ldx, users, rows, K, nsym, F2(d_Y), ldy,
+                                              hs(stream)),
+                     fn);
+}
+
 int ofdm_zf_detect_ex(const ofdm_cf32 *d_Wt, const ofdm_cf32 *d_Y, long long ldy, int users, int rows, int K,
                       long long nsym, ofdm_cf32 *d_X, long long ldx, ofdm_stream_t stream) {
     static const char *fn = "ofdm_zf_detect_ex";

@@ -207,6 +207,10 @@ hipError_t launch_zf_apply(const float2 *Wt, const float2 *X, int U, int R, int 
                            float2 *Y, hipStream_t s);
 hipError_t launch_zf_detect(const float2 *Wt, const float2 *Y, int U, int R, int K, long long nsym,
                             float2 *X, hipStream_t s);
+// ... with row pitches (elements, >= K); pitched apply: K >= 2, R >= 8, U <= 40
+bool zf_apply_pitched_supported(int U, int R, int K);
+hipError_t launch_zf_apply_ld(const float2 *Wt, const float2 *X, long long ldx, int U, int R, int K, long long nsym,
+                              float2 *Y, long long ldy, hipStream_t s);
 // ... with row pitches ldy / ldx (elements, >= K); pitched calls need R <= 72
 bool zf_detect_pitched_supported(int U, int R);
 hipError_t launch_zf_detect_ld(const float2 *Wt, const float2 *Y, long long ldy, int U, int R, int K,

@@ -986,7 +986,8 @@ k_zf_wstat(const float2 *__restrict__ Wt, int a_m, int a_n, const float2 *__rest
 template <int MT, int RG, int ST, int NW, int XM = 0>
 __global__ void __attribute__((amdgpu_flat_work_group_size(64 * NW, 64 * NW), amdgpu_waves_per_eu(NW / 4, NW / 4)))
 k_zf_apply_ws16(const float2 *__restrict__ Wt, const float2 *__restrict__ X, int U, int R, int K, long long nsym,
-                float2 *__restrict__ Y, int nkb, int nrb, int ngroups, long long chunk_syms) {
+                float2 *__restrict__ Y, int nkb, int nrb, int ngroups, long long chunk_syms, long long ldx,
+                long long ldy) {
     constexpr int SGN = NW / RG, MB = MT * RG;
     extern __shared__ __attribute__((aligned(16))) float4 smw[];  // [U][MB][64]
     const int b = blockIdx.x, xcd = b & 7, j = b >> 3;
@@ -1035,7 +1036,10 @@ k_zf_apply_ws16(const float2 *__restrict__ Wt, const float2 *__restrict__ X, int
 
     const float4 *wl = smw + (rg * MT) * 64 + lane;  // + (u * MB + i) * 64
     const int m0 = r0 + rg * MT;
-    const long long UK = (long long)U * K;
+    // input rows of ldx elements, output rows of ldy (>= K; the reference layout: K).  With an odd
+    // pitch the 16-B input loads of odd rows are 8-B aligned: unaligned dwordx4, which gfx950's
+    // global memory serves (the W tile loads above likewise); pitches padded to even lengths avoid it.
+    const long long UK = (long long)U * ldx;
     for (long long s0 = sbeg + (long long)sg * ST; s0 < send; s0 += (long long)SGN * ST) {
         const float2 *xs[ST];
 #pragma unroll
@@ -1062,11 +1066,11 @@ k_zf_apply_ws16(const float2 *__restrict__ Wt, const float2 *__restrict__ X, int
         int u = 0;
         for (; u + 1 < U; u += 2) {
 #pragma unroll
-            for (int q = 0; q < ST; ++q) xb[q] = *reinterpret_cast<const float4 *>(xs[q] + (long long)(u + 1) * K);
+            for (int q = 0; q < ST; ++q) xb[q] = *reinterpret_cast<const float4 *>(xs[q] + (long long)(u + 1) * ldx);
             step(u, xa);
             if (u + 2 < U) {
 #pragma unroll
-                for (int q = 0; q < ST; ++q) xa[q] = *reinterpret_cast<const float4 *>(xs[q] + (long long)(u + 2) * K);
+                for (int q = 0; q < ST; ++q) xa[q] = *reinterpret_cast<const float4 *>(xs[q] + (long long)(u + 2) * ldx);
             }
             step(u + 1, xb);
         }
@@ -1075,11 +1079,11 @@ k_zf_apply_ws16(const float2 *__restrict__ Wt, const float2 *__restrict__ X, int
 #pragma unroll
             for (int q = 0; q < ST; ++q) {
                 if (s0 + q >= send) break;
-                float2 *o = Y + ((s0 + q) * R + m0) * (long long)K + kc;
+                float2 *o = Y + ((s0 + q) * R + m0) * ldy + kc;
 #pragma unroll
                 for (int i = 0; i < MT; ++i) {
                     if (m0 + i >= R) break;
-                    float2 *y = o + (long long)i * K;
+                    float2 *y = o + (long long)i * ldy;
                     const float2 lo = pk::F(acc[i][q][0]), hi = pk::F(acc[i][q][1]);
                     if (pair)
                         __builtin_nontemporal_store(mf4{lo.x, lo.y, hi.x, hi.y}, reinterpret_cast<mf4 *>(y));
@@ -1164,7 +1168,7 @@ hipError_t gemm_lds_launch(const float2 *Wt, int a_m, int a_n, const float2 *in,
 // rows per tile, ST symbols per wave step
 template <int MT, int RG, int ST, int NW, int XM = 0>
 hipError_t apply_ws16_launch(const float2 *Wt, const float2 *X, int U, int R, int K, long long nsym, float2 *Y,
-                             int target_groups, hipStream_t s) {
+                             int target_groups, hipStream_t s, long long ldx = -1, long long ldy = -1) {
     constexpr int MB = MT * RG, WSTEP = NW / RG * ST;
     const size_t lds = (size_t)U * MB * 64 * sizeof(float4);
     if (lds > 160 * 1024 || K < 2) return hipErrorInvalidValue;
@@ -1180,7 +1184,7 @@ hipError_t apply_ws16_launch(const float2 *Wt, const float2 *X, int U, int R, in
     auto kern = zf::k_zf_apply_ws16<MT, RG, ST, NW, XM>;
     if (hipError_t e = opt_in_lds(reinterpret_cast<const void *>(kern), (int)lds); e != hipSuccess) return e;
     hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(64 * NW), lds, s, Wt, X, U, R, K, nsym, Y, nkb, nrb,
-                       (int)ngroups, chunk_syms);
+                       (int)ngroups, chunk_syms, ldx < 0 ? K : ldx, ldy < 0 ? K : ldy);
     return hipGetLastError();
 }
 
@@ -1306,6 +1310,18 @@ hipError_t launch_zf_apply(const float2 *Wt, const float2 *X, int U, int R, int 
     if (K >= 2 && R >= 8 && U <= 20) return apply_ws16_launch<8, 1, 4, 8, 1>(Wt, X, U, R, K, nsym, Y, 64, s);
     if (K >= 2 && R >= 8 && U <= 40) return apply_ws16_launch<4, 1, 8, 8>(Wt, X, U, R, K, nsym, Y, 32, s);
     return gemm_dispatch<false>(Wt, 1, R, X, U, R, K, nsym, Y, s);
+}
+
+// The apply with row pitches (X rows of ldx, Y rows of ldy elements >= K):
+// the 16-B-lane W-stationary kernel, R >= 8, U <= 40, K >= 2.
+bool zf_apply_pitched_supported(int U, int R, int K) { return K >= 2 && R >= 8 && U <= 40; }
+hipError_t launch_zf_apply_ld(const float2 *Wt, const float2 *X, long long ldx, int U, int R, int K, long long nsym,
+                              float2 *Y, long long ldy, hipStream_t s) {
+    if (K == 0 || nsym == 0) return hipSuccess;
+    if (ldx == K && ldy == K) return launch_zf_apply(Wt, X, U, R, K, nsym, Y, s);
+    if (!zf_apply_pitched_supported(U, R, K)) return hipErrorInvalidValue;
+    if (U <= 20) return apply_ws16_launch<8, 1, 4, 8, 1>(Wt, X, U, R, K, nsym, Y, 64, s, ldx, ldy);
+    return apply_ws16_launch<4, 1, 8, 8>(Wt, X, U, R, K, nsym, Y, 32, s, ldx, ldy);
 }
 
 // X[s][u][k] = sum_r conj(W(r, u)) Y[s][r][k]

@@ -77,6 +77,7 @@ _SIGS = {
     "ofdm_zf_apply": (_I, [_P, _P, _I, _I, _I, _LL, _P, _P]),
     "ofdm_zf_detect": (_I, [_P, _P, _I, _I, _I, _LL, _P, _P]),
     "ofdm_zf_detect_ex": (_I, [_P, _P, _LL, _I, _I, _I, _LL, _P, _LL, _P]),
+    "ofdm_zf_apply_ex": (_I, [_P, _P, _LL, _I, _I, _I, _LL, _P, _LL, _P]),
     "ofdm_hbm_probe": (_I, [_I, _P, _P, _c.c_size_t, _c.c_size_t, _P]),
     "ofdm_device_status": (_I, []),
     "ofdm_device_status_inject": (_I, [_c.c_uint]),
@@ -556,6 +557,20 @@ def zf_detect(Wt, Y, out=None, stream=None):
         out = c64((n, U, K), Y.device)
     _check(lib().ofdm_zf_detect(_dptr(Wt, "Wt"), _dptr(Y, "Y"), U, R, K, n, _dptr(out, "out"),
                                 _stream(stream)), "ofdm_zf_detect")
+    return out
+
+
+def zf_apply_pitched(Wt, X, out=None, ldy=None, stream=None):
+    """ofdm_zf_apply_ex: X (nsym, U, ldx) with rows padded to ldx >= K -> out
+    (nsym, R, ldy), first K columns written (ldy default: ldx)."""
+    U, R, K = Wt.shape
+    n, u, ldx = X.shape
+    assert u == U and ldx >= K, X.shape
+    if out is None:
+        out = c64((n, R, ldy or ldx), X.device)
+    assert out.shape[0] == n and out.shape[1] == R and out.shape[2] >= K, out.shape
+    _check(lib().ofdm_zf_apply_ex(_dptr(Wt, "Wt"), _dptr(X, "X"), ldx, U, R, K, n, _dptr(out, "out"),
+                                  out.shape[2], _stream(stream)), "ofdm_zf_apply_ex")
     return out
 
 

@@ -402,6 +402,12 @@ int ofdm_zf_apply(const ofdm_cf32 *d_Wt, const ofdm_cf32 *d_X, int users, int ro
                   ofdm_cf32 *d_Y, ofdm_stream_t stream);
 int ofdm_zf_detect(const ofdm_cf32 *d_Wt, const ofdm_cf32 *d_Y, int users, int rows, int K, long long nsym,
                    ofdm_cf32 *d_X, ofdm_stream_t stream);
+/* ofdm_zf_apply on row-padded layouts (no reference counterpart):
+ * d_X[(s*users + u)*ldx + k] and d_Y[(s*rows + r)*ldy + k], ldx, ldy >= K
+ * (ldx = ldy = K is ofdm_zf_apply); pitches other than K need K >= 2,
+ * rows >= 8 and users <= 40 (else OFDM_E_UNSUPPORTED). */
+int ofdm_zf_apply_ex(const ofdm_cf32 *d_Wt, const ofdm_cf32 *d_X, long long ldx, int users, int rows, int K,
+                     long long nsym, ofdm_cf32 *d_Y, long long ldy, ofdm_stream_t stream);
 /* ofdm_zf_detect on row-padded layouts (no reference counterpart):
  * d_Y[(s*rows + r)*ldy + k] and d_X[(s*users + u)*ldx + k], ldy, ldx >= K
  * (the pad is neither read nor written; ldy = ldx = K is ofdm_zf_detect).

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""ZF detect with row pitches (ofdm_zf_detect_ex) against the reference layout,
+"""ZF detect / apply with row pitches (ofdm_zf_detect_ex / _apply_ex) against the reference layout,
 same process, alternating: U users x R antennas x K subcarriers, nsym symbols
 in HBM.  Algorithmic bytes (U + R) K 8 per symbol in every layout (the pad is
 neither read nor written).  usage: python scripts/zf_pitch_ab.py [--U 16] [--reps 5]"""
@@ -18,6 +18,7 @@ ap.add_argument("--K", type=int, default=1023)
 ap.add_argument("--nsym", type=int, default=10000)
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--launches", type=int, default=10)
+ap.add_argument("--op", choices=["detect", "apply"], default="detect")
 a = ap.parse_args()
 
 import torch  # noqa: E402
@@ -30,14 +31,24 @@ _, Wt = ofdm.zf_precoder(torch.from_numpy(channel(U, R, K, seed=U)).to(dev), W=F
 g = torch.Generator(device=dev)
 g.manual_seed(0)
 Kp = (K + 15) // 16 * 16
-Ypad = torch.randn((n, R, Kp), dtype=torch.complex64, device=dev, generator=g)
-Y = Ypad[:, :, :K].contiguous()
-ref = ofdm.zf_detect(Wt, Y)
-cases = {
-    "reference layout (ldy = ldx = K)": (lambda o: ofdm.zf_detect(Wt, Y, out=o), (n, U, K), Y),
-    f"ldy = K, ldx = {Kp}": (lambda o: ofdm.zf_detect_pitched(Wt, Y, out=o), (n, U, Kp), Y),
-    f"ldy = ldx = {Kp}": (lambda o: ofdm.zf_detect_pitched(Wt, Ypad, out=o), (n, U, Kp), Ypad),
-}
+if a.op == "detect":
+    Ypad = torch.randn((n, R, Kp), dtype=torch.complex64, device=dev, generator=g)
+    Y = Ypad[:, :, :K].contiguous()
+    ref = ofdm.zf_detect(Wt, Y)
+    cases = {
+        "reference layout (ldy = ldx = K)": (lambda o: ofdm.zf_detect(Wt, Y, out=o), (n, U, K), Y),
+        f"ldy = K, ldx = {Kp}": (lambda o: ofdm.zf_detect_pitched(Wt, Y, out=o), (n, U, Kp), Y),
+        f"ldy = ldx = {Kp}": (lambda o: ofdm.zf_detect_pitched(Wt, Ypad, out=o), (n, U, Kp), Ypad),
+    }
+else:
+    Xpad = torch.randn((n, U, Kp), dtype=torch.complex64, device=dev, generator=g)
+    X = Xpad[:, :, :K].contiguous()
+    ref = ofdm.zf_apply(Wt, X)
+    cases = {
+        "reference layout (ldx = ldy = K)": (lambda o: ofdm.zf_apply(Wt, X, out=o), (n, R, K), X),
+        f"ldx = K, ldy = {Kp}": (lambda o: ofdm.zf_apply_pitched(Wt, X, out=o), (n, R, Kp), X),
+        f"ldx = ldy = {Kp}": (lambda o: ofdm.zf_apply_pitched(Wt, Xpad, out=o), (n, R, Kp), Xpad),
+    }
 outs = {k: torch.empty(shape, dtype=torch.complex64, device=dev) for k, (_, shape, _) in cases.items()}
 byt = n * (U + R) * K * 8.0
 res = {k: [] for k in cases}
@@ -55,6 +66,6 @@ for rep in range(a.reps):
 for name, v in res.items():
     m = sorted(v)[len(v) // 2]
     same = bool(torch.equal(outs[name][:, :, :K], ref))
-    print(json.dumps({"layout": name, "U": U, "R": R, "K": K, "nsym": n, "ms_median": m, "ms_all": v,
+    print(json.dumps({"op": a.op, "layout": name, "U": U, "R": R, "K": K, "nsym": n, "ms_median": m, "ms_all": v,
                       "TBps": byt / m / 1e9, "hbm_frac": byt / m / 8e9, "bit_identical_to_reference_layout": same}),
           flush=True)

@@ -223,7 +223,7 @@ def test_hbm_probe_refuses_small_destination(ofdm):
     assert L.ofdm_hbm_probe(2, fake, fake, 1 << 20, 1 << 20, None) == -1
 
 
-def test_zf_detect_pitched_validation_without_device(ofdm):
+def test_zf_pitched_validation_without_device(ofdm):
     L = ofdm.lib()
     fake = ctypes.c_void_p(4096)
     assert L.ofdm_zf_detect_ex(fake, fake, 1022, 16, 64, 1023, 4, fake, 1024, None) == -1  # ldy < K
@@ -232,3 +232,8 @@ def test_zf_detect_pitched_validation_without_device(ofdm):
     assert L.ofdm_zf_detect_ex(fake, fake, 1024, 16, 100, 1023, 4, fake, 1024, None) == -3  # pitched, R > 72
     assert L.ofdm_zf_detect_ex(fake, fake, 1024, 33, 64, 1023, 4, fake, 1024, None) == -3  # users > 32
     assert L.ofdm_zf_detect_ex(None, None, 1024, 16, 64, 1023, 0, None, 1024, None) == 0  # no symbols
+    assert L.ofdm_zf_apply_ex(fake, fake, 1000, 16, 64, 1023, 4, fake, 1024, None) == -1  # ldx < K
+    assert b"below K" in L.ofdm_last_error()
+    assert L.ofdm_zf_apply_ex(fake, fake, 1024, 16, 4, 1023, 4, fake, 1024, None) == -3  # pitched, rows < 8
+    assert L.ofdm_zf_apply_ex(fake, fake, 1024, 41, 64, 1023, 4, fake, 1024, None) == -3  # pitched, users > 40
+    assert L.ofdm_zf_apply_ex(None, None, 1024, 16, 64, 1023, 0, None, 1024, None) == 0

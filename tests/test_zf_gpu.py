@@ -172,3 +172,25 @@ def test_zf_detect_pitched_limits(ofdm, dev):
         ofdm.zf_detect_pitched(Wt, Y)
     Y = torch.zeros((2, 100, 16), dtype=torch.complex64, device=dev)  # ldy = K: the plain detect, any R
     assert ofdm.zf_detect_pitched(Wt, Y).shape == (2, 4, 16)
+
+
+@pytest.mark.parametrize("U,R,K,n,ldx,ldy", [(16, 64, 1023, 40, 1024, 1024), (16, 64, 1023, 17, 1023, 1024),
+                                             (24, 16, 130, 9, 144, 131), (4, 8, 2, 5, 16, 3)])
+def test_zf_apply_pitched(ofdm, oracle, dev, U, R, K, n, ldx, ldy):
+    """ofdm_zf_apply_ex on row-padded layouts: pads untouched (NaN sentinels),
+    results at the apply's 1e-5 bound against the oracle and bit-identical to
+    the unpadded apply (the same 16-B-lane W-stationary kernel)."""
+    import torch
+    H = channel(U, R, K, seed=n + 9)
+    W = oracle.zf_precoder(H)
+    X = qpsk(n, U, K, seed=n + 10)
+    ref = oracle.zf_apply(W, X)
+    Wt = ofdm.zf_transpose(dev_t(W, dev))
+    Xp = torch.full((n, U, ldx), float("nan"), dtype=torch.complex64, device=dev)
+    Xp[:, :, :K] = dev_t(X, dev)
+    out = torch.full((n, R, ldy), float("nan"), dtype=torch.complex64, device=dev)
+    ofdm.zf_apply_pitched(Wt, Xp, out=out)
+    got = out.cpu().numpy()
+    assert np.isnan(got[:, :, K:]).all()
+    parity(got[:, :, :K], ref)
+    assert np.array_equal(got[:, :, :K], ofdm.zf_apply(Wt, dev_t(X, dev)).cpu().numpy())
