@@ -147,8 +147,9 @@ def cpu_baseline(args, X, ofdm, torch, dev):
         reps += 1
     d1 = time.perf_counter() - t0
     fft = "none (frequency-domain input)" if freq else \
-        "float32 radix-2, AVX2/FMA-vectorised (oracle/fft_fast.c: split arrays, unit-stride per-stage twiddles; " \
-        "bit-identical to the scalar oracle_fft_row_f32, 2.8x its speed; FFTW's codelets are not available here)"
+        "float32 radix-2, AVX2-vectorised (oracle/fft_fast.c: split arrays, unit-stride per-stage twiddles, AVX2 " \
+        "code behind a runtime CPU check, no FMA contraction; bit-identical to the scalar oracle_fft_row_f32; " \
+        "FFTW's codelets are not available here)"
     # cores = the threads the sample ran on (the bench contract), i.e. the
     # CPU share this job has on the box (cgroup quota, else the affinity
     # mask, else os.cpu_count()); how that share was read is reported beside it
