@@ -141,7 +141,8 @@ def main():
            "hbm_bytes_per_launch": hbm, "hbm_over_algorithmic": hbm / alg,
            "mrc_hbm_bytes_per_launch": hbm, "mrc_algorithmic_bytes_per_launch": alg,
            "effective_clock_ghz_pmc_pass": clock_ghz, "sq_fractions_of_wave_cycles": frac,
-           "correction": "2*FETCH_SIZE + WRITE_SIZE (KiB->B); MI355X_MICROARCH.md HBM section"}
+           "correction": "2*FETCH_SIZE + WRITE_SIZE (KiB->B); MI355X_MICROARCH.md HBM section",
+           "build_id": traced.get("build_id")}  # the library the profiled run loaded (ofdm_lsmrc.build_id)
     clk = os.path.join(src, "clock_unprofiled.jsonl")
     if os.path.exists(clk):
         vals = []
@@ -153,15 +154,18 @@ def main():
                                                if busy else None, "max": max(vals) if vals else None}
     with open(os.path.join(prof, f"{tag}_pmc.json"), "w") as fp:
         json.dump(out, fp, indent=1)
-    if "traffic" in sys.argv[3:]:
+    if "frames_per_gpu" in cfg:  # frames / freq modes: a traffic record bench.py can attach (same build only)
         t = {"tag": tag, "config": {"R": cfg["R"], "C": cfg["C"], "S": cfg["S"], "prefix": cfg["prefix"],
                                     "frames_per_gpu": cfg["frames_per_gpu"], "domain": cfg.get("domain", "time"),
                                     "flow": cfg.get("flow", "two-launch")},
              "mrc_kernel": kern, "mrc_hbm_bytes_per_launch": hbm, "mrc_algorithmic_bytes_per_launch": alg,
-             "mrc_avg_ns_rocprof": avg_ns, "correction": out["correction"],
+             "mrc_avg_ns_rocprof": avg_ns, "correction": out["correction"], "build_id": out["build_id"],
              "source": os.path.relpath(os.path.join(prof, f"{tag}_pmc.json"), ROOT)}
-        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as fp:
+        with open(os.path.join(prof, f"{tag}_traffic.json"), "w") as fp:
             json.dump(t, fp, indent=1)
+        if "traffic" in sys.argv[3:]:  # the default shape's record
+            with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as fp:
+                json.dump(t, fp, indent=1)
     md = [f"# Profile {tag}", "",
           f"Command (driver form): `python3 bench.py {args}`, run three ways in ONE GPU session: un-profiled, "
           f"under `rocprofv3 --kernel-trace --stats`, and under `rocprofv3 --kernel-trace --pmc ...` "

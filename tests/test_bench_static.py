@@ -116,3 +116,4 @@ def test_pmc_traffic_only_for_the_profiled_build(tmp_path):
     assert len(bid) == 16 and int(bid, 16) >= 0 and bid == ofdm_lsmrc.build_id()
     assert '"build_id": build' in _src("bench.py")
     assert '"build_id": bench.get("build_id")' in _src("scripts/pmc_summary.py")
+    assert '"build_id": traced.get("build_id")' in _src("scripts/prof_summary_r4.py")
