@@ -38,6 +38,11 @@ def pilots(dev, K, seed=5):
     return torch.from_numpy(X).to(dev)
 
 
+def torch_index(idx, device):
+    import torch
+    return torch.as_tensor(idx, device=device)
+
+
 def two_launch(ofdm, iq, X, prefix):
     F, S, R, Cp = iq.shape
     ws = ofdm.workspace(F, S, R, Cp - prefix, iq.device)
@@ -343,7 +348,7 @@ def test_two_streams_two_workspaces_concurrently(ofdm, dev):
 
 
 @pytest.mark.parametrize("C,F,S,R", [(1024, 20000, 3, 1), (4096, 3000, 2, 1), (2048, 4000, 3, 1)])
-def test_many_small_frames(ofdm, dev, C, F, S, R):
+def test_many_small_frames(ofdm, oracle, dev, C, F, S, R):
     """Batches of many tiny frames (one antenna, one or two data symbols):
     thousands of estimator workgroups ahead of the receivers at C = 1024,
     blocks of one symbol and tail pairs at C = 4096, far more ticketed blocks
@@ -355,13 +360,23 @@ def test_many_small_frames(ofdm, dev, C, F, S, R):
     bound stays helpers.RTOL and every output must be written (NaN-filled).
     Measured (profiles/r5/r5al_r1_conditioning.txt): 133 of 41 M elements
     above 1e-5, at |ref| 3-17x the rms, where both flows sit 1e-5..9e-5 from
-    the float64 oracle alike."""
+    the float64 oracle alike.  A 64-frame sample is also checked against the
+    oracle itself."""
     X = pilots(dev, C - 1, seed=C + F)
     iq = ofdm.synth_frames(F, S, R, C, X, seed=F, noise_std=0.01)
     out = ofdm.c64((F, S - 1, C - 1), dev)
     out.fill_(float("nan"))
     ofdm.frame_demod(iq, X, 0, out=out)
-    parity(host(out), two_launch(ofdm, iq, X, 0), erel_tol=2e-3)
+    got = host(out)
+    parity(got, two_launch(ofdm, iq, X, 0), erel_tol=2e-3)
+    # parity evidence, not only self-consistency (VERDICT r5 "weak" 1): 64
+    # frames spread over the batch (first and last included) against the
+    # oracle's float64 FFT + LS + MRC; element-wise bound 2e-4 for the faded
+    # single-antenna bins (worst measured 8.8e-5, r5al_r1_conditioning.txt),
+    # norm-relative helpers.RTOL
+    idx = np.unique(np.linspace(0, F - 1, 64).astype(int))
+    ref = oracle.frames_demod(iq[torch_index(idx, iq.device)].cpu().numpy(), host(X))
+    parity(got[idx], ref, erel_tol=2e-4)
 
 
 def ticket_words(ws, F, R, C):
