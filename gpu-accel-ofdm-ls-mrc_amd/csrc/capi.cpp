@@ -140,33 +140,33 @@ unsigned next_tag() {
 // process, every device writes it), allocated at the first ticketed launch.
 // A ticketed launch that meets a counter it cannot trust stores a TK_* bit
 // there (wave_fft1024.hpp, ticket_fault); every entry that launches ticketed
-// kernels reads it first (a host load, no synchronisation) and, if set,
+// kernels reads it first (a host-side atomic exchange, no device
+// synchronisation) and, if set,
 // clears it and returns OFDM_E_DEVICE, as ofdm_device_status() does.
 // g_status_host stands in before the mapped word exists (and for
 // ofdm_device_status_inject on a machine without a GPU).
 std::once_flag g_status_once;
-unsigned *g_status_mapped = nullptr;
-volatile unsigned g_status_host = 0;
+std::atomic<unsigned *> g_status_mapped{nullptr};
+std::atomic<unsigned> g_status_host{0};
 unsigned *status_word_for_device() {
     std::call_once(g_status_once, [] {
         void *p = nullptr;
         if (hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocPortable | hipHostMallocCoherent) ==
             hipSuccess) {
             std::memset(p, 0, 64);
-            g_status_mapped = static_cast<unsigned *>(p);
+            g_status_mapped.store(static_cast<unsigned *>(p), std::memory_order_release);
         } else {
             (void)hipGetLastError();  // no mapped word: launches run without fault reporting
         }
     });
-    return g_status_mapped;
+    return g_status_mapped.load(std::memory_order_acquire);
 }
+// read-and-clear, each word by one atomic exchange (a device store landing
+// between a read and a clear is never lost)
 int take_status(const char *fn) {
-    unsigned v = g_status_host;
-    volatile unsigned *m = g_status_mapped;
-    if (m) v |= *m;
+    unsigned v = g_status_host.exchange(0u, std::memory_order_acq_rel);
+    if (unsigned *m = g_status_mapped.load(std::memory_order_acquire)) v |= __atomic_exchange_n(m, 0u, __ATOMIC_ACQ_REL);
     if (!v) return OFDM_OK;
-    g_status_host = 0;
-    if (m) *m = 0;
     return fail(OFDM_E_DEVICE,
                 "%s: an earlier work-ticketed launch (C = 1024 one-launch demod, C = 2048 / 4096 MRC) found its "
                 "work-ticket counters taken by another launch (status 0x%x: %s%s%s); its output may be incomplete "
@@ -185,7 +185,8 @@ hipError_t tickets_for(unsigned long long *area, hipStream_t s, ofdm::Tickets *t
     if (hipStreamIsCapturing(s, &st) != hipSuccess) st = hipStreamCaptureStatusNone;
     tk->set = area;
     tk->tag = next_tag();
-    tk->status = st == hipStreamCaptureStatusNone ? status_word_for_device() : g_status_mapped;
+    tk->status = st == hipStreamCaptureStatusNone ? status_word_for_device()
+                                                  : g_status_mapped.load(std::memory_order_acquire);
     if (st != hipStreamCaptureStatusNone) return ofdm::launch_zero_words(area, TICKET_WORDS, s);
     return hipSuccess;
 }
@@ -473,7 +474,7 @@ int ofdm_workspace_release(const void *d_ws) {
 int ofdm_device_status(void) { return take_status("ofdm_device_status"); }
 
 int ofdm_device_status_inject(unsigned bits) {
-    g_status_host = g_status_host | bits;
+    g_status_host.fetch_or(bits, std::memory_order_acq_rel);
     return OFDM_OK;
 }
 
