@@ -37,7 +37,9 @@
 extern "C" {
 #endif
 
-#define OFDM_LSMRC_VERSION 1
+/* 2: ofdm_hbm_probe takes dst_bytes; OFDM_E_DEVICE, ofdm_device_status(_inject),
+ *    ofdm_zf_detect_ex / ofdm_zf_apply_ex added (round 6) */
+#define OFDM_LSMRC_VERSION 2
 
 typedef struct ofdm_cf32 { float re, im; } ofdm_cf32;
 typedef void *ofdm_stream_t; /* hipStream_t */

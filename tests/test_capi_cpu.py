@@ -18,7 +18,7 @@ def test_library_exports_header(ofdm):
         assert hasattr(L, n), f"{n} declared in include/ofdm_lsmrc.h but not exported"
     # and the binding's signature table covers the header exactly
     assert set(names) == set(ofdm._SIGS), set(names) ^ set(ofdm._SIGS)
-    assert L.ofdm_version() == 1
+    assert L.ofdm_version() == 2
 
 
 def test_product_library_reads_no_environment(ofdm):
