@@ -854,6 +854,7 @@ def bench_split(args, X, dev, world, rank, barrier):
                      "bytes_per_launch": Q * b_sym, "avg_launch_ms": mrc_ms,
                      "median_launch_ms": mrc_median},
         "stages_ms": stages,
+        "build_id": ofdm.build_id(),
         "check": check,
         "cpu_baseline": None,
     }
