@@ -242,15 +242,15 @@ def test_work_tickets_wide_receivers_vs_freq_path(ofdm, dev, C, F, R):
     parity(got, ref)
 
 
-@pytest.mark.parametrize("F", [41, 52, 66, 100, 131, 300])
-def test_work_tickets_cover_every_unit(ofdm, dev, F):
+@pytest.mark.parametrize("F,R", [(41, 2), (52, 2), (66, 2), (100, 2), (131, 2), (300, 2), (60, 5), (100, 4), (45, 7)])
+def test_work_tickets_cover_every_unit(ofdm, dev, F, R):
     """Batch sizes around and beyond the static first round (512 blocks):
     every ticketed block and half unit must be processed exactly once (a
     grid smaller than the unit count would leave outputs unwritten: the
     output buffer is NaN-filled first, so a missed unit fails the finite
-    check in parity)."""
+    check in parity).  R = 5 / 7 give half units of uneven row counts."""
     import torch
-    S, R, C = 101, 2, 1024
+    S, C = 101, 1024
     X = pilots(dev, C - 1, seed=F)
     iq = ofdm.synth_frames(F, S, R, C, X, seed=F, noise_std=0.01)
     out = ofdm.c64((F, S - 1, C - 1), dev)
