@@ -195,9 +195,10 @@ __device__ __forceinline__ void hlds_rows(const float2 *sym, int Cp, int R, cons
         // the last row is peeled so that the prefetch is unconditional: the
         // wait for the Hc word before the exchange is then vmcnt(16), not 0
         for (int r = 0; r + 1 < R; ++r)
-            hlds_row_pf<true>(sym + (long long)(r + 1) * Cp, Hf + (long long)r * (C / 2), t, a, T, tw1,
+            hlds_row_pf<true>(sym + (long long)(r + 1) * Cp, Hf + (long long)r * (C / 2), lane_here(), a, T, tw1,
                                    tw2, lo, hi, mine, acc);
-        hlds_row_pf<false>(sym, Hf + (long long)(R - 1) * (C / 2), t, a, T, tw1, tw2, lo, hi, mine, acc);
+        hlds_row_pf<false>(sym, Hf + (long long)(R - 1) * (C / 2), lane_here(), a, T, tw1, tw2, lo, hi, mine,
+                           acc);
     } else {
         for (int r = 0; r < R; ++r) {
             float2 a[16], x[16], h[16];
@@ -354,9 +355,10 @@ __device__ __forceinline__ void hlds_ls_frame(const float2 *__restrict__ iq, int
     for (int k = 0; k < 16; ++k) p[k] = 0.f;
     for (int r = w; r < R; r += WAVES) {
         float2 a[16], x[16];
-        row_load<true>(pilot + (long long)r * Cp, t, a);
-        row_fft_a(a, t, T, tw1);
-        row_fft_b(t, T, tw2, x);
+        const int tl = lane_here();
+        row_load<true>(pilot + (long long)r * Cp, tl, a);
+        row_fft_a(a, tl, T, tw1);
+        row_fft_b(tl, T, tw2, x);
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             float2 h = ls_conj(x[k], xp[k]);  // divideOneRow + conj (cpuLS.hpp:233-244)
@@ -366,7 +368,7 @@ __device__ __forceinline__ void hlds_ls_frame(const float2 *__restrict__ iq, int
         }
         // hc_store's layout, write-through (sc1): visible at agent scope once vmcnt drains
 #pragma unroll
-        for (int i = 0; i < 8; ++i) store16_wt(Hf, R * C * 8, (r * (C / 2) + i * 64 + t) * 16, x[2 * i], x[2 * i + 1]);
+        for (int i = 0; i < 8; ++i) store16_wt(Hf, R * C * 8, (r * (C / 2) + i * 64 + tl) * 16, x[2 * i], x[2 * i + 1]);
         if (r == w) {
             OFDM_DIAG_MARKP(mx, 1)
         }
@@ -472,6 +474,12 @@ k_demod_td1024(const float2 *__restrict__ iq, int S, int R, int prefix, const fl
     // kept in SGPRs
     auto first_frame = [&](long long lb) { return (lb * HW) / (S - 1); };
     auto last_frame = [&](long long lb) { return ((lb * HW + HW - 1 < nq ? lb * HW + HW - 1 : nq - 1)) / (S - 1); };
+    const int nsym = S - 1, Cp = C + prefix;
+    // this wave's symbol of logical block lb (the last one for tail waves)
+    auto sym_of = [&](long long lb) {
+        const long long qw = lb * HW + w, q = qw < nq ? qw : nq - 1;
+        return iq + ((q / nsym) * S + 1 + q % nsym) * (long long)R * Cp + prefix;
+    };
     long long e0 = 1, e1 = 0, lb = 0;
     int um = 0;  // unit mode: 0 the whole block, 1 / 2 its first / second four symbols, rows split over waves
     if (estimator) {
@@ -486,12 +494,16 @@ k_demod_td1024(const float2 *__restrict__ iq, int S, int R, int prefix, const fl
         if (lb < 0) return;  // every block taken
         um = (int)(lb & 3);
         lb >>= 2;
+        // row 0 of the wave's symbol into its transpose image by LDS-DMA, in
+        // flight through the table fill and the estimate wait
+        if (!um) row0_dma(sym_of(lb), t, T);
         fill(tw1, tw2);
         // wait for the estimates of frames f0 .. fl (hfree, not used before
         // the rows, carries the outcome); not published in time: estimate
         // here (identical bytes) and read them back behind an acquire of our own
         const long long f0 = first_frame(lb), fl = last_frame(lb);
         if (!consume_flags(flags, f0, fl, epoch, spin_ticks, reinterpret_cast<int *>(hfree))) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // row 0's DMA landed before the images are reused
             __syncthreads();
             e0 = f0;
             e1 = fl;
@@ -505,10 +517,12 @@ k_demod_td1024(const float2 *__restrict__ iq, int S, int R, int prefix, const fl
         OFDM_DIAG_END_SLOT(td1024, epoch);
         return;
     }
-    if (e0 <= e1) acquire_all();
+    if (e0 <= e1) {
+        acquire_all();
+        if (!um) row0_dma(sym_of(lb), t, T);  // the estimate used the images: row 0 again
+    }
     OFDM_DIAG_MARK()
 
-    const int nsym = S - 1;
     if (um) {  // a half unit of the schedule's tail (launch_demod_td1024)
         split_unit(iq, S, R, prefix, Hc, P, out, nq, lb * HW + 4 * (um - 1), w, t, T, T0, tw1, tw2);
         OFDM_DIAG_END_SLOT(td1024, epoch);
@@ -519,17 +533,15 @@ k_demod_td1024(const float2 *__restrict__ iq, int S, int R, int prefix, const fl
     const long long q = store ? qw : nq - 1;
     const long long f = q / nsym;
     const long long f0 = first_frame(lb), fl = last_frame(lb);
-    const int s = 1 + (int)(q % nsym);
-    const int Cp = C + prefix;
-    const float2 *sym = iq + (f * S + s) * (long long)R * Cp + prefix;
+    const float2 *sym = sym_of(lb);
     float2 acc[16];
     if (f0 == fl)
-        hlds_rows<true, false>(sym, Cp, R, reinterpret_cast<const float4 *>(Hc + f0 * (long long)R * C), t, T,
-                               tw1, tw2, T0, hfree, acc);
+        hlds_rows<true, true>(sym, Cp, R, reinterpret_cast<const float4 *>(Hc + f0 * (long long)R * C), t, T,
+                              tw1, tw2, T0, hfree, acc);
     else
-        hlds_rows<false, false>(sym, Cp, R, reinterpret_cast<const float4 *>(Hc + f * (long long)R * C), t, T,
-                                tw1, tw2, T0, hfree, acc);
-    if (store) hlds_epilogue(acc, P, f, q, t, T, out, 0);
+        hlds_rows<false, true>(sym, Cp, R, reinterpret_cast<const float4 *>(Hc + f * (long long)R * C), t, T,
+                               tw1, tw2, T0, hfree, acc);
+    if (store) hlds_epilogue(acc, P, f, q, lane_here(), T, out, 0);
     OFDM_DIAG_END_SLOT(td1024, epoch);
 }
 
@@ -572,7 +584,8 @@ hipError_t launch_mrc_td1024(const float2 *iq, long long nframes, int S, int R, 
     // R0: each wave's row 0 DMA'd into its transpose image ahead of the table
     // fill (same process, bit-identical: R=16 x 100 frames 0.301 -> 0.293 ms,
     // R=64 x 400 3.961 -> 3.922; profiles/r3/r3p_row0_dma_ab.jsonl).  The
-    // one-launch kernel loses with it (+3-5 %) and keeps the register load.
+    // one-launch kernel takes it too since round 6, once its receivers ran
+    // without scratch (profiles/r6/r6m2_*).
     auto kern = k_mrc_td1024_hlds<true>;
     hipLaunchKernelGGL(kern, dim3((unsigned)(pxcd * 8)), dim3(64 * hlds::WAVES), hlds::LDS_BYTES, s, iq, S, R,
                        prefix, Hc, P, out, nq, nb, pxcd, mode);
