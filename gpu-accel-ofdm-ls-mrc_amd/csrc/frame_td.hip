@@ -485,6 +485,11 @@ k_demod_td1024(const float2 *__restrict__ iq, int S, int R, int prefix, const fl
     if (estimator) {
         e0 = e1 = blockIdx.x;
         if (e0 >= nframes) return;
+        // the estimates are the first round's critical path: the estimator
+        // waves issue ahead of receiver waves on the same SIMDs (same process,
+        // configs[1] 0.295 -> 0.292 ms on one box, equal on another;
+        // profiles/r6/r6s_*, r6t_*)
+        __builtin_amdgcn_s_setprio(3);
         fill(tw1, tw2);
         __syncthreads();
         OFDM_DIAG_MARKN(0)
@@ -495,9 +500,11 @@ k_demod_td1024(const float2 *__restrict__ iq, int S, int R, int prefix, const fl
         um = (int)(lb & 3);
         lb >>= 2;
         // row 0 of the wave's symbol into its transpose image by LDS-DMA, in
-        // flight through the table fill and the estimate wait
-        if (!um) row0_dma(sym_of(lb), t, T);
+        // flight through the estimate wait; issued after the table fill, whose
+        // loads would otherwise queue behind it (0.294 -> 0.292-0.293 ms,
+        // profiles/r6/r6t_*)
         fill(tw1, tw2);
+        if (!um) row0_dma(sym_of(lb), t, T);
         // wait for the estimates of frames f0 .. fl (hfree, not used before
         // the rows, carries the outcome); not published in time: estimate
         // here (identical bytes) and read them back behind an acquire of our own

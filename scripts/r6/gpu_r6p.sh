@@ -1,0 +1,14 @@
+# round 6 (p): estimators DMA their first pilot row before the table fill (ahead of the receivers' row 0):
+# prod = split estimator + that, e1 = one estimator per frame + that, pre = HEAD; one-launch tests, A/B at
+# configs[1] and the headline, stamps of prod at configs[1]
+set -o pipefail
+cd ${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=gpurun_out/r6p; mkdir -p $OUT
+timeout -k 10 600 python -u -m pytest tests/test_demod_onelaunch_gpu.py tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -30 $OUT/pytest.log; exit 1; }
+tail -2 $OUT/pytest.log
+timeout -k 10 300 python -u scripts/abx.py --C 1024 --R 16 --frames 100 --reps 11 --launches 20 --stage demod prod e1 pre > $OUT/ab_cfg1.jsonl 2> $OUT/ab_cfg1.err || { tail $OUT/ab_cfg1.err; exit 1; }
+tail -4 $OUT/ab_cfg1.jsonl
+timeout -k 10 300 python -u scripts/abx.py --C 1024 --R 64 --frames 1250 --reps 5 --launches 5 --stage demod prod pre > $OUT/ab_head.jsonl 2> $OUT/ab_head.err || { tail $OUT/ab_head.err; exit 1; }
+tail -3 $OUT/ab_head.jsonl
+timeout -k 10 300 python -u bench.py --R 16 --frames 100 --steps 200 --warmup 50 --no-cpu --stamps-out $OUT/stamps_cfg1.npy > $OUT/cfg1.json 2> $OUT/cfg1.err || { tail $OUT/cfg1.err; exit 1; }
+python3 scripts/est_phases.py $OUT/stamps_cfg1.npy 200 > $OUT/phases.txt && cat $OUT/phases.txt

@@ -1,0 +1,16 @@
+# round 6 (t): prod = HEAD + estimator waves at s_setprio 3; dafter = prod with the receivers' row-0 DMA after
+# the table fill; ddelay = prod with the first round's row-0 DMA 4 us after the fill; pre = HEAD.
+# One-launch tests, A/B at configs[1] (twice) and the headline, stamps of prod at configs[1]
+set -o pipefail
+cd ${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=gpurun_out/r6t; mkdir -p $OUT
+timeout -k 10 600 python -u -m pytest tests/test_demod_onelaunch_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -30 $OUT/pytest.log; exit 1; }
+tail -2 $OUT/pytest.log
+timeout -k 10 300 python -u scripts/abx.py --C 1024 --R 16 --frames 100 --reps 11 --launches 20 --stage demod prod dafter ddelay pre > $OUT/ab_cfg1.jsonl 2> $OUT/ab_cfg1.err || { tail $OUT/ab_cfg1.err; exit 1; }
+tail -4 $OUT/ab_cfg1.jsonl
+timeout -k 10 300 python -u scripts/abx.py --C 1024 --R 16 --frames 100 --reps 11 --launches 20 --stage demod pre ddelay dafter prod > $OUT/ab_cfg1b.jsonl 2> $OUT/ab_cfg1b.err || { tail $OUT/ab_cfg1b.err; exit 1; }
+tail -4 $OUT/ab_cfg1b.jsonl
+timeout -k 10 300 python -u scripts/abx.py --C 1024 --R 64 --frames 1250 --reps 5 --launches 5 --stage demod prod dafter pre > $OUT/ab_head.jsonl 2> $OUT/ab_head.err || { tail $OUT/ab_head.err; exit 1; }
+tail -3 $OUT/ab_head.jsonl
+timeout -k 10 300 python -u bench.py --R 16 --frames 100 --steps 200 --warmup 50 --no-cpu --stamps-out $OUT/stamps_cfg1.npy > $OUT/cfg1.json 2> $OUT/cfg1.err || { tail $OUT/cfg1.err; exit 1; }
+python3 scripts/est_phases.py $OUT/stamps_cfg1.npy 104 > $OUT/phases.txt && cat $OUT/phases.txt
