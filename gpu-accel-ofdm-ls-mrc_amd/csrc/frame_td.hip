@@ -494,22 +494,31 @@ k_demod_td1024(const float2 *__restrict__ iq, int S, int R, int prefix, const fl
         __syncthreads();
         OFDM_DIAG_MARKN(0)
     } else {
+        // the table loads first: in flight through the work ticket
+        FillRegs fr;
+        fill_load(fr);
         lb = wg_take_unit(tk, nblocks, k0, (long long)blockIdx.x - nls, split,
                           reinterpret_cast<long long *>(hfree + 255));
         if (lb < 0) return;  // every block taken
+        OFDM_DIAG_MARKN(0)
         um = (int)(lb & 3);
         lb >>= 2;
-        // row 0 of the wave's symbol into its transpose image by LDS-DMA, in
-        // flight through the estimate wait; issued after the table fill, whose
-        // loads would otherwise queue behind it (0.294 -> 0.292-0.293 ms,
-        // profiles/r6/r6t_*)
-        fill(tw1, tw2);
+        fill_store(tw1, tw2, fr);
+        // then row 0 of the wave's symbol into its transpose image by LDS-DMA
+        // and a first look at the estimate flags, in flight together: a
+        // block's start costs about two memory round trips (ticket, then
+        // DMA / flags), not four
+        const long long f0 = first_frame(lb), fl = last_frame(lb);
         if (!um) row0_dma(sym_of(lb), t, T);
+        bool seen_before = false;
+        if (threadIdx.x == 0)
+            seen_before = __hip_atomic_load((gu64 *)(flags + f0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch &&
+                          __hip_atomic_load((gu64 *)(flags + fl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+        OFDM_DIAG_MARKN(1)
         // wait for the estimates of frames f0 .. fl (hfree, not used before
         // the rows, carries the outcome); not published in time: estimate
         // here (identical bytes) and read them back behind an acquire of our own
-        const long long f0 = first_frame(lb), fl = last_frame(lb);
-        if (!consume_flags(flags, f0, fl, epoch, spin_ticks, reinterpret_cast<int *>(hfree))) {
+        if (!consume_flags(flags, f0, fl, epoch, spin_ticks, reinterpret_cast<int *>(hfree), seen_before)) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // row 0's DMA landed before the images are reused
             __syncthreads();
             e0 = f0;
@@ -548,6 +557,7 @@ k_demod_td1024(const float2 *__restrict__ iq, int S, int R, int prefix, const fl
     else
         hlds_rows<false, true>(sym, Cp, R, reinterpret_cast<const float4 *>(Hc + f * (long long)R * C), t, T,
                                tw1, tw2, T0, hfree, acc);
+    OFDM_DIAG_MARKN(2)
     if (store) hlds_epilogue(acc, P, f, q, lane_here(), T, out, 0);
     OFDM_DIAG_END_SLOT(td1024, epoch);
 }

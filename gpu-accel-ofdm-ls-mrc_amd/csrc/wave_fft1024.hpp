@@ -275,11 +275,14 @@ __device__ __forceinline__ bool wait_flag(unsigned long long *flag, unsigned lon
 // acquires; returns whether they were seen (false: the bounded wait expired
 // -- the caller estimates the frames itself, then calls acquire_all()).
 // seen: an LDS word no other code touches before the caller's next barrier.
+// seen_before: thread 0 already read every flag at epoch (an early look).
 __device__ __forceinline__ bool consume_flags(unsigned long long *flags, long long f0, long long fl,
-                                              unsigned long long epoch, long long ticks, int *seen) {
+                                              unsigned long long epoch, long long ticks, int *seen,
+                                              bool seen_before = false) {
     if (threadIdx.x == 0) {
         bool ok = true;
-        for (long long f = f0; f <= fl && ok; ++f) ok = wait_flag(flags + f, epoch, ticks);
+        if (!seen_before)
+            for (long long f = f0; f <= fl && ok; ++f) ok = wait_flag(flags + f, epoch, ticks);
         *seen = ok ? 1 : 0;
         if (ok) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -479,6 +482,30 @@ __device__ __forceinline__ void fill(float2 *tw1, float2 *tw2) {
         tw2[i] = float2{g * w.x, g * w.y};
     }
 }
+// fill() in two halves for 512-thread workgroups: fill_load issues this
+// thread's (at most 3) table loads, fill_store writes the same values fill()
+// does -- the loads' latency overlaps whatever the caller puts between (the
+// receivers' work ticket).
+struct FillRegs {
+    float2 v[3];
+};
+__device__ __forceinline__ void fill_load(FillRegs &f) {
+    const int i0 = threadIdx.x, i1 = threadIdx.x + 512;
+    auto w1 = [](int i) { return g_tw[(((i % 64) * (1 + i / 64)) & (C - 1)) * (OFDM_TW_N / C)]; };
+    f.v[0] = w1(i0);
+    f.v[1] = i1 < TW1S ? w1(i1) : float2{0.f, 0.f};
+    f.v[2] = i0 < TW2S ? g_tw[((16 * (i0 % 4) * (i0 / 4)) & (C - 1)) * (OFDM_TW_N / C)] : float2{0.f, 0.f};
+}
+__device__ __forceinline__ void fill_store(float2 *tw1, float2 *tw2, const FillRegs &f) {
+    const int i0 = threadIdx.x, i1 = threadIdx.x + 512;
+    tw1[i0] = f.v[0];
+    if (i1 < TW1S) tw1[i1] = f.v[1];
+    if (i0 < TW2S) {
+        const float g = quad_g(i0 % 4);
+        tw2[i0] = float2{g * f.v[2].x, g * f.v[2].y};
+    }
+}
+static_assert(TW1S <= 1024 && TW2S <= 512, "fill_load covers the tables with 512 threads");
 // index of (row, col) in a transpose image
 __device__ __forceinline__ int swz(int row, int col) { return row * TP + col; }
 
