@@ -6,6 +6,7 @@
 #   suite      pytest -m gpu (the driver's form)          smoke    __graft_entry__.smoke()
 #   default    bench.py (driver form: 20 steps, 3 warm-up, CPU baseline) + stamps
 #   cfg1       configs[1]: --R 16 --frames 100 --steps 20 --warmup 5 + stamps
+#   cfg1_200   configs[1] at a steady clock: 200 steps after 50 warm-up steps
 #   cfg2       configs[2]: --R 64 --C 2048 --frames 1000 --steps 10
 #   c4096      configs[4] per-GPU slice: --R 32 --C 4096 --frames 400 --steps 20 + stamps
 #   split      bench.py --mode split (RCCL, world 1) with stages_ms
@@ -29,6 +30,7 @@ for st in "$@"; do
            rc=$?; echo "smoke rc=$rc"; tail -2 $OUT/smoke.log ;;
     default) bench default 600 --gpus 1 --steps 20 --warmup 5 --stamps-out $OUT/stamps_default.npy; rc=$? ;;
     cfg1) bench cfg1 300 --R 16 --frames 100 --steps 20 --warmup 5 --no-cpu --stamps-out $OUT/stamps_cfg1.npy; rc=$? ;;
+    cfg1_200) bench cfg1_200 300 --R 16 --frames 100 --steps 200 --warmup 50 --no-cpu; rc=$? ;;
     cfg2) bench cfg2 300 --R 64 --C 2048 --frames 1000 --steps 10 --no-cpu --stamps-out $OUT/stamps_cfg2.npy; rc=$? ;;
     c4096) bench c4096 300 --R 32 --C 4096 --frames 400 --steps 20 --no-cpu --stamps-out $OUT/stamps_c4096.npy; rc=$? ;;
     split) bench split 300 --mode split --no-cpu; rc=$? ;;
