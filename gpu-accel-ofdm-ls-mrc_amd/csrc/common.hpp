@@ -26,6 +26,15 @@ __device__ __forceinline__ constexpr float2 tw_const() {
     return float2{kTw.v[2 * idx], kTw.v[2 * idx + 1]};
 }
 
+// The lane index recomputed where it is used (volatile: never merged with
+// threadIdx.x nor hoisted), so that the lane and its derived values need not
+// stay live (spilled to scratch) across a loop that does not use them.
+__device__ __forceinline__ int lane_here() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return {a.x + b.x, a.y + b.y}; }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return {a.x - b.x, a.y - b.y}; }
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {

@@ -321,9 +321,13 @@ k_mrc_td3072(const float2 *__restrict__ iq, long long nframes, int S, int R, int
         }
         float2 *o = out + q * K;
         const float *Pf = P + f * C;
+        // the lane recomputed here: output offsets hoisted out of the symbol
+        // loop were spilled and reloaded behind a vmcnt(0) that drained the
+        // next symbol's row load
+        const int Le = lane_here();
 #pragma unroll
         for (int i = 0; i < 24; ++i) {
-            const int b = bin_of(e, L, i);
+            const int b = bin_of(e, Le, i);
             if (b == 0) continue;
             const float2 a = pk::F(acc[i]);
             if (mode == 0) {
@@ -478,9 +482,13 @@ k_mrc_td6144(const float2 *__restrict__ iq, long long nframes, int S, int R, int
         }
         float2 *o = out + q * K;
         const float *Pf = P + f * C;
+        // the lane recomputed here: output offsets hoisted out of the symbol
+        // loop were spilled and reloaded behind a vmcnt(0) that drained the
+        // next symbol's row load
+        const int Le = lane_here();
 #pragma unroll
         for (int i = 0; i < 24; ++i) {
-            const int b = bin_of(e, L, i);
+            const int b = bin_of(e, Le, i);
             if (b == 0) continue;
             const float2 a = pk::F(acc[i]);
             if (mode == 0) {

@@ -43,15 +43,6 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-// The lane index recomputed where it is used (volatile: never merged with
-// threadIdx.x), so that the lane and its derived values need not stay live
-// (spilled to scratch) across a row loop that does not use them.
-__device__ __forceinline__ int lane_here() {
-    int l;
-    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
-    return l;
-}
-
 typedef __attribute__((address_space(3))) void lvoid_t;
 __device__ __forceinline__ unsigned lds_addr(const void *p) { return (unsigned)(size_t)(lvoid_t *)p; }
 
