@@ -38,6 +38,14 @@
 namespace ofdm {
 namespace fany {
 
+// threadIdx.x through a volatile copy: index math derived from it is formed
+// where it is used, not hoisted out of the symbol loop (where it was spilled)
+__device__ __forceinline__ unsigned tid_here() {
+    unsigned r;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"((unsigned)threadIdx.x));
+    return r;
+}
+
 constexpr int MAX_STAGES = 16;
 constexpr int TLO = 64;          // low twiddle table: W_C^j, j < 64
 constexpr int THI = 8192 / TLO;  // high table: W_C^{64 k}, k < C / 64
@@ -141,7 +149,7 @@ __device__ __forceinline__ void stage_small(const float2 *src, float2 *dst, cons
     float2 r[P];
 #pragma unroll
     for (int j = 0; j < P; ++j) r[j] = (P == 3 || P == 5 || P == 7) ? twv<INV>(T, j * cp) : float2{1.f, 0.f};
-    for (unsigned bb = threadIdx.x; bb < nb; bb += NT) {
+    for (unsigned bb = tid_here(); bb < nb; bb += NT) {
         const unsigned g = fdiv(bb, st.cp), b = bb - g * cp, m = fdiv(b, st.Lp), k1 = b - m * Lp;
         const unsigned s0 = g * C + b;
         float2 a[P];
@@ -160,7 +168,7 @@ template <int NT, bool INV>
 __device__ __forceinline__ void stage_any(const float2 *src, float2 *dst, const Tw &T, unsigned C, unsigned G,
                                           unsigned Lp, unsigned p, const Stage &st, FDiv dC) {
     const unsigned L = Lp * p, cp = C / p, M = C / L, n = G * C;
-    for (unsigned o = threadIdx.x; o < n; o += NT) {
+    for (unsigned o = tid_here(); o < n; o += NT) {
         const unsigned g = fdiv(o, dC), pos = o - g * C, m = fdiv(pos, st.L), k = pos - m * L;
         const unsigned k1 = k - fdiv(k, st.Lp) * Lp;
         const unsigned s0 = g * C + m * Lp + k1;
@@ -226,7 +234,7 @@ __device__ __forceinline__ void load_rows(float2 (&pf)[MAXE], const float2 *__re
     const unsigned ne = n * C;
 #pragma unroll
     for (int i = 0; i < MAXE; ++i) {
-        const unsigned e = threadIdx.x + i * NT;
+        const unsigned e = tid_here() + i * NT;
         pf[i] = float2{0.f, 0.f};
         if (e < ne) {
             const unsigned g = fdiv(e, dC);
@@ -245,7 +253,7 @@ __device__ __forceinline__ void load_rows_b(float2 (&pf)[MAXE], const float2 *__
     const unsigned ne = n * C;
 #pragma unroll
     for (int i = 0; i < MAXE; ++i) {
-        const unsigned e = threadIdx.x + i * NT;
+        const unsigned e = tid_here() + i * NT;
         pf[i] = float2{0.f, 0.f};
         if (e < ne) {
             const unsigned g = fdiv(e, dC);
@@ -273,13 +281,13 @@ k_fft_any(const float2 *__restrict__ in, long long in_stride, long long in_rb, l
     for (; grp < ngroups; grp += gridDim.x) {
         const unsigned n = rows_of(grp);
 #pragma unroll
-        for (int i = 0; i < MAXE; ++i) x0[threadIdx.x + i * NT] = pf[i];
+        for (int i = 0; i < MAXE; ++i) x0[tid_here() + i * NT] = pf[i];
         lds_sync();
         const long long nxt = grp + gridDim.x;
         if (nxt < ngroups) load_rows_b<NT, MAXE>(pf, in, nxt * G, in_stride, in_rb, in_bstride, C, plan.dC, rows_of(nxt));
         const float2 *res = run_stages<NT, INV>(x0, x1, T, plan, n, plan.ns);
         float2 *dst = out + grp * G * out_stride + out_off;
-        for (unsigned e = threadIdx.x; e < n * C; e += NT) {
+        for (unsigned e = tid_here(); e < n * C; e += NT) {
             const unsigned g = fdiv(e, plan.dC);
             const float2 v = res[e];
             dst[g * out_stride + (e - g * C)] = float2{v.x * scale, v.y * scale};
@@ -305,7 +313,7 @@ __device__ __forceinline__ void last_mac(const float2 *src, const Tw &T, unsigne
     for (int j = 0; j < P; ++j) r[j] = (P == 3 || P == 5 || P == 7) ? twv<false>(T, j * cp) : float2{1.f, 0.f};
 #pragma unroll
     for (int j = 0; j < MAXJ; ++j) {
-        const unsigned k1 = threadIdx.x + j * NT;
+        const unsigned k1 = tid_here() + j * NT;
         if (k1 < cp) {
             for (unsigned g = 0; g < n; ++g) {
                 float2 a[P], h[P];
@@ -335,7 +343,7 @@ __device__ __forceinline__ void last_mac_any(const float2 *src, const Tw &T, uns
     const unsigned cp = C / p;
 #pragma unroll
     for (int j = 0; j < NACC; ++j) {
-        const unsigned o = threadIdx.x + j * NT;
+        const unsigned o = tid_here() + j * NT;
         if (o < C) {
             const unsigned k1 = o % cp;
             for (unsigned g = 0; g < n; ++g) {
@@ -360,9 +368,9 @@ __device__ __forceinline__ void last_mac_any(const float2 *src, const Tw &T, uns
 template <int P, int NT>
 __device__ __forceinline__ unsigned acc_bin(int i, unsigned C) {
     if constexpr (P == 0) {
-        return threadIdx.x + i * NT;
+        return tid_here() + i * NT;
     } else {
-        const unsigned cp = C / P, k1 = threadIdx.x + (i / P) * NT;
+        const unsigned cp = C / P, k1 = tid_here() + (i / P) * NT;
         return k1 < cp ? k1 + cp * (i % P) : ~0u;
     }
 }
@@ -424,7 +432,7 @@ k_mrc_any(const float2 *__restrict__ iq, long long nframes, int S, int R, int pr
     while (q < nq) {
         const unsigned n = rows_in(gi);
 #pragma unroll
-        for (int i = 0; i < MAXE; ++i) x0[threadIdx.x + i * NT] = pf[i];
+        for (int i = 0; i < MAXE; ++i) x0[tid_here() + i * NT] = pf[i];
         lds_sync();
         long long qn = q, fn = f;
         int sn = s, gn = gi + 1;
