@@ -622,10 +622,15 @@ hipError_t launch_demod_td1024(const float2 *iq, long long nframes, int S, int R
     if (nq <= 0) return hipSuccess;
     const long long nb = (nq + hlds::WAVES - 1) / hlds::WAVES;
     const long long nls = (nframes + 7) / 8 * 8;
-    // the schedule's tail in half units: the last k0 blocks of every XCD
-    // range (k0 = the XCD's resident workgroups) -- the last rounds end on
+    // the first TWO rounds static (k0 = twice the XCD's resident workgroups
+    // per XCD range: a second-round unit costs no ticket round trip before
+    // its row 0 and flags are in flight; configs[1] 0.292 -> 0.280 ms, R = 64
+    // x 100 frames 1.043 -> 1.008 ms, larger batches equal; 1.5 / 3 static
+    // rounds 0.288 / 0.286 ms: profiles/r6/r6ag_*, r6ah_*), then work tickets
+    // with the schedule's tail in half units: the last k1 blocks of every
+    // XCD range (k1 = the XCD's resident workgroups) -- the last rounds end on
     // units of about half a block's time (R >= 2)
-    const long long k0 = ticket_k0(2), split = R >= 2 ? k0 : 0;
+    const long long k1 = ticket_k0(2), k0 = 2 * k1, split = R >= 2 ? k1 : 0;
     const long long g = ticket_grid(nb, 8 * split);
     if (g + nls > 0x7fffffffll) return hipErrorInvalidValue;
     hipLaunchKernelGGL(k_demod_td1024, dim3((unsigned)(nls + g)), dim3(64 * hlds::WAVES), hlds::LDS_BYTES, s, iq,

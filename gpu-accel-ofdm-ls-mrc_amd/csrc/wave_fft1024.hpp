@@ -303,8 +303,9 @@ __device__ __forceinline__ void acquire_all() {
 // C = 4096, at equal clocks -- a memory-side difference).  The blocks are
 // cut into 8 contiguous ranges, one per XCD (a frame's consecutive blocks
 // keep sharing one L2).  The first k0 blocks of range y go statically to
-// the workgroups with (index & 7) == y, (index >> 3) < k0 -- the first round,
-// which would otherwise queue on the counters all at once; every later block
+// the workgroups with (index & 7) == y, (index >> 3) < k0 -- the first round
+// (k_demod_td1024: the first two), which would otherwise queue on the
+// counters all at once; every later block
 // is a ticket: a workgroup takes the next one of its own XCD's range (the
 // XCC_ID register; speed only) and, once that range is exhausted, of the
 // other ranges in turn (one atomic add per block taken).  The grid is
@@ -371,7 +372,7 @@ __device__ __forceinline__ long long take_ticket(const Tickets &tk, unsigned y, 
 __device__ __forceinline__ long long take_unit(const Tickets &tk, long long nb, long long k0, long long pb,
                                                long long split) {
     const long long per = (nb + 7) / 8;
-    if (pb < 8 * k0) {  // the static first round
+    if (pb < 8 * k0) {  // the static first round(s)
         const unsigned y = (unsigned)(pb & 7);
         const long long k = pb >> 3, cnt = ticket_range_count(nb, per, y);
         if (k < (cnt < k0 ? cnt : k0)) return ((long long)y * per + k) << 2;
