@@ -285,19 +285,33 @@ hipError_t launch_mrc_freq(const float2 *Y, long long frame_stride, long long sy
     return hipGetLastError();
 }
 
+// Element e = q K + j of [e0, e0 + count): out[q][out_pos(j)] = num / P[f][j].
+// Grid-stride; the (symbol, subcarrier) pair is carried from one stride to
+// the next and the frame formed by a 32-bit division, so that the loop holds
+// none of the three 64-bit divisions per element it had (VALU-bound at
+// 4.2 TB/s).
 __global__ void __launch_bounds__(256) k_mrc_finalize(const float2 *__restrict__ num, long long e0,
                                                       long long count, int nsym, int K,
                                                       const float *__restrict__ P,
                                                       float2 *__restrict__ out) {
     const long long stride = (long long)gridDim.x * blockDim.x;
-    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) {
-        const long long e = e0 + i;
-        const long long q = e / K;
-        const int j = (int)(e % K);
-        const long long f = q / nsym;
+    long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    long long q = (e0 + i) / K;
+    int j = (int)(e0 + i - q * K);
+    const long long dq = stride / K;
+    const int dj = (int)(stride - dq * K);
+    for (; i < count; i += stride) {
+        const long long f = q < 0x100000000ll ? (long long)((unsigned)q / (unsigned)nsym) : q / nsym;
         const float p = P[f * K + j];
         const float2 v = num[i];
         out[q * K + out_pos_any(j, K)] = float2{v.x / p, v.y / p};
+        q += dq;
+        j += dj;
+        if (j >= K) {
+            j -= K;
+            ++q;
+        }
     }
 }
 
