@@ -141,14 +141,22 @@ __global__ void __launch_bounds__(256) k_pn_extract(const float2 *__restrict__ b
     const long long p = *pos;
     if (p < 0) return;  // no hit: nothing to extract
     const long long lag = p % nl, head = N - lag - L;
-    for (long long e = blockIdx.x * 256ll + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
-        const int k = (int)(e % C);
-        const long long r = e / C;
-        const int ch = (int)(r % R);
-        const long long s = r / R;
+    // element e = (s R + ch) C + k: sample cp + k of symbol s on channel ch
+    auto put = [&](long long e, int k, int ch, long long s) {
         const long long q = s * (C + cp) + cp + k;
         const long long base = (long long)ch * N;
         sym[e] = q < head ? buf1[base + lag + L + q] : buf2[base + q - head];
+    };
+    if (total < 0x80000000ll) {  // 32-bit index math (a frame is far below 2^31 elements)
+        for (unsigned e = blockIdx.x * 256u + threadIdx.x; e < (unsigned)total; e += gridDim.x * 256u) {
+            const unsigned r = e / (unsigned)C, s = r / (unsigned)R;
+            put(e, (int)(e - r * (unsigned)C), (int)(r - s * (unsigned)R), s);
+        }
+        return;
+    }
+    for (long long e = blockIdx.x * 256ll + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+        const long long r = e / C, s = r / R;
+        put(e, (int)(e - r * C), (int)(r - s * R), s);
     }
 }
 
