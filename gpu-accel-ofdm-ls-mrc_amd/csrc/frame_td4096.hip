@@ -426,8 +426,11 @@ __device__ __forceinline__ void mrc4096_block(const float2 *__restrict__ iq, int
         for (int k = 0; k < 16; ++k) {
             const int be = 4 * (b0 + 16 * k) + e;
             const float pe = Pf[be], po = Pf[be + 2];  // Pf[0] = 1: the DC slot
-            ae[k] = float2{ae[k].x / pe, ae[k].y / pe};
-            ao[k] = float2{ao[k].x / po, ao[k].y / po};
+            // one reciprocal (v_rcp_f32) and two products per bin instead of
+            // two IEEE divisions (within 2 ulp; frame_td.hip hlds_epilogue)
+            const float re = __builtin_amdgcn_rcpf(pe), ro = __builtin_amdgcn_rcpf(po);
+            ae[k] = float2{ae[k].x * re, ae[k].y * re};
+            ao[k] = float2{ao[k].x * ro, ao[k].y * ro};
         }
     }
     float2 *Tpair = lds + X_TAB + 2 * pair * TS4;  // images of waves 2 pair, 2 pair + 1

@@ -169,7 +169,7 @@ k_mrc_td1536(const float2 *__restrict__ iq, long long nframes, int S, int R, int
             const float2 a = pk::F(acc[i]);
             if (mode == 0) {
                 const float p = Pf[b];
-                o[out_pos(b - 1, K)] = float2{a.x / p, a.y / p};
+                o[out_pos(b - 1, K)] = float2{a.x * __builtin_amdgcn_rcpf(p), a.y * __builtin_amdgcn_rcpf(p)};
             } else {
                 o[b - 1] = a;
             }
@@ -332,7 +332,7 @@ k_mrc_td3072(const float2 *__restrict__ iq, long long nframes, int S, int R, int
             const float2 a = pk::F(acc[i]);
             if (mode == 0) {
                 const float p = Pf[b];
-                o[out_pos(b - 1, K)] = float2{a.x / p, a.y / p};
+                o[out_pos(b - 1, K)] = float2{a.x * __builtin_amdgcn_rcpf(p), a.y * __builtin_amdgcn_rcpf(p)};
             } else {
                 o[b - 1] = a;
             }
@@ -493,7 +493,7 @@ k_mrc_td6144(const float2 *__restrict__ iq, long long nframes, int S, int R, int
             const float2 a = pk::F(acc[i]);
             if (mode == 0) {
                 const float p = Pf[b];
-                o[out_pos(b - 1, K)] = float2{a.x / p, a.y / p};
+                o[out_pos(b - 1, K)] = float2{a.x * __builtin_amdgcn_rcpf(p), a.y * __builtin_amdgcn_rcpf(p)};
             } else {
                 o[b - 1] = a;
             }
@@ -630,7 +630,7 @@ __device__ __forceinline__ void mrc_small(const float2 *__restrict__ iq, long lo
             const float2 a = pk::F(acc[d]);
             if (mode == 0) {
                 const float p = Pf[b];
-                o[out_pos(b - 1, K)] = float2{a.x / p, a.y / p};
+                o[out_pos(b - 1, K)] = float2{a.x * __builtin_amdgcn_rcpf(p), a.y * __builtin_amdgcn_rcpf(p)};
             } else {
                 o[b - 1] = a;
             }
