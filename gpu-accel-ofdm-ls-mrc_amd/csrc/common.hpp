@@ -171,10 +171,15 @@ __device__ __forceinline__ int out_src(int k, int K) {
 
 // LS for one subcarrier: conj(y / x) with divideOneRow's naive formula
 // (cpuLS.hpp:240-241) followed by the conjugate (303-307).
+// The two divisions by |x|^2 as one reciprocal (v_rcp_f32, 1 ulp) and two
+// products: within 2 ulp of the reference's quotients, ~18 fewer
+// instructions per bin in the estimators' rows (the first round of the
+// one-launch demod waits for them).
 __device__ __forceinline__ float2 ls_conj(float2 y, float2 x) {
     const float den = x.x * x.x + x.y * x.y;
-    const float re = (y.x * x.x + y.y * x.y) / den;
-    const float im = (y.y * x.x - y.x * x.y) / den;
+    const float rd = __builtin_amdgcn_rcpf(den);
+    const float re = (y.x * x.x + y.y * x.y) * rd;
+    const float im = (y.y * x.x - y.x * x.y) * rd;
     return {re, -1.0f * im};
 }
 
