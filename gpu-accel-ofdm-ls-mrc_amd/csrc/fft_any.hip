@@ -387,7 +387,7 @@ __device__ __forceinline__ void store_acc(float2 (&acc)[NACC], float2 *__restric
             const float2 a = acc[i];
             if (mode == 0) {
                 const float p = Pf[b];
-                o[out_pos_any((int)b - 1, (int)K)] = float2{a.x / p, a.y / p};
+                o[out_pos_any((int)b - 1, (int)K)] = float2{a.x * __builtin_amdgcn_rcpf(p), a.y * __builtin_amdgcn_rcpf(p)};
             } else {
                 o[b - 1] = a;
             }

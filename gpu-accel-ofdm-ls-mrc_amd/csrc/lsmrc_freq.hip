@@ -105,10 +105,10 @@ __global__ void __launch_bounds__(256) k_mrc_freq(const float2 *__restrict__ Y, 
         const float *Pf = P + f * p_fstride + p_jofs;
         if (m > 0) {
             const float p0 = Pf[j0];
-            o[out_pos(j0, K)] = float2{a0.x / p0, a0.y / p0};
+            o[out_pos(j0, K)] = float2{a0.x * __builtin_amdgcn_rcpf(p0), a0.y * __builtin_amdgcn_rcpf(p0)};
         }
         const float p1 = Pf[j1];
-        o[out_pos(j1, K)] = float2{a1.x / p1, a1.y / p1};
+        o[out_pos(j1, K)] = float2{a1.x * __builtin_amdgcn_rcpf(p1), a1.y * __builtin_amdgcn_rcpf(p1)};
     } else {
         if (m > 0) o[j0] = a0;
         o[j1] = a1;
@@ -139,7 +139,7 @@ __global__ void __launch_bounds__(256) k_mrc_freq1(const float2 *__restrict__ Y,
     }
     if (mode == 0) {
         const float p = P[f * p_fstride + p_jofs + j];
-        out[q * K + out_pos_any(j, K)] = float2{a.x / p, a.y / p};
+        out[q * K + out_pos_any(j, K)] = float2{a.x * __builtin_amdgcn_rcpf(p), a.y * __builtin_amdgcn_rcpf(p)};
     } else {
         out[q * K + j] = a;
     }
@@ -228,8 +228,11 @@ __global__ void __launch_bounds__(256) k_mrc_freq_frames(const float2 *__restric
         float2 *o = out + (f * nsym + s0 + g) * (long long)K;
         float2 v0 = a0[g], v1 = a1[g];
         if (mode == 0) {
-            v0 = float2{v0.x / p0, v0.y / p0};
-            v1 = float2{v1.x / p1, v1.y / p1};
+            // one reciprocal and two products per bin (within 2 ulp of the
+            // two divisions; frame_td.hip hlds_epilogue)
+            const float r0 = __builtin_amdgcn_rcpf(p0), r1 = __builtin_amdgcn_rcpf(p1);
+            v0 = float2{v0.x * r0, v0.y * r0};
+            v1 = float2{v1.x * r1, v1.y * r1};
         }
         if (m > 0)
             __builtin_nontemporal_store(__builtin_bit_cast(unsigned long long, v0),
@@ -305,7 +308,7 @@ __global__ void __launch_bounds__(256) k_mrc_finalize(const float2 *__restrict__
         const long long f = q < 0x100000000ll ? (long long)((unsigned)q / (unsigned)nsym) : q / nsym;
         const float p = P[f * K + j];
         const float2 v = num[i];
-        out[q * K + out_pos_any(j, K)] = float2{v.x / p, v.y / p};
+        out[q * K + out_pos_any(j, K)] = float2{v.x * __builtin_amdgcn_rcpf(p), v.y * __builtin_amdgcn_rcpf(p)};
         q += dq;
         j += dj;
         if (j >= K) {

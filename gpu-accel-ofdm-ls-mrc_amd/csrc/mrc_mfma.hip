@@ -120,7 +120,7 @@ __global__ void __launch_bounds__(256) k_mrc_freq_mfma(
         float2 v = *reinterpret_cast<const float2 *>(img + os * PITCH + 2 * (oj + j));
         if (mode == 0) {
             const float p = Pf[b];
-            o[out_pos(b - 1, K)] = float2{v.x / p, v.y / p};
+            o[out_pos(b - 1, K)] = float2{v.x * __builtin_amdgcn_rcpf(p), v.y * __builtin_amdgcn_rcpf(p)};
         } else {
             o[b - 1] = v;
         }
